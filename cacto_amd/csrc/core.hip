@@ -1,0 +1,88 @@
+// Error plumbing and the system handle (cacto_sys_create / destroy).
+#include <cstring>
+#include <string>
+
+#include "common.h"
+#include "env.h"
+#include "internal.h"
+
+namespace cacto {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int hip_fail(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return CACTO_EHIP;
+}
+
+}  // namespace cacto
+
+extern "C" const char* cacto_last_error(void) { return cacto::g_last_error.c_str(); }
+
+extern "C" int cacto_abi_version(void) { return CACTO_ABI_VERSION; }
+
+extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* joint_table_h, cacto_sys** out) {
+  using namespace cacto;
+  try {
+    CACTO_REQUIRE(params_h && out, "cacto_sys_create: null argument");
+    const cacto_sys_params& p = *params_h;
+    CACTO_REQUIRE(p.nb_state >= 2 && p.nb_state <= CACTO_MAX_STATE, "cacto_sys_create: nb_state out of range");
+    CACTO_REQUIRE(p.nb_action >= 1 && p.nb_action <= CACTO_MAX_ACTION, "cacto_sys_create: nb_action out of range");
+    CACTO_REQUIRE(p.nb_state <= 16 && p.nb_action <= 16, "cacto_sys_create: MLP tiles assume ns, na <= 16");
+    CACTO_REQUIRE(p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR || p.dyn_kind == CACTO_DYN_CHAIN,
+                  "cacto_sys_create: dynamics kind not implemented in this build (car / car_park)");
+    CACTO_REQUIRE(p.reward_kind == CACTO_REW_PLANAR || p.reward_kind == CACTO_REW_MANIPULATOR,
+                  "cacto_sys_create: reward kind not implemented in this build (ur5 / car_park)");
+    if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) {
+      CACTO_REQUIRE(p.nb_state == 3 && p.nb_action == 2, "single integrator needs ns = 3, na = 2");
+    }
+    if (p.dyn_kind == CACTO_DYN_CHAIN) {
+      CACTO_REQUIRE(joint_table_h != nullptr, "cacto_sys_create: chain dynamics needs a joint table");
+      CACTO_REQUIRE(p.n_joints >= 1 && p.n_joints <= CACTO_MAX_JOINTS, "cacto_sys_create: n_joints out of range");
+      CACTO_REQUIRE(p.nq == p.n_joints && p.nv == p.n_joints && p.nb_state == 2 * p.n_joints + 1 &&
+                        p.nb_action == p.n_joints,
+                    "cacto_sys_create: chain needs nq = nv = na = n_joints, ns = 2n + 1");
+      CACTO_REQUIRE(p.ee_parent >= 0 && p.ee_parent < p.n_joints, "cacto_sys_create: bad ee_parent");
+      for (int i = 0; i < p.n_joints; ++i) {
+        const int parent = (int)joint_table_h[i * CACTO_JOINT_COLS];
+        const int kind = (int)joint_table_h[i * CACTO_JOINT_COLS + 1];
+        CACTO_REQUIRE(parent >= -1 && parent < i, "cacto_sys_create: joints must be in depth-first order");
+        CACTO_REQUIRE(kind == 0 || kind == 1, "cacto_sys_create: joint type must be revolute(0)/prismatic(1)");
+      }
+    }
+    CACTO_REQUIRE(p.n_weights >= 7 && p.n_weights <= 8, "cacto_sys_create: n_weights must be 7 or 8");
+    SysDevice host{};
+    host.p = p;
+    if (joint_table_h && p.dyn_kind == CACTO_DYN_CHAIN)
+      std::memcpy(host.joints, joint_table_h, sizeof(double) * p.n_joints * CACTO_JOINT_COLS);
+    cacto_sys* s = new cacto_sys();
+    s->host = host;
+    hipError_t e = hipMalloc(&s->dev, sizeof(SysDevice));
+    if (e != hipSuccess) {
+      delete s;
+      return hip_fail(e, "hipMalloc(sys)");
+    }
+    e = hipMemcpy(s->dev, &host, sizeof(SysDevice), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(s->dev);
+      delete s;
+      return hip_fail(e, "hipMemcpy(sys)");
+    }
+    s->actor = make_topo(CACTO_NET_ACTOR, p.nb_state, p.nb_action);
+    s->critic = make_topo(CACTO_NET_CRITIC, p.nb_state, p.nb_action);
+    *out = s;
+    return CACTO_OK;
+  } catch (const std::exception& ex) {
+    set_error(std::string("cacto_sys_create: ") + ex.what());
+    return CACTO_ENOMEM;
+  }
+}
+
+extern "C" int cacto_sys_destroy(cacto_sys* sys) {
+  if (!sys) return CACTO_OK;
+  (void)hipFree(sys->dev);
+  delete sys;
+  return CACTO_OK;
+}

@@ -1,0 +1,481 @@
+// Device-side CACTO environments in float64: chain dynamics (Pinocchio computeAllTerms + solve,
+// computeABADerivatives.Minv, framePlacement), analytic single-integrator dynamics, rewards and the
+// float32 TF pieces of reward_batch. One thread evaluates one sample.
+//
+// Reference: environment.py (Env :10-163, SingleIntegrator :165-286, DoubleIntegrator :288-362,
+// Manipulator :654-734, UR5 :736-816), robot_utils.py:348-432 (RobotSimulator.step/simulate).
+#pragma once
+
+#include "common.h"
+
+namespace cacto {
+
+struct SysDevice {
+  cacto_sys_params p;
+  double joints[CACTO_MAX_JOINTS * CACTO_JOINT_COLS];
+};
+
+// ------------------------------------------------------------------ small 3-vector algebra
+struct V3 {
+  double x, y, z;
+};
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+struct M3 {
+  double m[9];  // row-major
+};
+__device__ __forceinline__ V3 mul(const M3& R, V3 v) {
+  return v3(R.m[0] * v.x + R.m[1] * v.y + R.m[2] * v.z, R.m[3] * v.x + R.m[4] * v.y + R.m[5] * v.z,
+            R.m[6] * v.x + R.m[7] * v.y + R.m[8] * v.z);
+}
+__device__ __forceinline__ V3 mulT(const M3& R, V3 v) {
+  return v3(R.m[0] * v.x + R.m[3] * v.y + R.m[6] * v.z, R.m[1] * v.x + R.m[4] * v.y + R.m[7] * v.z,
+            R.m[2] * v.x + R.m[5] * v.y + R.m[8] * v.z);
+}
+__device__ __forceinline__ M3 mul(const M3& A, const M3& B) {
+  M3 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C.m[3 * i + j] = A.m[3 * i] * B.m[j] + A.m[3 * i + 1] * B.m[3 + j] + A.m[3 * i + 2] * B.m[6 + j];
+  return C;
+}
+
+// Symmetric 3x3 stored xx, xy, xz, yy, yz, zz
+struct S3 {
+  double xx, xy, xz, yy, yz, zz;
+};
+__device__ __forceinline__ V3 mul(const S3& I, V3 w) {
+  return v3(I.xx * w.x + I.xy * w.y + I.xz * w.z, I.xy * w.x + I.yy * w.y + I.yz * w.z,
+            I.xz * w.x + I.yz * w.y + I.zz * w.z);
+}
+
+// Spatial motion / force, Pinocchio ordering (linear, angular)
+struct SV {
+  V3 l, a;
+};
+
+// Rigid-body inertia about the body origin: mass, first moment h = m*c, rotational inertia Io
+// about the origin (= Ic + m(|c|^2 1 - c c^T)). Linear under summation.
+struct Inertia {
+  double m;
+  V3 h;
+  S3 Io;
+};
+__device__ __forceinline__ SV inertia_mul(const Inertia& I, const SV& v) {
+  // f = m v - h x w ; n = Io w + h x v
+  SV f;
+  f.l = I.m * v.l - cross(I.h, v.a);
+  f.a = mul(I.Io, v.a) + cross(I.h, v.l);
+  return f;
+}
+// SE3 (R, p): placement of child frame in parent frame
+struct SE3 {
+  M3 R;
+  V3 p;
+};
+__device__ __forceinline__ SV act_motion_inv(const SE3& M, const SV& v) {  // parent -> child
+  SV o;
+  o.a = mulT(M.R, v.a);
+  o.l = mulT(M.R, v.l - cross(M.p, v.a));
+  return o;
+}
+__device__ __forceinline__ SV act_force(const SE3& M, const SV& f) {  // child -> parent
+  SV o;
+  o.l = mul(M.R, f.l);
+  o.a = mul(M.R, f.a) + cross(M.p, o.l);
+  return o;
+}
+__device__ __forceinline__ SV cross_motion(const SV& v, const SV& m) {
+  SV o;
+  o.l = cross(v.a, m.l) + cross(v.l, m.a);
+  o.a = cross(v.a, m.a);
+  return o;
+}
+__device__ __forceinline__ SV cross_force(const SV& v, const SV& f) {
+  SV o;
+  o.l = cross(v.a, f.l);
+  o.a = cross(v.a, f.a) + cross(v.l, f.l);
+  return o;
+}
+// Express a child-frame inertia in the parent frame.
+__device__ __forceinline__ Inertia act_inertia(const SE3& M, const Inertia& I) {
+  Inertia o;
+  o.m = I.m;
+  V3 hr = mul(M.R, I.h);
+  o.h = hr + I.m * M.p;
+  // R Io R^T
+  M3 A;
+  const double io[9] = {I.Io.xx, I.Io.xy, I.Io.xz, I.Io.xy, I.Io.yy, I.Io.yz, I.Io.xz, I.Io.yz, I.Io.zz};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      A.m[3 * i + j] = io[3 * i] * M.R.m[3 * j] + io[3 * i + 1] * M.R.m[3 * j + 1] + io[3 * i + 2] * M.R.m[3 * j + 2];
+  M3 RIR = mul(M.R, A);
+  const V3 p = M.p;
+  const double pp = dot(p, p), ph = 2.0 * dot(p, hr);
+  o.Io.xx = RIR.m[0] + I.m * (pp - p.x * p.x) + ph - 2.0 * p.x * hr.x;
+  o.Io.yy = RIR.m[4] + I.m * (pp - p.y * p.y) + ph - 2.0 * p.y * hr.y;
+  o.Io.zz = RIR.m[8] + I.m * (pp - p.z * p.z) + ph - 2.0 * p.z * hr.z;
+  o.Io.xy = RIR.m[1] - I.m * p.x * p.y - p.x * hr.y - hr.x * p.y;
+  o.Io.xz = RIR.m[2] - I.m * p.x * p.z - p.x * hr.z - hr.x * p.z;
+  o.Io.yz = RIR.m[5] - I.m * p.y * p.z - p.y * hr.z - hr.y * p.z;
+  return o;
+}
+__device__ __forceinline__ void add_inertia(Inertia& a, const Inertia& b) {
+  a.m += b.m;
+  a.h = a.h + b.h;
+  a.Io.xx += b.Io.xx; a.Io.xy += b.Io.xy; a.Io.xz += b.Io.xz;
+  a.Io.yy += b.Io.yy; a.Io.yz += b.Io.yz; a.Io.zz += b.Io.zz;
+}
+
+// ------------------------------------------------------------------ joint table access
+struct JointView {
+  const double* r;
+  __device__ int parent() const { return (int)r[0]; }
+  __device__ int kind() const { return (int)r[1]; }
+  __device__ V3 axis() const { return v3(r[2], r[3], r[4]); }
+  __device__ M3 R0() const {
+    M3 R;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R.m[k] = r[5 + k];
+    return R;
+  }
+  __device__ V3 p0() const { return v3(r[14], r[15], r[16]); }
+  __device__ Inertia inertia() const {
+    // stored: mass, com, Ic (about COM) -> origin form
+    Inertia I;
+    I.m = r[17];
+    V3 c = v3(r[18], r[19], r[20]);
+    I.h = I.m * c;
+    const double cc = dot(c, c);
+    I.Io.xx = r[21] + I.m * (cc - c.x * c.x);
+    I.Io.xy = r[22] - I.m * c.x * c.y;
+    I.Io.xz = r[23] - I.m * c.x * c.z;
+    I.Io.yy = r[24] + I.m * (cc - c.y * c.y);
+    I.Io.yz = r[25] - I.m * c.y * c.z;
+    I.Io.zz = r[26] + I.m * (cc - c.z * c.z);
+    return I;
+  }
+};
+
+// Joint transform; axis-aligned revolute joints use the closed form (Pinocchio JointModelR{X,Y,Z}),
+// others Rodrigues (JointModelRevoluteUnaligned).
+__device__ inline M3 joint_rotation(V3 ax, double q) {
+  double s, c;
+  sincos(q, &s, &c);
+  M3 R;
+  if (ax.x == 1.0 && ax.y == 0.0 && ax.z == 0.0) {
+    R = M3{{1, 0, 0, 0, c, -s, 0, s, c}};
+  } else if (ax.x == 0.0 && ax.y == 1.0 && ax.z == 0.0) {
+    R = M3{{c, 0, s, 0, 1, 0, -s, 0, c}};
+  } else if (ax.x == 0.0 && ax.y == 0.0 && ax.z == 1.0) {
+    R = M3{{c, -s, 0, s, c, 0, 0, 0, 1}};
+  } else {
+    const double t = 1.0 - c;
+    R = M3{{c + t * ax.x * ax.x, t * ax.x * ax.y - s * ax.z, t * ax.x * ax.z + s * ax.y,
+            t * ax.x * ax.y + s * ax.z, c + t * ax.y * ax.y, t * ax.y * ax.z - s * ax.x,
+            t * ax.x * ax.z - s * ax.y, t * ax.y * ax.z + s * ax.x, c + t * ax.z * ax.z}};
+  }
+  return R;
+}
+
+__device__ inline SE3 joint_placement(const JointView& j, double q) {
+  SE3 M;
+  const M3 R0 = j.R0();
+  if (j.kind() == 0) {
+    M.R = mul(R0, joint_rotation(j.axis(), q));
+    M.p = j.p0();
+  } else {
+    M.R = R0;
+    M.p = j.p0() + mul(R0, q * j.axis());
+  }
+  return M;
+}
+
+__device__ __forceinline__ SV joint_S(const JointView& j) {
+  SV S;
+  V3 z = v3(0, 0, 0);
+  if (j.kind() == 0) {
+    S.l = z;
+    S.a = j.axis();
+  } else {
+    S.l = j.axis();
+    S.a = z;
+  }
+  return S;
+}
+__device__ __forceinline__ double sdot(const SV& S, const SV& f) { return dot(S.l, f.l) + dot(S.a, f.a); }
+
+// M(q) via CRBA and h(q, v) via RNEA (qdd = 0, a_0 = -gravity), Featherstone / Pinocchio.
+__device__ inline void chain_terms(const SysDevice& sd, const double* q, const double* v, double* M,
+                                   double* h) {
+  const int n = sd.p.n_joints;
+  SE3 X[CACTO_MAX_JOINTS];
+  SV vel[CACTO_MAX_JOINTS], acc[CACTO_MAX_JOINTS], f[CACTO_MAX_JOINTS];
+  Inertia Ic[CACTO_MAX_JOINTS];
+  const SV gacc{v3(-sd.p.gravity[0], -sd.p.gravity[1], -sd.p.gravity[2]), v3(0, 0, 0)};
+  for (int i = 0; i < n; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    X[i] = joint_placement(j, q[i]);
+    const SV S = joint_S(j);
+    const int pa = j.parent();
+    SV vp = pa < 0 ? SV{v3(0, 0, 0), v3(0, 0, 0)} : vel[pa];
+    SV ap = pa < 0 ? gacc : acc[pa];
+    SV vi = act_motion_inv(X[i], vp);
+    SV Sq{v[i] * S.l, v[i] * S.a};
+    vi.l = vi.l + Sq.l;
+    vi.a = vi.a + Sq.a;
+    SV ai = act_motion_inv(X[i], ap);
+    SV c = cross_motion(vi, Sq);
+    ai.l = ai.l + c.l;
+    ai.a = ai.a + c.a;
+    vel[i] = vi;
+    acc[i] = ai;
+    Ic[i] = j.inertia();
+    SV Iv = inertia_mul(Ic[i], vi);
+    SV Ia = inertia_mul(Ic[i], ai);
+    SV vf = cross_force(vi, Iv);
+    f[i].l = Ia.l + vf.l;
+    f[i].a = Ia.a + vf.a;
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    h[i] = sdot(joint_S(j), f[i]);
+    const int pa = j.parent();
+    if (pa >= 0) {
+      SV fp = act_force(X[i], f[i]);
+      f[pa].l = f[pa].l + fp.l;
+      f[pa].a = f[pa].a + fp.a;
+      add_inertia(Ic[pa], act_inertia(X[i], Ic[i]));
+    }
+  }
+  // CRBA with the composite inertias (accumulated above, children before parents)
+  for (int i = 0; i < n; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    SV F = inertia_mul(Ic[i], joint_S(j));
+    M[i * n + i] = sdot(joint_S(j), F);
+    int k = i;
+    while (true) {
+      JointView jk{sd.joints + k * CACTO_JOINT_COLS};
+      const int pk = jk.parent();
+      if (pk < 0) break;
+      F = act_force(X[k], F);
+      k = pk;
+      JointView jp{sd.joints + k * CACTO_JOINT_COLS};
+      const double mij = sdot(joint_S(jp), F);
+      M[i * n + k] = mij;
+      M[k * n + i] = mij;
+    }
+  }
+}
+
+// In-place Cholesky of SPD M (n x n); returns false if not positive definite.
+__device__ inline bool cholesky(double* L, int n) {
+  for (int j = 0; j < n; ++j) {
+    double d = L[j * n + j];
+    for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
+    if (!(d > 0.0)) return false;
+    d = sqrt(d);
+    L[j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double s = L[i * n + j];
+      for (int k = 0; k < j; ++k) s -= L[i * n + k] * L[j * n + k];
+      L[i * n + j] = s / d;
+    }
+  }
+  return true;
+}
+__device__ inline void chol_solve(const double* L, int n, double* x) {
+  for (int i = 0; i < n; ++i) {
+    double s = x[i];
+    for (int k = 0; k < i; ++k) s -= L[i * n + k] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = x[i];
+    for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+}
+
+// EE frame translation (forward kinematics to the EE parent joint, then the fixed placement).
+__device__ inline V3 chain_ee(const SysDevice& sd, const double* q) {
+  const int n = sd.p.n_joints;
+  M3 oR[CACTO_MAX_JOINTS];
+  V3 op[CACTO_MAX_JOINTS];
+  for (int i = 0; i < n; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    SE3 X = joint_placement(j, q[i]);
+    const int pa = j.parent();
+    if (pa < 0) {
+      oR[i] = X.R;
+      op[i] = X.p;
+    } else {
+      oR[i] = mul(oR[pa], X.R);
+      op[i] = mul(oR[pa], X.p) + op[pa];
+    }
+  }
+  const int e = sd.p.ee_parent;
+  return mul(oR[e], v3(sd.p.ee_p[0], sd.p.ee_p[1], sd.p.ee_p[2])) + op[e];
+}
+
+// ------------------------------------------------------------------ environment functions
+
+// Env.simulate. `f32in`: state/action originate from float32 tensors (compute_actor_grad path),
+// which makes `v*dt` a float32 product and `self.v += dv*dt` round to float32 (numpy in-place on a
+// float32 view, robot_utils.py:403-405); otherwise all float64 (rollouts). environment.py:80-91.
+__device__ inline bool env_simulate(const SysDevice& sd, const double* s, const double* a, bool f32in,
+                                    double* out) {
+  const cacto_sys_params& p = sd.p;
+  const int ns = p.nb_state;
+  const double dt = p.dt;
+  if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) {  // environment.py:235-243
+    out[0] = s[0] + dt * a[0];
+    out[1] = s[1] + dt * a[1];
+    out[2] = s[2] + dt;
+    return true;
+  }
+  if (p.dyn_kind == CACTO_DYN_CHAIN) {
+    const int n = p.n_joints;
+    double M[CACTO_MAX_JOINTS * CACTO_MAX_JOINTS], h[CACTO_MAX_JOINTS], dv[CACTO_MAX_JOINTS];
+    chain_terms(sd, s, s + n, M, h);
+    for (int i = 0; i < n; ++i) dv[i] = a[i] - h[i];
+    bool ok = cholesky(M, n);
+    chol_solve(M, n, dv);
+    for (int i = 0; i < n; ++i) {
+      const double v = s[n + i];
+      if (f32in) {
+        const float vdt = __fmul_rn((float)v, (float)dt);
+        out[i] = s[i] + (double)vdt;
+        out[n + i] = (double)(float)(v + dv[i] * dt);
+      } else {
+        out[i] = s[i] + v * dt;
+        out[n + i] = v + dv[i] * dt;
+      }
+    }
+    out[ns - 1] = s[ns - 1] + dt;
+    return ok;
+  }
+  return false;
+}
+
+// Env.derivative (environment.py:93-109 / SI :209-219): Fu[ns, na] row-major, rows scaled by
+// 1/state_norm when NORMALIZE_INPUTS.
+__device__ inline void env_derivative(const SysDevice& sd, const double* s, double* Fu) {
+  const cacto_sys_params& p = sd.p;
+  const int ns = p.nb_state, na = p.nb_action;
+  for (int k = 0; k < ns * na; ++k) Fu[k] = 0.0;
+  if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) {
+    Fu[0 * na + 0] = p.dt;
+    Fu[1 * na + 1] = p.dt;
+  } else if (p.dyn_kind == CACTO_DYN_CHAIN) {
+    const int n = p.n_joints;
+    double M[CACTO_MAX_JOINTS * CACTO_MAX_JOINTS], h[CACTO_MAX_JOINTS], zero[CACTO_MAX_JOINTS];
+    for (int i = 0; i < n; ++i) zero[i] = 0.0;
+    chain_terms(sd, s, zero, M, h);
+    cholesky(M, n);
+    for (int c = 0; c < n; ++c) {  // column c of Minv
+      double x[CACTO_MAX_JOINTS];
+      for (int i = 0; i < n; ++i) x[i] = (i == c) ? 1.0 : 0.0;
+      chol_solve(M, n, x);
+      for (int i = 0; i < n; ++i) Fu[(p.nv + i) * na + c] = x[i] * p.dt;
+    }
+  }
+  if (p.normalize)
+    for (int r = 0; r < ns - 1; ++r) {
+      const double inv = 1.0 / p.state_norm[r];
+      for (int c = 0; c < na; ++c) Fu[r * na + c] *= inv;
+    }
+}
+
+__device__ inline V3 env_ee(const SysDevice& sd, const double* s) {
+  if (sd.p.dyn_kind == CACTO_DYN_CHAIN) return chain_ee(sd, s);
+  return v3(s[0], s[1], 0.0);  // SI / car: environment.py:245-250
+}
+
+__device__ __forceinline__ double ell_cost(const cacto_sys_params& p, double x, double y, double xc,
+                                           double yc, double A, double B) {
+  const double e = ((x - xc) * (x - xc)) / ((A / 2) * (A / 2)) + ((y - yc) * (y - yc)) / ((B / 2) * (B / 2));
+  return log(exp(p.alpha * -(e - 1.0)) + 1.0) / p.alpha;
+}
+
+// bound_control_cost (environment.py:158-163), float64
+__device__ inline double bound_control_cost(const cacto_sys_params& p, const double* a) {
+  double u = 0.0;
+  for (int i = 0; i < p.nb_action; ++i) u += a[i] * a[i] + p.w_b * pow(a[i] / p.u_max[i], 10.0);
+  return u;
+}
+
+// Env.reward (float64). `f32state`: the state came from a float32 tensor (affects the float32
+// numpy dot of the manipulator velocity term). a may be nullptr (reward(w, s) with action=None).
+__device__ inline double env_reward(const SysDevice& sd, const double* w, const double* s, const double* a,
+                                    bool f32state) {
+  const cacto_sys_params& p = sd.p;
+  const V3 e = env_ee(sd, s);
+  const double x = e.x, y = e.y;
+  const double* o = p.obs;
+  const double ell1 = ell_cost(p, x, y, o[0], o[1], o[6], o[7]);
+  const double ell2 = ell_cost(p, x, y, o[2], o[3], o[8], o[9]);
+  const double ell3 = ell_cost(p, x, y, o[4], o[5], o[10], o[11]);
+  const double dx = x - p.target[0], dy = y - p.target[1];
+  const double s01 = sqrt(0.1);
+  double pk = sqrt(dx * dx + 0.1);
+  pk = pk - s01;
+  pk = pk - 0.1;
+  pk = pk + sqrt(dy * dy + 0.1);
+  pk = pk - s01;
+  pk = pk - 0.1;
+  const double peak = log(exp(p.alpha2 * -pk) + 1.0) / p.alpha2;
+  const double u_cost = a ? bound_control_cost(p, a) : 0.0;
+  const double dist = dx * dx + dy * dy;
+  double r = -w[0] * dist + w[1] * peak;
+  if (p.reward_kind == CACTO_REW_MANIPULATOR) {
+    double vel = 0.0;
+    if (w[2] != 0.0) {
+      const int nq = p.nq;
+      if (f32state) {
+        float acc = 0.0f;
+        for (int k = 0; k < p.nv; ++k) acc = __fadd_rn(acc, __fmul_rn((float)s[nq + k], (float)s[nq + k]));
+        vel = acc;
+      } else {
+        for (int k = 0; k < p.nv; ++k) vel += s[nq + k] * s[nq + k];
+      }
+    }
+    r = r - w[2] * vel;
+  }
+  r = r - w[3] * ell1 - w[4] * ell2 - w[5] * ell3 - w[6] * u_cost + p.offset;
+  return p.scale * r;
+}
+
+// reward_batch's TF float32 part and its tape gradient (environment.py:282-286 and the dr_da tape
+// of NeuralNetwork.py:199-204): r = scale*(-w6*u_cost) + f32(partial);
+// u_cost = sum(a^2 + w_b*(a/u_max)^10); gradient in TF's op order (Mul/Pow/RealDiv grads).
+__device__ inline float reward_batch_f32(const cacto_sys_params& p, double w6, const float* a, double partial,
+                                         float* dr_da) {
+  const float scale = (float)p.scale, wb = (float)p.w_b, nw6 = (float)(-w6);
+  float u = 0.0f;
+  const float g = __fmul_rn(nw6, scale);
+  for (int i = 0; i < p.nb_action; ++i) {
+    const float umax = (float)p.u_max[i];
+    const float D = __fdiv_rn(a[i], umax);
+    const float t = __fadd_rn(__fmul_rn(a[i], a[i]), __fmul_rn(wb, powf(D, 10.0f)));
+    u = (i == 0) ? t : __fadd_rn(u, t);
+    if (dr_da) {
+      const float t1 = __fmul_rn(__fmul_rn(g, 2.0f), a[i]);
+      const float gD = __fmul_rn(__fmul_rn(__fmul_rn(wb, g), 10.0f), powf(D, 9.0f));
+      dr_da[i] = __fadd_rn(t1, __fdiv_rn(gD, umax));
+    }
+  }
+  return __fadd_rn(__fmul_rn(scale, __fmul_rn(nw6, u)), (float)partial);
+}
+
+}  // namespace cacto

@@ -1,0 +1,19 @@
+// Host-side handle layout shared by the translation units of libcacto_hip.so.
+#pragma once
+
+#include "env.h"
+#include "mlp.h"
+
+struct cacto_sys {
+  cacto::SysDevice host;  // host copy (validated)
+  cacto::SysDevice* dev;  // device copy read by every kernel
+  cacto::NetTopo actor, critic;
+};
+
+namespace cacto {
+inline const NetTopo& topo(const cacto_sys* s, int net) { return net == CACTO_NET_ACTOR ? s->actor : s->critic; }
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline int64_t flat_span(const NetTopo& t) { return ((int64_t)t.params + 63) / 64 * 64; }
+}  // namespace cacto
+
+cacto::NetView cacto_make_view(const cacto_sys* sys, int net, const float* netbuf);

@@ -1,0 +1,696 @@
+// Learner kernels: the per-sample chains of NN.compute_critic_grad (Sobolev, double backprop)
+// and NN.compute_actor_grad (dynamics Jacobian path), the weight-gradient GEMM (K = samples,
+// split-K partial slabs), and the fused slab-reduce + Keras Adam + packed refresh (+ soft update).
+//
+// Data flow per update (workspace, float32):
+//   chain kernel (16 samples / workgroup) -> per-layer operand panels LT_l [in_pad][ld], RT_l
+//   [out_pad][ld] (feature-major, sample rows contiguous) such that
+//        dW_l = sum_rows LT_l[:, r] (x) RT_l[:, r],  db_l = sum_{rows >= bias_r0} RT_l[:, r]
+//   critic rows: [0, Bp) = (Gbar_l, D_l) (Sobolev term), [Bp, 2Bp) = (h_l, zbar_l) (plain backprop)
+//   actor rows : [0, Bp) = (h_l, zbar_l)
+//   -> k_wgrad: one wave per (layer, 16x16 output tile | bias tile, row chunk) -> slab[chunk][P]
+//   -> k_adam : sum chunks in fixed order (deterministic), Adam, packed copies, soft update.
+#include "net_common.h"
+
+namespace cacto {
+
+struct GradBufs {
+  float* LT[MAX_LAYERS];
+  float* RT[MAX_LAYERS];
+  int ld;  // row stride of the panels
+  int Bp;  // batch rounded up to 16
+};
+
+struct ChainScalars {
+  float w_S;
+  int MC;
+  int B_global;
+  int want_vt;
+};
+
+__device__ __forceinline__ void store_panel(float* base, int ld, int row, int t, int g, float4 v) {
+  float* p = base + (size_t)(16 * t + 4 * g) * ld + row;
+  p[0] = v.x;
+  p[ld] = v.y;
+  p[2 * (size_t)ld] = v.z;
+  p[3 * (size_t)ld] = v.w;
+}
+
+// custom_logarithm (NeuralNetwork.py:140-148) and its TF gradient (tf.where / tf.maximum / Log).
+__device__ __forceinline__ float clog(float x) {
+  const float eps = 1e-7f;
+  return x > 0.f ? logf(fadd(fmaxf(x, eps), 1.f)) : -logf(fadd(fmaxf(-x, eps), 1.f));
+}
+__device__ __forceinline__ float clog_backward(float x, float g) {
+  const float eps = 1e-7f;
+  const float ax = x > 0.f ? x : -x;
+  if (!(ax >= eps)) return 0.f;  // Maximum grad goes to the constant when |x| < eps
+  return fmul(g, fdiv(1.f, fadd(ax, 1.f)));
+}
+
+// ---------------------------------------------------------------- critic chain (a11)
+__global__ void __launch_bounds__(CACTO_THREADS)
+    k_critic_grad(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, ChainScalars cs,
+                  const double* __restrict__ storage, const int32_t* __restrict__ idx, const float* __restrict__ isw,
+                  int B, GradBufs gb, float* __restrict__ y_out, float* __restrict__ V_out, float* __restrict__ Vt_out,
+                  int32_t* __restrict__ step) {
+  __shared__ float4 X0[64], XT[64], G0[64];
+  __shared__ float4 Z[24 * 64];
+  __shared__ float4 H[16 * 64];
+  __shared__ float4 G[16 * 64];
+  __shared__ float4 ZB[24 * 64];
+  __shared__ float4 GB[16 * 64];
+  __shared__ float4 red[4 * 64];
+  __shared__ float st[256], stn[256], dvdx[256];
+  __shared__ float Rs[16], ds[16], ws[16], Vn[16], V[16], y[16], Vb[16], Vt2[16];
+  const cacto_sys_params& p = sdp->p;
+  const Lane L;
+  const int ns = p.nb_state, cols = 3 * ns + 3, s0 = blockIdx.x * CACTO_TILE;
+  const int ld = gb.ld, Bp = gb.Bp;
+  const bool sob = cs.w_S != 0.f;
+  const int zoff[4] = {0, 4, 8, 16};
+  const int goff[4] = {0, 0, 4, 8};
+  if (blockIdx.x == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
+
+  if (L.tid < 16) {
+    const int c = L.tid;
+    const bool valid = s0 + c < B;
+    const double* rp = storage + (size_t)(valid ? idx[s0 + c] : 0) * cols;
+    for (int f = 0; f < 16; ++f) {
+      const bool in = valid && f < ns;
+      st[c * 16 + f] = in ? (float)rp[f] : 0.f;
+      stn[c * 16 + f] = in ? (float)rp[ns + 1 + f] : 0.f;
+      dvdx[c * 16 + f] = in ? (float)rp[2 * ns + 1 + f] : 0.f;
+    }
+    Rs[c] = valid ? (float)rp[ns] : 0.f;
+    ds[c] = valid ? (float)rp[3 * ns + 1] : 0.f;
+    ws[c] = valid ? (isw ? isw[s0 + c] : 1.f) : 0.f;
+  }
+  __syncthreads();
+  if (L.wave == 0) {
+    fill_input_tile(p, st, X0, L);
+    fill_input_tile(p, stn, XT, L);
+  }
+  __syncthreads();
+
+  // y = R + (1 - d) * V_tgt(s_next)   (NeuralNetwork.py:153-158)
+  if (!cs.MC) critic_forward_tile(Tg, XT, nullptr, H, red, Vn, L, [](int, int, float4, float4) {});
+  __syncthreads();
+  if (L.tid < 16) y[L.tid] = cs.MC ? Rs[L.tid] : fadd(Rs[L.tid], fmul(fsub(1.f, ds[L.tid]), Vn[L.tid]));
+  if (cs.want_vt) {  // the extra V_tgt(s) of NeuralNetwork.py:178
+    critic_forward_tile(Tg, X0, nullptr, H, red, Vt2, L, [](int, int, float4, float4) {});
+    __syncthreads();
+  }
+
+  // forward at s, keeping z; h_l -> LT_l second half
+  if (L.wave == 0) store_panel(gb.LT[0], ld, Bp + s0 + L.c, 0, L.g, X0[L.lane]);
+  critic_forward_tile(C, X0, Z, H, red, V, L, [&](int l, int ot, float4, float4 h4) {
+    store_panel(gb.LT[l + 1], ld, Bp + s0 + L.c, ot, L.g, h4);
+  });
+  __syncthreads();
+
+  if (sob) {
+    // first backward: D_l -> RT_l first half; G_l kept in LDS; G_0 = dV/dx0
+    critic_first_backward(C, Z, H, G, G0, red, L, [&](int l, int ot, int lane, float4 d4) {
+      store_panel(gb.RT[l], ld, s0 + (lane & 15), ot, lane >> 4, d4);
+    });
+    __syncthreads();
+    // Sobolev loss gradient w.r.t. dV/ds, then w.r.t. G_0 (NeuralNetwork.py:167-170)
+    if (L.wave == 0) {
+      const float4 g4 = G0[L.lane];
+      const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+      float gb0[4];
+      const float gsq = fdiv(fmul(fdiv(1.f, (float)cs.B_global), ws[L.c]), (float)(ns - 1));
+      for (int r = 0; r < 4; ++r) {
+        const int f = 4 * L.g + r;
+        gb0[r] = 0.f;
+        if (f < ns - 1) {
+          const float dvds = normalize_backward(p, f, gv[r]);
+          const float yp = clog(dvds), yt = clog(dvdx[L.c * 16 + f]);
+          const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
+          gb0[r] = normalize_backward(p, f, clog_backward(dvds, gyp));
+        }
+      }
+      const float4 v = make_float4(gb0[0], gb0[1], gb0[2], gb0[3]);
+      GB[L.lane] = v;
+      store_panel(gb.LT[0], ld, s0 + L.c, 0, L.g, v);
+    }
+    __syncthreads();
+    // backward of the first backward, l = 0..3 (see oracle/nn.py compute_critic_grad)
+    const float4* cur = GB;
+    for (int l = 0; l < 4; ++l) {
+      float4* nxt = GB + ((l + 1) & 1) * 8 * 64;
+      layer(C.fwd(l), C.t.OT[l], C.t.KT[l], cur, red, L, [&](int ot, floatx4 acc) {
+        const float4 z = Z[(zoff[l] + ot) * 64 + L.lane];
+        float4 gu;
+        if (l < 3) {
+          gu = G[(goff[l + 1] + ot) * 64 + L.lane];
+        } else {
+          const int f = 16 * ot + 4 * L.g;
+          gu = make_float4(C.w(4, f, 0), C.w(4, f + 1, 0), C.w(4, f + 2, 0), C.w(4, f + 3, 0));
+        }
+        const float zz[4] = {z.x, z.y, z.z, z.w}, gg[4] = {gu.x, gu.y, gu.z, gu.w};
+        float zb[4], gn[4];
+        for (int r = 0; r < 4; ++r) {
+          zb[r] = fmul(-fmul(acc[r], gg[r]), sinf(zz[r]));  // CosGrad: -grad * sin(x)
+          gn[r] = fmul(acc[r], cosf(zz[r]));                 // MulGrad into the upstream grad
+        }
+        ZB[(zoff[l] + ot) * 64 + L.lane] = make_float4(zb[0], zb[1], zb[2], zb[3]);
+        const float4 g4 = make_float4(gn[0], gn[1], gn[2], gn[3]);
+        nxt[ot * 64 + L.lane] = g4;
+        store_panel(gb.LT[l + 1], ld, s0 + L.c, ot, L.g, g4);
+      });
+      cur = nxt;
+    }
+    if (L.tid < 16) gb.RT[4][s0 + L.tid] = 1.f;  // dW5 += Gbar_4 (G_4 = W5[:, 0])
+  } else {
+    for (int k = L.tid; k < 24 * 64; k += CACTO_THREADS) ZB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+
+  // value loss: Vbar = (2 * ((wS/B) * w)) * (V - y)   (Keras MSE, SUM_OVER_BATCH_SIZE)
+  if (L.tid < 16) {
+    const int c = L.tid;
+    const float wv = sob ? cs.w_S : 1.f;
+    const float gl = fmul(fdiv(wv, (float)cs.B_global), ws[c]);
+    Vb[c] = fmul(fmul(2.f, gl), fsub(V[c], y[c]));
+    gb.RT[4][Bp + s0 + c] = Vb[c];
+    if (s0 + c < B) {
+      if (y_out) y_out[s0 + c] = y[c];
+      if (V_out) V_out[s0 + c] = V[c];
+      if (Vt_out && cs.want_vt) Vt_out[s0 + c] = Vt2[c];
+    }
+  }
+  __syncthreads();
+  for (int k = L.tid; k < 8 * 64; k += CACTO_THREADS) {  // zbar_3 += (Vbar * W5) * cos(z3)
+    const int ot = k >> 6, lane = k & 63, g = lane >> 4, c = lane & 15;
+    const float4 z = Z[(zoff[3] + ot) * 64 + lane];
+    float4 zb = ZB[(zoff[3] + ot) * 64 + lane];
+    const int f = 16 * ot + 4 * g;
+    zb.x = fadd(zb.x, fmul(fmul(Vb[c], C.w(4, f, 0)), cosf(z.x)));
+    zb.y = fadd(zb.y, fmul(fmul(Vb[c], C.w(4, f + 1, 0)), cosf(z.y)));
+    zb.z = fadd(zb.z, fmul(fmul(Vb[c], C.w(4, f + 2, 0)), cosf(z.z)));
+    zb.w = fadd(zb.w, fmul(fmul(Vb[c], C.w(4, f + 3, 0)), cosf(z.w)));
+    ZB[(zoff[3] + ot) * 64 + lane] = zb;
+  }
+  __syncthreads();
+  // backward through the forward graph: zbar_{l-1} += (zbar_l W_l^T) * cos(z_{l-1})
+  for (int l = 3; l >= 0; --l) {
+    for (int k = L.tid; k < C.t.OT[l] * 64; k += CACTO_THREADS) {
+      const int ot = k >> 6, lane = k & 63;
+      store_panel(gb.RT[l], ld, Bp + s0 + (lane & 15), ot, lane >> 4, ZB[(zoff[l] + ot) * 64 + lane]);
+    }
+    if (l == 0) break;
+    layer(C.bwd(l), C.t.KT[l], C.t.OT[l], ZB + zoff[l] * 64, red, L, [&](int it, floatx4 acc) {
+      const float4 z = Z[(zoff[l - 1] + it) * 64 + L.lane];
+      float4 zb = ZB[(zoff[l - 1] + it) * 64 + L.lane];
+      zb.x = fadd(zb.x, fmul(acc[0], cosf(z.x)));
+      zb.y = fadd(zb.y, fmul(acc[1], cosf(z.y)));
+      zb.z = fadd(zb.z, fmul(acc[2], cosf(z.z)));
+      zb.w = fadd(zb.w, fmul(acc[3], cosf(z.w)));
+      ZB[(zoff[l - 1] + it) * 64 + L.lane] = zb;
+    });
+  }
+}
+
+// ---------------------------------------------------------------- actor chain (a12)
+__global__ void __launch_bounds__(CACTO_THREADS)
+    k_actor_grad(const SysDevice* __restrict__ sdp, NetView Ac, NetView C, ChainScalars cs,
+                 const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
+                 int32_t* __restrict__ step) {
+  __shared__ float4 X0[64], XS[64], G0[64], ZB3[64];
+  __shared__ float4 ZA[32 * 64];  // actor z1, z2
+  __shared__ float4 H[32 * 64];   // actor h ping-pong; later critic H (16) + actor zbar2 (16)
+  __shared__ float4 ZC[24 * 64];  // critic z at s'
+  __shared__ float4 red[4 * 64];
+  __shared__ float st[256], stn[256];
+  __shared__ float A[16 * CACTO_MAX_ACTION];
+  __shared__ float Fu[16 * CACTO_MAX_STATE * CACTO_MAX_ACTION];
+  __shared__ float dra[16 * CACTO_MAX_ACTION];
+  __shared__ float Vn[16];
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const Lane L;
+  const int ns = p.nb_state, na = p.nb_action, cols = 3 * ns + 3, s0 = blockIdx.x * CACTO_TILE;
+  const int ld = gb.ld;
+  if (blockIdx.x == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
+  double term_c = 0.0;
+  if (L.tid < 16) {
+    const int c = L.tid;
+    const bool valid = s0 + c < B;
+    const double* rp = storage + (size_t)(valid ? idx[s0 + c] : 0) * cols;
+    for (int f = 0; f < 16; ++f) st[c * 16 + f] = (valid && f < ns) ? (float)rp[f] : 0.f;
+    term_c = valid ? rp[3 * ns + 2] : 0.0;
+  }
+  __syncthreads();
+  if (L.wave == 0) {
+    fill_input_tile(p, st, X0, L);
+    store_panel(gb.LT[0], ld, s0 + L.c, 0, L.g, X0[L.lane]);  // input of layer 0 (normalised)
+  }
+  __syncthreads();
+  // actor forward; h1 -> LT_1, h2 -> LT_2
+  actor_forward_tile(Ac, na, X0, ZA, H, red, A, L, [&](int l, int ot, float4, float4 h4) {
+    store_panel(gb.LT[l + 1], ld, s0 + L.c, ot, L.g, h4);
+  });
+  __syncthreads();
+  // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
+  if (L.tid < 16) {
+    const int c = L.tid;
+    double s[CACTO_MAX_STATE], a[CACTO_MAX_ACTION], sn[CACTO_MAX_STATE], F[CACTO_MAX_STATE * CACTO_MAX_ACTION], w[8];
+    float af[CACTO_MAX_ACTION], g[CACTO_MAX_ACTION];
+    for (int f = 0; f < ns; ++f) s[f] = (double)st[c * 16 + f];
+    for (int i = 0; i < na; ++i) {
+      af[i] = A[c * na + i];
+      a[i] = (double)af[i];
+    }
+    env_simulate(sd, s, a, true, sn);
+    for (int f = 0; f < 16; ++f) stn[c * 16 + f] = f < ns ? (float)sn[f] : 0.f;
+    env_derivative(sd, s, F);
+    for (int k = 0; k < ns * na; ++k) Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
+    for (int k = 0; k < p.n_weights; ++k) w[k] = term_c * p.w_terminal[k] + (1.0 - term_c) * p.w_running[k];
+    const double partial = env_reward(sd, w, s, nullptr, true);
+    (void)reward_batch_f32(p, w[6], af, partial, g);
+    for (int i = 0; i < na; ++i) dra[c * na + i] = g[i];
+  }
+  __syncthreads();
+  if (L.wave == 0) fill_input_tile(p, stn, XS, L);
+  __syncthreads();
+  // critic (already updated) at s': V and dV/dx0 (NeuralNetwork.py:190-195)
+  float4* HC = H;            // 16 tiles
+  float4* ZB2 = H + 16 * 64;  // 16 tiles
+  critic_forward_tile(C, XS, ZC, HC, red, Vn, L, [](int, int, float4, float4) {});
+  __syncthreads();
+  critic_first_backward(C, ZC, HC, nullptr, G0, red, L, [](int, int, int, float4) {});
+  __syncthreads();
+  // dQ/da = dV/ds' Fu + dr/da ; abar = -dQ/da / B  (NeuralNetwork.py:206-231)
+  if (L.wave == 0) {
+    const int c = L.c;
+    float abar[4];
+    for (int r = 0; r < 4; ++r) {
+      const int j = 4 * L.g + r;
+      abar[r] = 0.f;
+      if (j < na && s0 + c < B) {
+        float q = 0.f;
+        for (int i = 0; i < ns; ++i) {
+          const float4 gt = G0[tile_lane(i) + c];
+          const float gi = normalize_backward(p, i, get4(gt, i & 3));
+          const float t = fmul(gi, Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + i * na + j]);
+          q = (i == 0) ? t : fadd(q, t);
+        }
+        q = fadd(q, dra[c * na + j]);
+        abar[r] = fmul(-q, fdiv(1.f, (float)cs.B_global));
+      }
+    }
+    const float4 v = make_float4(abar[0], abar[1], abar[2], abar[3]);
+    ZB3[L.lane] = v;
+    store_panel(gb.RT[2], ld, s0 + c, 0, L.g, v);
+  }
+  __syncthreads();
+  // zbar2 = (abar W3^T) * lrelu'(z2) ; zbar1 = (zbar2 W2^T) * lrelu'(z1)
+  layer(Ac.bwd(2), Ac.t.KT[2], Ac.t.OT[2], ZB3, red, L, [&](int it, floatx4 acc) {
+    const float4 z = ZA[(16 + it) * 64 + L.lane];
+    const float zz[4] = {z.x, z.y, z.z, z.w};
+    float o[4];
+    for (int r = 0; r < 4; ++r) o[r] = zz[r] > 0.f ? acc[r] : fmul(acc[r], 0.3f);
+    const float4 v = make_float4(o[0], o[1], o[2], o[3]);
+    ZB2[it * 64 + L.lane] = v;
+    store_panel(gb.RT[1], ld, s0 + L.c, it, L.g, v);
+  });
+  layer(Ac.bwd(1), Ac.t.KT[1], Ac.t.OT[1], ZB2, red, L, [&](int it, floatx4 acc) {
+    const float4 z = ZA[it * 64 + L.lane];
+    const float zz[4] = {z.x, z.y, z.z, z.w};
+    float o[4];
+    for (int r = 0; r < 4; ++r) o[r] = zz[r] > 0.f ? acc[r] : fmul(acc[r], 0.3f);
+    store_panel(gb.RT[0], ld, s0 + L.c, it, L.g, make_float4(o[0], o[1], o[2], o[3]));
+  });
+}
+
+// ---------------------------------------------------------------- weight-gradient GEMM
+struct WgLayer {
+  const float* LT;
+  const float* RT;
+  int in, out, IT, OT, woff, boff;
+};
+struct WgArgs {
+  WgLayer l[MAX_LAYERS];
+  int nl, ld, r_begin, r_end, bias_r0, CH, nch, P, tpc;
+  int toff[MAX_LAYERS + 1];
+};
+
+__global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab) {
+  const int wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wave_id >= a.nch * a.tpc) return;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int chunk = wave_id / a.tpc, rem = wave_id - chunk * a.tpc;
+  int li = 0;
+  while (rem >= a.toff[li + 1]) ++li;
+  const WgLayer& Ly = a.l[li];
+  const int local = rem - a.toff[li];
+  const int lo = a.r_begin + chunk * a.CH, hi = min(a.r_end, lo + a.CH);
+  float* out = slab + (size_t)chunk * a.P;
+  if (local < Ly.IT * Ly.OT) {
+    const int it = local / Ly.OT, ot = local - it * Ly.OT;
+    const float* ap = Ly.LT + (size_t)(16 * it + c) * a.ld + 4 * g;
+    const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+    int r = lo;
+    for (; r + 16 < hi; r += 32) {
+      acc = mfma_block(*reinterpret_cast<const float4*>(ap + r), *reinterpret_cast<const float4*>(bp + r), acc);
+      acc2 = mfma_block(*reinterpret_cast<const float4*>(ap + r + 16), *reinterpret_cast<const float4*>(bp + r + 16),
+                        acc2);
+    }
+    if (r < hi) acc = mfma_block(*reinterpret_cast<const float4*>(ap + r), *reinterpret_cast<const float4*>(bp + r), acc);
+    acc = acc + acc2;
+    const int o = 16 * ot + c;
+    for (int q = 0; q < 4; ++q) {
+      const int i = 16 * it + 4 * g + q;
+      if (i < Ly.in && o < Ly.out) out[Ly.woff + i * Ly.out + o] = acc[q];
+    }
+  } else {
+    const int ot = local - Ly.IT * Ly.OT;
+    const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
+    float s = 0.f;
+    for (int r = max(lo, a.bias_r0); r < hi; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(bp + r);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (g == 0 && 16 * ot + c < Ly.out) out[Ly.boff + 16 * ot + c] = s;
+  }
+}
+
+// ---------------------------------------------------------------- Adam (+ packed refresh, soft update)
+struct AdamArgs {
+  double beta1, beta2, eps, tau;
+  double lr[5];
+  double bounds[4];
+  int which;  // 0 critic counter, 1 actor counter
+  int soft;
+};
+
+__device__ __forceinline__ void write_packed(float4* pk4, const NetTopo& t, int p, float val) {
+  float* pk = reinterpret_cast<float*>(pk4);
+  int l = t.L - 1;
+  while (t.woff[l] > p) --l;
+  if (p >= t.boff[l]) return;
+  const int local = p - t.woff[l];
+  const int i = local / t.out[l], o = local - (local / t.out[l]) * t.out[l];
+  pk[((size_t)(t.pkoff[l] + (o >> 4) * t.KT[l] + (i >> 4)) * 64 + ((i & 15) >> 2) * 16 + (o & 15)) * 4 + (i & 3)] = val;
+  pk[((size_t)(t.blocks + t.pkoff[l] + (i >> 4) * t.OT[l] + (o >> 4)) * 64 + ((o & 15) >> 2) * 16 + (i & 15)) * 4 +
+     (o & 3)] = val;
+}
+
+__global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, int nch, NetTopo t, float* netbuf,
+                                              float4* packed, float* __restrict__ m, float* __restrict__ v,
+                                              const int32_t* __restrict__ step, AdamArgs a, float* target,
+                                              float4* target_packed) {
+  const int it = step[a.which];  // = Keras iterations + 1
+  const int iters = it - 1;
+  double lr = a.lr[4];
+  for (int k = 0; k < 4; ++k)
+    if ((double)iters <= a.bounds[k]) {
+      lr = a.lr[k];
+      break;
+    }
+  const float tf = (float)it;
+  const float b1p = powf((float)a.beta1, tf), b2p = powf((float)a.beta2, tf);
+  const float alpha = fdiv(fmul((float)lr, __fsqrt_rn(fsub(1.f, b2p))), fsub(1.f, b1p));
+  const float c1 = (float)(1.0 - a.beta1), c2 = (float)(1.0 - a.beta2), eps = (float)a.eps;
+  const float tau = (float)a.tau, omt = (float)(1.0 - a.tau);
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < t.params; p += gridDim.x * blockDim.x) {
+    float g = slab[p];
+    for (int ch = 1; ch < nch; ++ch) g += slab[(size_t)ch * t.params + p];
+    float mm = m[p], vv = v[p];
+    mm = fadd(mm, fmul(fsub(g, mm), c1));
+    vv = fadd(vv, fmul(fsub(fmul(g, g), vv), c2));
+    const float th = fsub(netbuf[p], fdiv(fmul(mm, alpha), fadd(__fsqrt_rn(vv), eps)));
+    m[p] = mm;
+    v[p] = vv;
+    netbuf[p] = th;
+    write_packed(packed, t, p, th);
+    if (a.soft) {
+      const float tg = fadd(fmul(th, tau), fmul(target[p], omt));
+      target[p] = tg;
+      write_packed(target_packed, t, p, tg);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_soft(NetTopo t, const float* __restrict__ src, float* target,
+                                              float4* target_packed, double tau_d) {
+  const float tau = (float)tau_d, omt = (float)(1.0 - tau_d);
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < t.params; p += gridDim.x * blockDim.x) {
+    const float tg = fadd(fmul(src[p], tau), fmul(target[p], omt));
+    target[p] = tg;
+    write_packed(target_packed, t, p, tg);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_reduce(const float* __restrict__ slab, int nch, int P, float* __restrict__ out) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    float g = slab[p];
+    for (int ch = 1; ch < nch; ++ch) g += slab[(size_t)ch * P + p];
+    out[p] = g;
+  }
+}
+
+}  // namespace cacto
+
+using namespace cacto;
+
+namespace {
+
+constexpr int WG_CHUNK = 256;
+
+struct Workspace {
+  GradBufs crit, act;
+  float* slab;
+  float* scal;  // y, V, Vt scratch (3 * Bp)
+  size_t bytes;
+  int Bp;
+};
+
+inline size_t align64(size_t n) { return (n + 63) / 64 * 64; }
+
+Workspace plan(const cacto_sys* sys, int B, char* base) {
+  Workspace w{};
+  const int Bp = (B + 15) / 16 * 16;
+  w.Bp = Bp;
+  const NetTopo& tc = sys->critic;
+  const NetTopo& ta = sys->actor;
+  size_t off = 0;
+  float* f = reinterpret_cast<float*>(base);
+  // critic panels (ld = 2Bp)
+  w.crit.ld = 2 * Bp;
+  w.crit.Bp = Bp;
+  size_t coff = 0;
+  for (int l = 0; l < tc.L; ++l) {
+    w.crit.LT[l] = f ? f + coff : nullptr;
+    coff += (size_t)16 * tc.KT[l] * w.crit.ld;
+    w.crit.RT[l] = f ? f + coff : nullptr;
+    coff += (size_t)16 * tc.OT[l] * w.crit.ld;
+  }
+  w.act.ld = Bp;
+  w.act.Bp = Bp;
+  size_t aoff = 0;
+  for (int l = 0; l < ta.L; ++l) {
+    w.act.LT[l] = f ? f + aoff : nullptr;
+    aoff += (size_t)16 * ta.KT[l] * w.act.ld;
+    w.act.RT[l] = f ? f + aoff : nullptr;
+    aoff += (size_t)16 * ta.OT[l] * w.act.ld;
+  }
+  off = align64(std::max(coff, aoff));
+  const int nch_c = (2 * Bp + WG_CHUNK - 1) / WG_CHUNK, nch_a = (Bp + WG_CHUNK - 1) / WG_CHUNK;
+  w.slab = f ? f + off : nullptr;
+  off += align64(std::max((size_t)nch_c * tc.params, (size_t)nch_a * ta.params));
+  w.scal = f ? f + off : nullptr;
+  off += align64((size_t)3 * Bp);
+  w.bytes = off * sizeof(float);
+  return w;
+}
+
+WgArgs wg_args(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int bias_r0) {
+  WgArgs a{};
+  a.nl = t.L;
+  a.ld = gb.ld;
+  a.r_begin = r_begin;
+  a.r_end = r_end;
+  a.bias_r0 = bias_r0;
+  a.CH = WG_CHUNK;
+  a.nch = (r_end - r_begin + WG_CHUNK - 1) / WG_CHUNK;
+  a.P = t.params;
+  int tpc = 0;
+  for (int l = 0; l < t.L; ++l) {
+    a.l[l] = WgLayer{gb.LT[l], gb.RT[l], t.in[l], t.out[l], t.KT[l], t.OT[l], t.woff[l], t.boff[l]};
+    a.toff[l] = tpc;
+    tpc += t.KT[l] * t.OT[l] + t.OT[l];
+  }
+  a.toff[t.L] = tpc;
+  a.tpc = tpc;
+  return a;
+}
+
+ChainScalars chain_scalars(const cacto_update_cfg* cfg, int B) {
+  ChainScalars cs;
+  cs.w_S = (float)cfg->w_S;
+  cs.MC = cfg->MC;
+  cs.B_global = cfg->B_global > 0 ? cfg->B_global : B;
+  cs.want_vt = cfg->want_target_V;
+  return cs;
+}
+
+AdamArgs adam_args(const cacto_update_cfg* cfg, int which, int soft) {
+  AdamArgs a{};
+  a.beta1 = cfg->beta1;
+  a.beta2 = cfg->beta2;
+  a.eps = cfg->epsilon;
+  a.tau = cfg->tau;
+  const double* lr = which == CACTO_NET_CRITIC ? cfg->critic_lr : cfg->actor_lr;
+  for (int k = 0; k < 5; ++k) a.lr[k] = lr[k];
+  for (int k = 0; k < 4; ++k) a.bounds[k] = cfg->lr_bounds[k];
+  a.which = which == CACTO_NET_CRITIC ? 0 : 1;
+  a.soft = soft;
+  return a;
+}
+
+int check_nets(const cacto_nets* n) {
+  CACTO_REQUIRE(n && n->actor_d && n->actor_m_d && n->actor_v_d && n->critic_d && n->critic_m_d && n->critic_v_d &&
+                    n->target_d && n->step_d,
+                "cacto_nets: null member");
+  return CACTO_OK;
+}
+
+int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                  const double* storage, const int32_t* idx, const float* isw, int B, float* y,
+                                  float* V, float* Vt, const Workspace& w, hipStream_t st, int* nch_out) {
+  NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
+  NetView Tg = cacto_make_view(sys, CACTO_NET_CRITIC, nets->target_d);
+  const ChainScalars cs = chain_scalars(cfg, B);
+  float* yb = y ? y : w.scal;
+  float* Vb = V ? V : w.scal + w.Bp;
+  float* Vtb = Vt ? Vt : w.scal + 2 * w.Bp;
+  hipLaunchKernelGGL(k_critic_grad, dim3(w.Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, cs, storage, idx, isw,
+                     B, w.crit, yb, Vb, Vtb, nets->step_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  const bool sob = cs.w_S != 0.f;
+  WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
+  const int waves = a.nch * a.tpc;
+  hipLaunchKernelGGL(k_wgrad, dim3((waves + 3) / 4), dim3(256), 0, st, a, w.slab);
+  CACTO_CHECK_HIP(hipGetLastError());
+  *nch_out = a.nch;
+  return CACTO_OK;
+}
+
+int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                 const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
+                                 int* nch_out) {
+  NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
+  NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
+  const ChainScalars cs = chain_scalars(cfg, B);
+  hipLaunchKernelGGL(k_actor_grad, dim3(w.Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage, idx, B,
+                     w.act, nets->step_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
+  const int waves = a.nch * a.tpc;
+  hipLaunchKernelGGL(k_wgrad, dim3((waves + 3) / 4), dim3(256), 0, st, a, w.slab);
+  CACTO_CHECK_HIP(hipGetLastError());
+  *nch_out = a.nch;
+  return CACTO_OK;
+}
+
+int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, int which,
+                const float* slab, int nch, int soft, hipStream_t st) {
+  const NetTopo& t = topo(sys, which);
+  float* nb = which == CACTO_NET_CRITIC ? nets->critic_d : nets->actor_d;
+  float* m = which == CACTO_NET_CRITIC ? nets->critic_m_d : nets->actor_m_d;
+  float* v = which == CACTO_NET_CRITIC ? nets->critic_v_d : nets->actor_v_d;
+  float4* pk = reinterpret_cast<float4*>(nb + flat_span(t));
+  float4* tpk = reinterpret_cast<float4*>(nets->target_d + flat_span(t));
+  const int grid = std::min((t.params + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, slab, nch, t, nb, pk, m, v, nets->step_d,
+                     adam_args(cfg, which, soft && which == CACTO_NET_CRITIC), nets->target_d, tpk);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+}  // namespace
+
+extern "C" size_t cacto_workspace_bytes(const cacto_sys* sys, int B) {
+  if (!sys || B <= 0) return 0;
+  return plan(sys, B, nullptr).bytes;
+}
+
+#define CHECK_WS(ws, nbytes, B)                                                                   \
+  CACTO_REQUIRE((ws) != nullptr && (nbytes) >= plan(sys, (B), nullptr).bytes,                     \
+                "workspace too small: query cacto_workspace_bytes(sys, B)");                      \
+  CACTO_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 255) == 0, "workspace must be 256-byte aligned")
+
+extern "C" int cacto_critic_grad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                 const double* storage_d, const int32_t* idx_d, const float* is_w_d, int B,
+                                 float* grad_d, float* y_d, float* V_d, float* Vt_d, void* workspace_d,
+                                 size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && idx_d && grad_d && B > 0, "cacto_critic_grad: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  hipStream_t st = as_stream(stream);
+  int nch = 0;
+  if (int e = launch_critic_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, is_w_d, B, y_d, V_d, Vt_d, w, st, &nch))
+    return e;
+  const int P = sys->critic.params;
+  hipLaunchKernelGGL(k_reduce, dim3(std::min((P + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, P, grad_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_actor_grad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                const double* storage_d, const int32_t* idx_d, int B, float* grad_d, void* workspace_d,
+                                size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && idx_d && grad_d && B > 0, "cacto_actor_grad: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  hipStream_t st = as_stream(stream);
+  int nch = 0;
+  if (int e = launch_actor_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, B, w, st, &nch)) return e;
+  const int P = sys->actor.params;
+  hipLaunchKernelGGL(k_reduce, dim3(std::min((P + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, P, grad_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_adam_step(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, int which,
+                               const float* grad_d, int soft_update, void* stream) {
+  CACTO_REQUIRE(sys && cfg && grad_d && (which == CACTO_NET_ACTOR || which == CACTO_NET_CRITIC),
+                "cacto_adam_step: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  return launch_adam(sys, nets, cfg, which, grad_d, 1, soft_update, as_stream(stream));
+}
+
+extern "C" int cacto_soft_update(const cacto_sys* sys, const cacto_nets* nets, float tau, void* stream) {
+  CACTO_REQUIRE(sys, "cacto_soft_update: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  const NetTopo& t = sys->critic;
+  hipLaunchKernelGGL(k_soft, dim3(std::min((t.params + 255) / 256, 1024)), dim3(256), 0, as_stream(stream), t,
+                     nets->critic_d, nets->target_d, reinterpret_cast<float4*>(nets->target_d + flat_span(t)),
+                     (double)tau);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                            const double* storage_d, const int32_t* idx_d, const float* is_w_d, int B, float* y_d,
+                            float* V_d, float* Vt_d, void* workspace_d, size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && idx_d && B > 0, "cacto_update: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  hipStream_t st = as_stream(stream);
+  int nch = 0;
+  if (int e = launch_critic_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, is_w_d, B, y_d, V_d, Vt_d, w, st, &nch))
+    return e;
+  if (int e = launch_adam(sys, nets, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st)) return e;
+  if (int e = launch_actor_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, B, w, st, &nch)) return e;
+  return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab, nch, 0, st);
+}

@@ -1,0 +1,117 @@
+// MFMA (v_mfma_f32_16x16x4_f32) tile machinery for the CACTO actor and critic MLPs.
+//
+// Orientation: features are the MFMA M dimension, samples the N dimension (16 samples per tile),
+// so a layer computes out^T[OUT x 16] = W^T[OUT x IN] · in^T[IN x 16].
+//
+// Activation tile (16 features x 16 samples) = 64 lanes x float4, lane l = g*16 + c holds
+// features 4g..4g+3 of sample c. This is exactly the C/D layout of the 16x16 MFMA (row = 4g + r,
+// col = c), and — reading component j as k-step j — the B-operand layout for k = 4g + j, so a
+// layer's output tile feeds the next layer with no lane movement (one ds_write_b128 /
+// ds_read_b128 per lane, conflict-free).
+//
+// Packed weights ("pk", forward): for out-tile ot and k-tile kt, lane l = (g, c), component j:
+//     A[i = c][k = g] of MFMA j  =  W[16kt + 4g + j][16ot + c]      (zero-padded)
+// stored at ((pkoff_l + ot*KT + kt) * 64 + l) * 4 + j — one coalesced 1 KiB dwordx4 wave load per
+// 4 MFMAs. Transposed ("pkT", input-gradient g_in = W · d_out): block (it, kt):
+//     A[i = c][k = g] of MFMA j  =  W[16it + c][16kt + 4g + j]
+// at ((pktbase + pkoff_l + it*OT + kt) * 64 + l) * 4 + j.
+#pragma once
+
+#include "common.h"
+
+namespace cacto {
+
+constexpr int ACTOR_LAYERS = 3;
+constexpr int CRITIC_LAYERS = 5;
+constexpr int MAX_LAYERS = 5;
+
+struct NetTopo {
+  int L;
+  int in[MAX_LAYERS], out[MAX_LAYERS];
+  int KT[MAX_LAYERS], OT[MAX_LAYERS];  // k-tiles (= in tiles), out tiles
+  int woff[MAX_LAYERS], boff[MAX_LAYERS];
+  int pkoff[MAX_LAYERS];  // in blocks
+  int blocks;             // pk blocks (pkT region has the same count, starts at `blocks`)
+  int params;
+};
+
+inline NetTopo make_topo(int net, int ns, int na) {
+  NetTopo t{};
+  const int actor_dims[4] = {ns, 256, 256, na};
+  const int critic_dims[6] = {ns, 64, 64, 128, 128, 1};
+  const int* d = net == CACTO_NET_ACTOR ? actor_dims : critic_dims;
+  t.L = net == CACTO_NET_ACTOR ? ACTOR_LAYERS : CRITIC_LAYERS;
+  int off = 0, blk = 0;
+  for (int l = 0; l < t.L; ++l) {
+    t.in[l] = d[l];
+    t.out[l] = d[l + 1];
+    t.KT[l] = (d[l] + 15) / 16;
+    t.OT[l] = (d[l + 1] + 15) / 16;
+    t.woff[l] = off;
+    off += d[l] * d[l + 1];
+    t.boff[l] = off;
+    off += d[l + 1];
+    t.pkoff[l] = blk;
+    blk += t.KT[l] * t.OT[l];
+  }
+  t.blocks = blk;
+  t.params = off;
+  return t;
+}
+
+// Device view of one network: flat Keras params (biases, W5 column) + packed fragments.
+struct NetView {
+  const float* flat;
+  const float4* pk;  // base of packed buffer (pk blocks then pkT blocks)
+  NetTopo t;
+  __device__ __forceinline__ const float4* fwd(int l) const { return pk + (size_t)t.pkoff[l] * 64; }
+  __device__ __forceinline__ const float4* bwd(int l) const {
+    return pk + (size_t)(t.blocks + t.pkoff[l]) * 64;
+  }
+  __device__ __forceinline__ float bias(int l, int f) const { return flat[t.boff[l] + f]; }
+  __device__ __forceinline__ float w(int l, int i, int o) const { return flat[t.woff[l] + i * t.out[l] + o]; }
+};
+
+// out-tile loop of one layer: each wave takes out tiles ot = wave, wave+4, ...; X = LDS tiles.
+template <typename Epi>
+__device__ __forceinline__ void mm_layer(const float4* __restrict__ A, int OT, int KT, const float4* X,
+                                         int wave, int lane, Epi&& epi) {
+  for (int ot = wave; ot < OT; ot += CACTO_NWAVES) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float4* Ap = A + (size_t)ot * KT * 64 + lane;
+    if (KT >= 2) {
+      floatx4 acc2 = {0.f, 0.f, 0.f, 0.f};
+      int kt = 0;
+      for (; kt + 1 < KT; kt += 2) {
+        acc = mfma_block(Ap[kt * 64], X[kt * 64 + lane], acc);
+        acc2 = mfma_block(Ap[(kt + 1) * 64], X[(kt + 1) * 64 + lane], acc2);
+      }
+      if (kt < KT) acc = mfma_block(Ap[kt * 64], X[kt * 64 + lane], acc);
+      acc = acc + acc2;
+    } else {
+      acc = mfma_block(Ap[0], X[lane], acc);
+    }
+    epi(ot, acc);
+  }
+}
+
+// utils.py:17-24 in float32 (TF ops: RealDiv, then *2 - 1 for the time column).
+__device__ __forceinline__ float normalize_feature(const cacto_sys_params& p, int f, float s) {
+  if (!p.normalize) return s;
+  const int ns = p.nb_state;
+  if (f == ns - 1) return fsub(fmul(fdiv(s, (float)p.state_norm[ns - 1]), 2.0f), 1.0f);
+  return fdiv(s, (float)p.state_norm[f]);
+}
+
+// d normalize / d s applied to an upstream gradient (RealDiv grad: grad / y; time: (grad*2)/nT).
+__device__ __forceinline__ float normalize_backward(const cacto_sys_params& p, int f, float g) {
+  if (!p.normalize) return g;
+  const int ns = p.nb_state;
+  if (f == ns - 1) return fdiv(fmul(g, 2.0f), (float)p.state_norm[ns - 1]);
+  return fdiv(g, (float)p.state_norm[f]);
+}
+
+// element (f, c) of a tile
+__device__ __forceinline__ int tile_lane(int f) { return (f >> 2) * 16; }
+
+}  // namespace cacto

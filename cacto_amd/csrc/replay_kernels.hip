@@ -1,0 +1,254 @@
+// Prioritized replay on the GPU: float64 sum/min segment trees in the exact node layout and
+// combination order of segment_tree.py (so sampled indices are bit-exact), stratified proportional
+// sampling, IS weights, the duplicate-once exp_counter update and last-write-wins priority updates
+// (replay_buffer.py:87-218).
+#include "internal.h"
+
+namespace cacto {
+
+constexpr int PER_THREADS = 1024;
+constexpr int PER_MAX_B = 8192;
+
+__device__ __forceinline__ double tree_min(double a, double b) { return b < a ? b : a; }  // Python min(a, b)
+
+__global__ void k_per_init(double* sum_tree, double* min_tree, int64_t n2) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n2; k += (int64_t)gridDim.x * blockDim.x) {
+    sum_tree[k] = 0.0;
+    min_tree[k] = __builtin_inf();
+  }
+}
+
+// Leaves [start, start+n) mod ring get `value`; then every ancestor is recomputed bottom-up.
+// Recomputing an ancestor from final children yields the value the sequential Python updates
+// leave behind (each node's last recomputation follows its subtree's last leaf write).
+__global__ void k_per_fill_leaves(double* sum_tree, double* min_tree, int64_t cap, int64_t ring, int64_t start, int64_t n,
+                                  double value) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t leaf = cap + (start + k) % ring;
+    sum_tree[leaf] = value;
+    min_tree[leaf] = value;
+  }
+}
+
+// One level of ancestors of the leaf range: nodes [lo, hi] at this level.
+__global__ void k_per_level(double* sum_tree, double* min_tree, int64_t lo, int64_t hi) {
+  for (int64_t k = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k <= hi; k += (int64_t)gridDim.x * blockDim.x) {
+    sum_tree[k] = sum_tree[2 * k] + sum_tree[2 * k + 1];
+    min_tree[k] = tree_min(min_tree[2 * k], min_tree[2 * k + 1]);
+  }
+}
+
+// _reduce_helper(0, end, 1, 0, cap-1) for the sum tree (end inclusive): right-nested sum of the
+// maximal left-aligned nodes, exactly as the recursion combines them.
+__device__ double prefix_reduce(const double* tree, int64_t cap, int64_t end) {
+  double terms[64];
+  int nt = 0;
+  int64_t node = 1, ns = 0, ne = cap - 1;
+  while (true) {
+    if (end == ne) {
+      terms[nt++] = tree[node];
+      break;
+    }
+    const int64_t mid = (ns + ne) / 2;
+    if (end <= mid) {
+      node = 2 * node;
+      ne = mid;
+    } else {
+      terms[nt++] = tree[2 * node];
+      node = 2 * node + 1;
+      ns = mid + 1;
+    }
+  }
+  double r = terms[nt - 1];
+  for (int k = nt - 2; k >= 0; --k) r = terms[k] + r;
+  return r;
+}
+
+__global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __restrict__ sum_tree,
+                                                           const double* __restrict__ min_tree, int64_t cap,
+                                                           int64_t max_idx, double beta,
+                                                           const double* __restrict__ uniforms, int B,
+                                                           int32_t* __restrict__ idx_out, float* __restrict__ w_out,
+                                                           double* __restrict__ exp_counter) {
+  __shared__ double seg_s, total_s, maxw_s;
+  __shared__ int32_t idx_s[PER_MAX_B];
+  if (threadIdx.x == 0) {
+    const double p_total = prefix_reduce(sum_tree, cap, max_idx - 2);  // sum(0, max_idx - 1)
+    seg_s = p_total / B;
+    total_s = sum_tree[1];
+    const double p_min = min_tree[1] / total_s;
+    maxw_s = pow(p_min * (double)max_idx, -beta);
+  }
+  __syncthreads();
+  const double seg = seg_s, total = total_s, maxw = maxw_s;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    double p = uniforms[i] * seg + i * seg;
+    int64_t node = 1;
+    while (node < cap) {
+      if (sum_tree[2 * node] > p) {
+        node = 2 * node;
+      } else {
+        p -= sum_tree[2 * node];
+        node = 2 * node + 1;
+      }
+    }
+    const int32_t id = (int32_t)(node - cap);
+    idx_s[i] = id;
+    idx_out[i] = id;
+    const double pr = sum_tree[node] / total;
+    w_out[i] = (float)(pow(pr * (double)max_idx, -beta) / maxw);
+  }
+  __syncthreads();
+  // exp_counter[idxes] += 1: numpy fancy-index increment counts each distinct index once.
+  double old[PER_MAX_B / PER_THREADS];
+  int k = 0;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) old[k++] = exp_counter ? exp_counter[idx_s[i]] : 0.0;
+  __syncthreads();
+  k = 0;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    if (exp_counter) exp_counter[idx_s[i]] = old[k] + 1.0;
+    ++k;
+  }
+}
+
+// Leaf writes with last-write-wins among duplicates, then ancestor refresh level by level.
+__global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, double* min_tree, int64_t cap,
+                                                        const int32_t* __restrict__ idx, const double* __restrict__ vals,
+                                                        int n, const float* __restrict__ y, const float* __restrict__ V,
+                                                        const double* __restrict__ exp_counter, double fresh, double eps,
+                                                        double alpha, double* max_priority) {
+  __shared__ int32_t id_s[PER_MAX_B];
+  __shared__ double maxp_s[PER_THREADS];
+  double my_max = -__builtin_inf();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) id_s[i] = idx[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    double leaf;
+    if (vals) {
+      leaf = vals[i];
+    } else {
+      // p = fresh^count * |y - V| + eps evaluated as TF would (float32 tensors), leaf = p^alpha
+      const float td = fabsf(__fsub_rn(y[i], V[i]));
+      const float fd = (float)pow(fresh, exp_counter[id_s[i]]);
+      const float p = __fadd_rn(__fmul_rn(fd, td), (float)eps);
+      my_max = fmax(my_max, (double)p);
+      leaf = pow((double)p, alpha);
+    }
+    bool last = true;
+    for (int j = i + 1; j < n; ++j)
+      if (id_s[j] == id_s[i]) {
+        last = false;
+        break;
+      }
+    if (last) {
+      sum_tree[cap + id_s[i]] = leaf;
+      min_tree[cap + id_s[i]] = leaf;
+    }
+  }
+  if (max_priority) {
+    maxp_s[threadIdx.x] = my_max;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double m = max_priority[0];
+      for (int t = 0; t < (int)blockDim.x; ++t) m = fmax(m, maxp_s[t]);
+      max_priority[0] = m;
+    }
+  }
+  __syncthreads();
+  __threadfence_block();
+  // ancestors: every thread walks its leaf's path one level per barrier
+  int64_t nodes[PER_MAX_B / PER_THREADS];
+  int k = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) nodes[k++] = (cap + id_s[i]) >> 1;
+  while (true) {
+    bool any = false;
+    k = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x, ++k) {
+      const int64_t nd = nodes[k];
+      if (nd >= 1) {
+        sum_tree[nd] = sum_tree[2 * nd] + sum_tree[2 * nd + 1];
+        min_tree[nd] = tree_min(min_tree[2 * nd], min_tree[2 * nd + 1]);
+        nodes[k] = nd >> 1;
+        any = true;
+      }
+    }
+    __syncthreads();
+    __threadfence_block();
+    if (!__syncthreads_or(any)) break;
+  }
+}
+
+}  // namespace cacto
+
+using namespace cacto;
+
+static bool pow2(int64_t c) { return c > 0 && (c & (c - 1)) == 0; }
+
+extern "C" int cacto_per_init(double* sum_tree_d, double* min_tree_d, int64_t capacity, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && pow2(capacity), "cacto_per_init: capacity must be a power of two");
+  hipLaunchKernelGGL(k_per_init, dim3((unsigned)std::min<int64_t>((2 * capacity + 255) / 256, 4096)), dim3(256), 0,
+                     as_stream(stream), sum_tree_d, min_tree_d, 2 * capacity);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
+                                   int64_t start, int64_t n, double value, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && pow2(capacity) && ring_size > 0 && ring_size <= capacity && n >= 0 &&
+                    start >= 0 && start < ring_size,
+                "cacto_per_set_range: bad arguments");
+  if (n == 0) return CACTO_OK;
+  hipStream_t st = as_stream(stream);
+  n = std::min(n, ring_size);
+  hipLaunchKernelGGL(k_per_fill_leaves, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                     sum_tree_d, min_tree_d, capacity, ring_size, start, n, value);
+  CACTO_CHECK_HIP(hipGetLastError());
+  // affected leaf interval(s); refresh the covering node interval per level (superset is harmless)
+  const int64_t a = start, b = start + n - 1;
+  int64_t lo = capacity + (b < ring_size ? a : 0), hi = capacity + (b < ring_size ? b : ring_size - 1);
+  while (lo > 1) {
+    lo >>= 1;
+    hi >>= 1;
+    const int64_t cnt = hi - lo + 1;
+    hipLaunchKernelGGL(k_per_level, dim3((unsigned)std::min<int64_t>((cnt + 255) / 256, 4096)), dim3(256), 0, st,
+                       sum_tree_d, min_tree_d, lo, hi);
+    CACTO_CHECK_HIP(hipGetLastError());
+  }
+  return CACTO_OK;
+}
+
+extern "C" int cacto_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
+                                double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
+                                double* exp_counter_d, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && uniforms_d && idx_d && is_w_d && pow2(capacity),
+                "cacto_per_sample: bad arguments");
+  CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_sample: 0 < B <= 8192");
+  // max_idx <= 1 makes the reference's sum(0, max_idx - 1) recurse past the leaves (segment_tree.py:36-49)
+  CACTO_REQUIRE(max_idx >= 2 && max_idx <= capacity, "cacto_per_sample: need 2 <= max_idx <= capacity");
+  hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
+                     max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                                const float* y_d, const float* V_d, const double* exp_counter_d, double fresh_factor,
+                                double eps, double alpha, double* max_priority_d, int B, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && y_d && V_d && exp_counter_d && max_priority_d && pow2(capacity),
+                "cacto_per_update: bad arguments");
+  CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_update: 0 < B <= 8192");
+  hipLaunchKernelGGL(k_per_set, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
+                     idx_d, nullptr, B, y_d, V_d, exp_counter_d, fresh_factor, eps, alpha, max_priority_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_per_set_leaves(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                                    const double* values_d, int n, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && values_d && pow2(capacity), "cacto_per_set_leaves: bad arguments");
+  CACTO_REQUIRE(n > 0 && n <= PER_MAX_B, "cacto_per_set_leaves: 0 < n <= 8192");
+  hipLaunchKernelGGL(k_per_set, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
+                     idx_d, values_d, n, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0, nullptr);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}

@@ -1,0 +1,165 @@
+"""Actor/critic networks with the reference surface (NeuralNetwork.py:10-233), on the HIP kernels.
+
+A model is a `Net`: one device "net buffer" [flat Keras-order params | MFMA-packed fragments]
+(include/cacto_hip.h). NN.eval / compute_critic_grad / compute_actor_grad call the fused kernels;
+the training loop (cacto_amd.rl.RL_AC) uses the fused `cacto_update` directly on replay rows.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .system import DEVICE, dptr, stream
+
+ACTOR, CRITIC = L.CACTO_NET_ACTOR, L.CACTO_NET_CRITIC
+
+
+def layer_shapes(kind, ns, na):
+    if kind == ACTOR:  # NeuralNetwork.py:51-63
+        dims = [ns, 256, 256, na]
+    else:              # NeuralNetwork.py:95-108 (critic_type 'sine', every shipped config)
+        dims = [ns, 64, 64, 128, 128, 1]
+    shapes = []
+    for i, o in zip(dims[:-1], dims[1:]):
+        shapes += [(i, o), (o,)]
+    return shapes
+
+
+class Net:
+    """Keras-model stand-in: weights live on the device in the net-buffer layout."""
+
+    def __init__(self, sys, kind):
+        self.sys = sys
+        self.kind = kind
+        self.shapes = layer_shapes(kind, sys.ns, sys.na)
+        self.P = sys.param_count(kind)
+        assert self.P == sum(int(np.prod(s)) for s in self.shapes)
+        self.buf = torch.zeros(sys.netbuf_floats(kind), dtype=torch.float32, device=DEVICE)
+
+    @property
+    def flat(self):
+        return self.buf[:self.P]
+
+    def pack(self):
+        L.lib().call("cacto_mlp_pack", self.sys.handle, self.kind, dptr(self.buf), stream())
+
+    def set_weights(self, weights):
+        flat = np.concatenate([np.asarray(w, dtype=np.float32).reshape(-1) for w in weights])
+        if flat.size != self.P:
+            raise ValueError("expected %d parameters, got %d" % (self.P, flat.size))
+        self.flat.copy_(torch.from_numpy(flat))
+        self.pack()
+
+    def get_weights(self):
+        flat = self.flat.detach().cpu().numpy()
+        out, off = [], 0
+        for s in self.shapes:
+            n = int(np.prod(s))
+            out.append(flat[off:off + n].reshape(s).copy())
+            off += n
+        return out
+
+    def copy_from(self, other):
+        self.buf.copy_(other.buf)
+
+    def save_weights(self, path):
+        np.savez(path, *self.get_weights())
+
+    def load_weights(self, path):
+        z = np.load(path)
+        self.set_weights([z["arr_%d" % i] for i in range(len(self.shapes))])
+
+
+def init_weights(kind, ns, na, rng):
+    """Keras initialisers: Glorot-uniform kernels / zero biases for Dense; tf_siren
+    SinusodialRepresentationDense (w0 = 1, c = 6): kernel U(+-sqrt(6/fan_in)), bias he_uniform
+    U(+-sqrt(6/units))."""
+    ws = []
+    shapes = layer_shapes(kind, ns, na)
+    for li in range(0, len(shapes), 2):
+        fi, fo = shapes[li]
+        siren = kind == CRITIC and li < 8
+        lim = np.sqrt(6.0 / fi) if siren else np.sqrt(6.0 / (fi + fo))
+        ws.append(rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32))
+        b = rng.uniform(-np.sqrt(6.0 / fo), np.sqrt(6.0 / fo), size=fo) if siren else np.zeros(fo)
+        ws.append(b.astype(np.float32))
+    return ws
+
+
+class NN:
+    """NeuralNetwork.py:10-233 surface."""
+
+    def __init__(self, env, conf, w_S=0, seed=0):
+        self.env = env
+        self.conf = conf
+        self.w_S = w_S
+        self.sys = env.sys
+        self.rng = np.random.default_rng(seed)
+
+    def create_actor(self):
+        net = Net(self.sys, ACTOR)
+        net.set_weights(init_weights(ACTOR, self.sys.ns, self.sys.na, self.rng))
+        return net
+
+    def create_critic_sine(self):
+        net = Net(self.sys, CRITIC)
+        net.set_weights(init_weights(CRITIC, self.sys.ns, self.sys.na, self.rng))
+        return net
+
+    def create_critic_elu(self):
+        raise NotImplementedError("critic_type 'elu' is outside the hot path (every conf uses 'sine')")
+
+    create_critic_sine_elu = create_critic_elu
+    create_critic_relu = create_critic_elu
+
+    # ---- NeuralNetwork.py:130-138 ----
+    def eval(self, model, x):
+        S = torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x,
+                            dtype=torch.float32, device=DEVICE).contiguous()
+        if S.dim() == 1:
+            S = S[None]
+        B = S.shape[0]
+        if model.kind == ACTOR:
+            out = torch.empty(B, self.sys.na, dtype=torch.float32, device=DEVICE)
+            L.lib().call("cacto_actor_forward", self.sys.handle, dptr(model.buf), dptr(S), dptr(out), B, stream())
+            return out
+        out = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        L.lib().call("cacto_critic_forward", self.sys.handle, dptr(model.buf), dptr(S), dptr(out), B, stream())
+        return out.reshape(B, 1)
+
+    def critic_input_grad(self, model, x):
+        """tape.gradient(V(s), s) for a batch (NeuralNetwork.py:162-165, :190-195)."""
+        S = torch.as_tensor(x, dtype=torch.float32, device=DEVICE).contiguous()
+        B = S.shape[0]
+        V = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        g = torch.empty(B, self.sys.ns, dtype=torch.float32, device=DEVICE)
+        L.lib().call("cacto_critic_input_grad", self.sys.handle, dptr(model.buf), dptr(S), dptr(V), dptr(g), B,
+                     stream())
+        return V.reshape(B, 1), g
+
+    # ---- gradients on explicit tensors (the training loop uses replay rows directly) ----
+    @staticmethod
+    def _rows(state, R, state_next, dVdx, d, term):
+        f = lambda x: torch.as_tensor(x, device=DEVICE).to(torch.float64).reshape(len(state), -1)
+        return torch.cat([f(state), f(R), f(state_next), f(dVdx), f(d), f(term)], dim=1).contiguous()
+
+    def compute_critic_grad(self, learner, state_batch, state_next_rollout_batch, partial_reward_to_go_batch,
+                            dVdx_batch, d_batch, weights_batch, term_batch=None):
+        """NeuralNetwork.py:150-178. Returns (grads [Keras order], y [B,1], V [B,1], V_tgt(s) [B,1]).
+        `learner` is the RL_AC holding the critic/target/optimizer state."""
+        B = len(state_batch)
+        term = np.zeros(B) if term_batch is None else term_batch
+        rows = self._rows(state_batch, partial_reward_to_go_batch, state_next_rollout_batch, dVdx_batch, d_batch,
+                          term)
+        idx = torch.arange(B, dtype=torch.int32, device=DEVICE)
+        w = torch.as_tensor(weights_batch, dtype=torch.float32, device=DEVICE).reshape(B).contiguous()
+        return learner.critic_grad_rows(rows, idx, w)
+
+    def compute_actor_grad(self, learner, state_batch, term_batch, batch_size=None):
+        """NeuralNetwork.py:180-233 (uses the learner's current critic)."""
+        B = len(state_batch)
+        z = np.zeros((B, self.sys.ns))
+        rows = self._rows(state_batch, np.zeros(B), z, z, np.zeros(B), term_batch)
+        idx = torch.arange(B, dtype=torch.int32, device=DEVICE)
+        return learner.actor_grad_rows(rows, idx, batch_size or B)

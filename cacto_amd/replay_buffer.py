@@ -1,0 +1,149 @@
+"""Replay buffers with the reference surface (replay_buffer.py:9-240), device-resident.
+
+Storage is the reference's float64 row layout [s | R | s_next | dVdx | d | term] (3ns+3 columns,
+replay_buffer.py:20) in HBM; sampling gathers rows on the GPU (or the update kernels read them in
+place by index). The prioritized buffer keeps float64 sum/min segment trees on the GPU with the
+reference's node layout and combination order (segment_tree.py) so sampled indices are bit-exact.
+"""
+import random
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .system import DEVICE, dptr, stream
+
+
+class ReplayBuffer:
+    prioritized = False
+
+    def __init__(self, conf, sys):
+        self.conf = conf
+        self.sys = sys
+        self.N = conf.REPLAY_SIZE
+        self.ns = conf.nb_state
+        self.cols = 3 * self.ns + 3
+        self.storage = torch.zeros(self.N, self.cols, dtype=torch.float64, device=DEVICE)
+        self.next_idx = 0
+        self.full = 0
+        self.np_rng = np.random  # the reference draws from the global numpy RNG (unseeded)
+
+    @staticmethod
+    def concatenate_sample(obses_t, rewards, obses_t1, dVdxs, dones, terms):
+        """replay_buffer.py:63-72."""
+        cat = lambda xs: np.concatenate(xs, axis=0)
+        return np.concatenate((cat(obses_t), cat(rewards).reshape(-1, 1), cat(obses_t1), cat(dVdxs),
+                               cat(dones).reshape(-1, 1), cat(terms).reshape(-1, 1)), axis=1)
+
+    def add_rows(self, rows):
+        rows = torch.as_tensor(rows, dtype=torch.float64, device=DEVICE).contiguous()
+        n = rows.shape[0]
+        if n == 0:
+            return
+        if n > self.N:
+            raise ValueError("cannot add more rows than REPLAY_SIZE at once")
+        L.lib().call("cacto_buffer_add", self.sys.handle, dptr(self.storage), self.N, self.next_idx, dptr(rows), n,
+                     stream())
+        if n + self.next_idx > self.N:
+            self.full = 1
+        self.next_idx = (self.next_idx + n) % self.N
+
+    def add(self, obses_t, rewards, obses_t1, dVdxs, dones, terms):
+        """replay_buffer.py:25-36."""
+        self.add_rows(self.concatenate_sample(obses_t, rewards, obses_t1, dVdxs, dones, terms))
+
+    def max_idx(self):
+        return self.N if self.full else self.next_idx
+
+    def sample_indices(self, n, rng=None):
+        """n batches of indices in one draw (int32, device)."""
+        r = self.np_rng if rng is None else rng
+        idx = r.randint(0, self.max_idx(), size=(n, self.conf.BATCH_SIZE)) if hasattr(r, "randint") else \
+            r.integers(0, self.max_idx(), size=(n, self.conf.BATCH_SIZE))
+        return torch.as_tensor(idx.astype(np.int32), device=DEVICE)
+
+    def gather(self, idx):
+        B = idx.shape[0]
+        ns = self.ns
+        f32 = dict(dtype=torch.float32, device=DEVICE)
+        s, r, sn, dv, d = (torch.empty(B, ns, **f32), torch.empty(B, 1, **f32), torch.empty(B, ns, **f32),
+                           torch.empty(B, ns, **f32), torch.empty(B, 1, **f32))
+        term = torch.empty(B, 1, dtype=torch.float64, device=DEVICE)
+        L.lib().call("cacto_buffer_gather", self.sys.handle, dptr(self.storage), dptr(idx, torch.int32), B, dptr(s),
+                     dptr(r), dptr(sn), dptr(dv), dptr(d), dptr(term), stream())
+        return s, r, sn, dv, d, term
+
+    def sample(self, idx=None):
+        """replay_buffer.py:38-61: (s, R, s_next, dVdx, d, term, weights, None)."""
+        if idx is None:
+            idx = self.sample_indices(1)[0]
+        s, r, sn, dv, d, term = self.gather(idx)
+        w = torch.ones(idx.shape[0], 1, dtype=torch.float32, device=DEVICE)
+        return s, r, sn, dv, d, term, w, None
+
+
+class PrioritizedReplayBuffer(ReplayBuffer):
+    """replay_buffer.py:87-218 (with the three shipped crash bugs fixed — DESIGN.md §PER)."""
+    prioritized = True
+
+    def __init__(self, conf, sys, py_random=None):
+        super().__init__(conf, sys)
+        cap = 1
+        while cap < self.N:
+            cap *= 2
+        self.cap = cap
+        self.sum_tree = torch.empty(2 * cap, dtype=torch.float64, device=DEVICE)
+        self.min_tree = torch.empty(2 * cap, dtype=torch.float64, device=DEVICE)
+        L.lib().call("cacto_per_init", dptr(self.sum_tree), dptr(self.min_tree), cap, stream())
+        self.max_priority = torch.ones(1, dtype=torch.float64, device=DEVICE)
+        self.exp_counter = torch.zeros(self.N, dtype=torch.float64, device=DEVICE)
+        self.alpha = float(conf.prioritized_replay_alpha)
+        self.beta = float(conf.prioritized_replay_beta)
+        self.eps = float(conf.prioritized_replay_eps)
+        self.fresh = float(conf.fresh_factor)
+        self.random = py_random or random  # replay_buffer.py:150 uses the global `random`
+
+    def add_rows(self, rows):
+        start = self.next_idx
+        n = len(rows)
+        super().add_rows(rows)
+        # leaves = max_priority ** alpha (replay_buffer.py:133-135); max_priority read on the host
+        leaf = float(self.max_priority.item()) ** self.alpha
+        L.lib().call("cacto_per_set_range", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.N, start, n,
+                     leaf, stream())
+
+    def sample_device(self, uniforms=None):
+        """_sample_proportional + IS weights + exp_counter (replay_buffer.py:139-188)."""
+        B = self.conf.BATCH_SIZE
+        if uniforms is None:
+            uniforms = [self.random.random() for _ in range(B)]
+        u = torch.as_tensor(np.asarray(uniforms, dtype=np.float64), device=DEVICE)
+        idx = torch.empty(B, dtype=torch.int32, device=DEVICE)
+        w = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        L.lib().call("cacto_per_sample", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.max_idx(),
+                     self.beta, dptr(u), B, dptr(idx), dptr(w), dptr(self.exp_counter), stream())
+        return idx, w
+
+    def sample(self, uniforms=None):
+        idx, w = self.sample_device(uniforms)
+        s, r, sn, dv, d, term = self.gather(idx)
+        return s, r, sn, dv, d, term, w.reshape(-1, 1), idx
+
+    def update_priorities_device(self, idx, y, V):
+        B = idx.shape[0]
+        L.lib().call("cacto_per_update", dptr(self.sum_tree), dptr(self.min_tree), self.cap, dptr(idx, torch.int32),
+                     dptr(y.reshape(-1).contiguous(), torch.float32), dptr(V.reshape(-1).contiguous(), torch.float32),
+                     dptr(self.exp_counter), self.fresh, self.eps, self.alpha, dptr(self.max_priority), B, stream())
+
+    def update_priorities(self, idxes, reward_to_go_batch, critic_value, target_critic_value=None):
+        """replay_buffer.py:190-218 ('PER')."""
+        idx = torch.as_tensor(np.asarray(idxes, dtype=np.int32) if not isinstance(idxes, torch.Tensor) else idxes,
+                              dtype=torch.int32, device=DEVICE).contiguous()
+        self.update_priorities_device(idx, torch.as_tensor(reward_to_go_batch, device=DEVICE),
+                                      torch.as_tensor(critic_value, device=DEVICE))
+
+    def set_leaves(self, idx, values):
+        idx = torch.as_tensor(np.asarray(idx, dtype=np.int32), device=DEVICE)
+        v = torch.as_tensor(np.asarray(values, dtype=np.float64), device=DEVICE)
+        L.lib().call("cacto_per_set_leaves", dptr(self.sum_tree), dptr(self.min_tree), self.cap, dptr(idx), dptr(v),
+                     len(idx), stream())

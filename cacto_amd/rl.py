@@ -1,0 +1,263 @@
+"""RL_AC with the reference surface (RL.py:6-233) on the HIP kernels.
+
+The update hot loop (learn_and_update, RL.py:120-143) runs entirely on the device: per iteration
+one `cacto_update` (critic chain -> weight-grad GEMM -> Adam + soft target update -> actor chain
+-> weight-grad GEMM -> Adam), reading replay rows in place by index. Indices for the whole loop
+are drawn up front (the reference draws them with the unseeded global numpy RNG,
+replay_buffer.py:45) and copied once, so the loop enqueues work with no host synchronisation.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .neural_network import ACTOR, CRITIC, Net
+from .system import DEVICE, dptr, stream
+
+
+class RL_AC:
+    def __init__(self, env, NN, conf, N_try=0, w_S=None):
+        self.env = env
+        self.NN = NN
+        self.conf = conf
+        self.N_try = N_try
+        self.sys = env.sys
+        self.w_S = NN.w_S if w_S is None else w_S
+        self.actor_model = None
+        self.critic_model = None
+        self.target_critic = None
+        self.NSTEPS_SH = 0
+        self._ws = None
+        self._ws_B = 0
+
+    # ---- RL.py:61-99 ----
+    def setup_model(self, recover_training=None, weights=None):
+        """`weights`: optional dict {'actor', 'critic', 'target'} of Keras-order arrays (e.g. the
+        .h5-derived fixtures) instead of fresh initialisers."""
+        self.actor_model = self.NN.create_actor()
+        self.critic_model = self.NN.create_critic_sine()
+        self.target_critic = Net(self.sys, CRITIC)
+        if weights is not None:
+            self.actor_model.set_weights(weights["actor"])
+            self.critic_model.set_weights(weights["critic"])
+            self.target_critic.set_weights(weights.get("target", weights["critic"]))
+        elif recover_training is not None:
+            path, n_try, step = recover_training
+            self.actor_model.load_weights("%s/N_try_%s/actor_%s.npz" % (path, n_try, step))
+            self.critic_model.load_weights("%s/N_try_%s/critic_%s.npz" % (path, n_try, step))
+            self.target_critic.load_weights("%s/N_try_%s/target_critic_%s.npz" % (path, n_try, step))
+        else:
+            self.target_critic.copy_from(self.critic_model)       # RL.py:99
+        f32 = dict(dtype=torch.float32, device=DEVICE)
+        self.actor_m = torch.zeros(self.actor_model.P, **f32)
+        self.actor_v = torch.zeros(self.actor_model.P, **f32)
+        self.critic_m = torch.zeros(self.critic_model.P, **f32)
+        self.critic_v = torch.zeros(self.critic_model.P, **f32)
+        self.steps = torch.zeros(2, dtype=torch.int32, device=DEVICE)  # Keras optimizer iterations
+        self.nets = L.Nets(self.actor_model.buf.data_ptr(), self.actor_m.data_ptr(), self.actor_v.data_ptr(),
+                           self.critic_model.buf.data_ptr(), self.critic_m.data_ptr(), self.critic_v.data_ptr(),
+                           self.target_critic.buf.data_ptr(), self.steps.data_ptr())
+        self.cfg = self.make_cfg()
+
+    def make_cfg(self, B_global=None):
+        c = self.conf
+        cfg = L.UpdateCfg()
+        cfg.w_S = float(self.w_S)
+        cfg.tau = float(c.UPDATE_RATE)
+        cfg.beta1, cfg.beta2, cfg.epsilon = 0.9, 0.999, 1e-7        # Keras Adam defaults
+        if c.LR_SCHEDULE:                                          # PiecewiseConstantDecay, RL.py:80-85
+            for k in range(5):
+                cfg.critic_lr[k] = c.values_schedule_LR_C[k]
+                cfg.actor_lr[k] = c.values_schedule_LR_A[k]
+            for k in range(4):
+                cfg.lr_bounds[k] = c.boundaries_schedule_LR_C[k]
+        else:
+            for k in range(5):
+                cfg.critic_lr[k] = c.CRITIC_LEARNING_RATE
+                cfg.actor_lr[k] = c.ACTOR_LEARNING_RATE
+            for k in range(4):
+                cfg.lr_bounds[k] = float("inf")
+        cfg.MC = int(c.MC)
+        cfg.B_global = int(B_global or c.BATCH_SIZE)
+        cfg.want_target_V = 0
+        return cfg
+
+    def workspace(self, B):
+        if self._ws is None or self._ws_B < B:
+            nbytes = self.sys.workspace_bytes(B)
+            self._ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=DEVICE)
+            self._ws_B = B
+        return self._ws
+
+    def _cfg_for(self, B, want_vt=False):
+        cfg = L.UpdateCfg.from_buffer_copy(self.cfg)
+        if self.cfg.B_global <= 0 or getattr(self, "_dp_world", 1) == 1:
+            cfg.B_global = B
+        cfg.want_target_V = int(want_vt)
+        return cfg
+
+    # ---- gradient pieces (explicit rows; used by the DP path and the parity tests) ----
+    def critic_grad_rows(self, rows, idx, w=None, want_vt=True):
+        B = idx.shape[0]
+        ws = self.workspace(B)
+        grad = torch.empty(self.critic_model.P, dtype=torch.float32, device=DEVICE)
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        V = torch.empty_like(y)
+        Vt = torch.empty_like(y)
+        cfg = self._cfg_for(B, want_vt)
+        L.lib().call("cacto_critic_grad", self.sys.handle, C.byref(self.nets), C.byref(cfg),
+                     dptr(rows, torch.float64), dptr(idx, torch.int32), dptr(w), B, dptr(grad), dptr(y), dptr(V),
+                     dptr(Vt), dptr(ws), ws.numel() * 4, stream())
+        return self._split(grad, self.critic_model), y.reshape(B, 1), V.reshape(B, 1), Vt.reshape(B, 1)
+
+    def actor_grad_rows(self, rows, idx, batch_size=None):
+        B = idx.shape[0]
+        ws = self.workspace(B)
+        grad = torch.empty(self.actor_model.P, dtype=torch.float32, device=DEVICE)
+        cfg = self._cfg_for(batch_size or B)
+        L.lib().call("cacto_actor_grad", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(rows, torch.float64),
+                     dptr(idx, torch.int32), B, dptr(grad), dptr(ws), ws.numel() * 4, stream())
+        return self._split(grad, self.actor_model)
+
+    @staticmethod
+    def _split(flat, net):
+        out, off = [], 0
+        for s in net.shapes:
+            n = int(np.prod(s))
+            out.append(flat[off:off + n].reshape(s))
+            off += n
+        return out
+
+    def apply_gradients(self, which, flat_grad, soft_update=False):
+        """optimizer.apply_gradients (RL.py:105/:109) for a flat gradient (after the grad call that
+        advanced the iteration counter)."""
+        L.lib().call("cacto_adam_step", self.sys.handle, C.byref(self.nets), C.byref(self.cfg), which,
+                     dptr(flat_grad.contiguous(), torch.float32), int(soft_update), stream())
+
+    # ---- RL.py:101-111 on replay rows ----
+    def update_rows(self, storage, idx, is_w=None, y=None, V=None, Vt=None):
+        B = idx.shape[0]
+        ws = self.workspace(B)
+        cfg = self._cfg_for(B, Vt is not None)
+        L.lib().call("cacto_update", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(storage, torch.float64),
+                     dptr(idx, torch.int32), dptr(is_w), B, dptr(y), dptr(V), dptr(Vt), dptr(ws), ws.numel() * 4,
+                     stream())
+
+    def update(self, state_batch, state_next_rollout_batch, partial_reward_to_go_batch, dVdx_batch, d_batch,
+               term_batch, weights_batch, batch_size=None):
+        """RL.py:101-111 surface on explicit tensors (+ update_target, which learn_and_update would
+        call next). Returns (reward_to_go, critic_value, target_critic_value)."""
+        B = len(state_batch)
+        rows = self.NN._rows(state_batch, partial_reward_to_go_batch, state_next_rollout_batch, dVdx_batch, d_batch,
+                             term_batch)
+        idx = torch.arange(B, dtype=torch.int32, device=DEVICE)
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        V, Vt = torch.empty_like(y), torch.empty_like(y)
+        w = torch.as_tensor(weights_batch, dtype=torch.float32, device=DEVICE).reshape(B).contiguous()
+        self.update_rows(rows, idx, w, y, V, Vt)
+        return y.reshape(B, 1), V.reshape(B, 1), Vt.reshape(B, 1)
+
+    def update_target(self, target_weights=None, weights=None):
+        """RL.py:113-118 (standalone; cacto_update already fuses it into the critic Adam step)."""
+        L.lib().call("cacto_soft_update", self.sys.handle, C.byref(self.nets), float(self.conf.UPDATE_RATE), stream())
+
+    # ---- RL.py:120-143 ----
+    def learn_and_update(self, update_step_counter, buffer, ep, rng=None):
+        n = int(self.conf.UPDATE_LOOPS[ep])
+        B = self.conf.BATCH_SIZE
+        per = getattr(buffer, "prioritized", False)
+        if per:
+            for _ in range(n):
+                idx, w = buffer.sample_device()
+                y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+                V = torch.empty_like(y)
+                self.update_rows(buffer.storage, idx, w, y, V)
+                buffer.update_priorities_device(idx, y, V)
+                update_step_counter = self._after_step(update_step_counter)
+            return update_step_counter
+        idx_all = buffer.sample_indices(n, rng)                  # [n, B] int32 on device
+        for i in range(n):
+            self.update_rows(buffer.storage, idx_all[i])
+            update_step_counter = self._after_step(update_step_counter)
+        return update_step_counter
+
+    def _after_step(self, counter):
+        counter += 1
+        if counter % self.conf.save_interval == 0 and getattr(self.conf, "NNs_path", None):
+            self.RL_save_weights(counter)
+        return counter
+
+    # ---- RL.py:145-189 (host, float64 as the reference) ----
+    def RL_Solve(self, TO_controls, TO_states, TO_step_cost):
+        T = self.NSTEPS_SH
+        rwrd = -np.asarray(TO_step_cost, dtype=np.float64)
+        ns = self.conf.nb_state
+        s_next = np.zeros((T + 1, ns))
+        partial = np.empty(T + 1)
+        total = np.empty(T + 1)
+        term = np.zeros(T + 1)
+        term[-1] = 1
+        done = np.zeros(T + 1)
+        for i in range(T + 1):
+            if self.conf.MC:
+                final = T
+                done[i] = 1
+            else:
+                final = min(i + self.conf.nsteps_TD_N, T)
+                if final == T:
+                    done[i] = 1
+                else:
+                    s_next[i, :] = TO_states[final + 1, :]
+            partial[i] = np.float32(sum(rwrd[i:final + 1]))
+            total[i] = np.float32(sum(rwrd[i:T + 1]))
+        ep_return = sum(rwrd)
+        return TO_states, partial, total, s_next, done, rwrd, term, ep_return, None
+
+    def RL_save_weights(self, update_step_counter='final'):
+        base = "%s/N_try_%s/" % (self.conf.NNs_path, self.N_try)
+        self.actor_model.save_weights(base + "actor_%s.npz" % update_step_counter)
+        self.critic_model.save_weights(base + "critic_%s.npz" % update_step_counter)
+        self.target_critic.save_weights(base + "target_critic_%s.npz" % update_step_counter)
+
+    # ---- RL.py:197-233, batched over episodes on the GPU ----
+    def rollout_batch(self, S0, nsteps, T, ep=1, weights=None, want=("S", "A", "R", "EE")):
+        """Roll out len(S0) episodes in one persistent kernel (K18)."""
+        S0 = torch.as_tensor(np.asarray(S0, dtype=np.float64), device=DEVICE).contiguous()
+        R = S0.shape[0]
+        ns, na = self.conf.nb_state, self.conf.nb_action
+        n = torch.as_tensor(np.asarray(nsteps, dtype=np.int32), device=DEVICE).contiguous()
+        f64 = dict(dtype=torch.float64, device=DEVICE)
+        out = {}
+        if "S" in want:
+            out["S"] = torch.empty(R, T + 1, ns, **f64)
+        if "A" in want:
+            out["A"] = torch.empty(R, T, na, dtype=torch.float32, device=DEVICE)
+        if "R" in want:
+            out["R"] = torch.empty(R, T, **f64)
+        if "EE" in want:
+            out["EE"] = torch.empty(R, T + 1, 3, **f64)
+        out["status"] = torch.empty(R, dtype=torch.int32, device=DEVICE)
+        W = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float64), device=DEVICE)
+        L.lib().call("cacto_rollout", self.sys.handle, dptr(self.actor_model.buf), dptr(S0), dptr(n), T,
+                     int(ep != 0), dptr(W), dptr(out.get("S")), dptr(out.get("A")), dptr(out.get("R")),
+                     dptr(out.get("EE")), dptr(out["status"]), R, stream())
+        return out
+
+    def nsteps_sh(self, s0):
+        return self.conf.NSTEPS - int(s0[-1] / self.conf.dt)
+
+    def create_TO_init(self, ep, ICS):
+        """RL.py:197-233 for one episode."""
+        self.init_rand_state = ICS
+        self.NSTEPS_SH = self.nsteps_sh(ICS)
+        if self.NSTEPS_SH == 0:
+            return None, None, None, None, 0
+        T = self.NSTEPS_SH
+        out = self.rollout_batch(np.asarray(ICS)[None], [T], T, ep=ep, want=("S", "A"))
+        if int(out["status"][0].item()) != 0:
+            return None, None, None, None, 0
+        states = out["S"][0].cpu().numpy()
+        controls = out["A"][0].double().cpu().numpy()
+        return self.init_rand_state, states, controls, self.NSTEPS_SH, 1

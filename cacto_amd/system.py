@@ -1,0 +1,106 @@
+"""System handle: packs a conf_*.py module into `cacto_sys_params` (include/cacto_hip.h) and owns
+the `cacto_sys` handle every HIP entry point takes. Also the tensor-contract helpers of the
+ctypes boundary (device, dtype, contiguity, shape checks)."""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+DEVICE = "cuda"
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("cacto_amd needs an MI355X (HIP device); none is visible — there is no CPU path")
+
+
+def dptr(t, dtype=None, shape=None, name="tensor"):
+    """Device pointer of a contiguous CUDA tensor after checking the contract."""
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError("%s must be a CUDA (HIP) tensor" % name)
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError("%s must be %s, got %s" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError("%s must have shape %s, got %s" % (name, tuple(shape), tuple(t.shape)))
+    return C.c_void_p(t.data_ptr())
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _fill(arr, values):
+    for i, v in enumerate(values):
+        arr[i] = float(v)
+
+
+class System:
+    """Numeric content of a conf module + the device copy the kernels read."""
+
+    def __init__(self, conf):
+        require_gpu()
+        self.conf = conf
+        p = L.SysParams()
+        sid = conf.system_id
+        robot = getattr(conf, "robot", None)
+        if sid == "single_integrator":
+            p.dyn_kind, p.reward_kind = L.CACTO_DYN_SINGLE_INTEGRATOR, L.CACTO_REW_PLANAR
+        elif robot is not None and sid in ("double_integrator", "manipulator"):
+            p.dyn_kind = L.CACTO_DYN_CHAIN
+            p.reward_kind = L.CACTO_REW_MANIPULATOR if sid == "manipulator" else L.CACTO_REW_PLANAR
+        else:
+            raise NotImplementedError("system %r is not in this build's hot path yet" % sid)
+        p.nb_state, p.nb_action = conf.nb_state, conf.nb_action
+        p.nq = conf.nq or 0
+        p.nv = conf.nv or 0
+        p.normalize = int(conf.NORMALIZE_INPUTS)
+        p.n_weights = len(conf.cost_weights_running)
+        p.dt = conf.dt
+        _fill(p.state_norm, conf.state_norm_arr)
+        _fill(p.u_max, conf.u_max)
+        p.w_b = conf.w_b
+        p.offset, p.scale = float(conf.cost_funct_param[0]), float(conf.cost_funct_param[1])
+        p.alpha, p.alpha2 = float(conf.soft_max_param[0]), float(conf.soft_max_param[1])
+        _fill(p.obs, conf.obs_param)
+        _fill(p.target, conf.TARGET_STATE)
+        _fill(p.w_running, conf.cost_weights_running)
+        _fill(p.w_terminal, conf.cost_weights_terminal)
+        table = None
+        if robot is not None:
+            p.n_joints = robot.nq
+            p.ee_parent = robot.ee_parent
+            _fill(p.ee_R, np.asarray(robot.ee_R).reshape(-1))
+            _fill(p.ee_p, robot.ee_p)
+            _fill(p.gravity, robot.gravity)
+            table = np.ascontiguousarray(robot.table(), dtype=np.float64)
+        self.params = p
+        self._table = table
+        h = C.c_void_p()
+        L.lib().call("cacto_sys_create", C.byref(p),
+                     table.ctypes.data_as(C.c_void_p) if table is not None else None, C.byref(h))
+        self.handle = h
+        self.ns, self.na = conf.nb_state, conf.nb_action
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                L.lib().raw("cacto_sys_destroy")(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    def param_count(self, net):
+        return int(L.lib().raw("cacto_mlp_param_count")(self.handle, net))
+
+    def netbuf_floats(self, net):
+        return int(L.lib().raw("cacto_mlp_netbuf_floats")(self.handle, net))
+
+    def workspace_bytes(self, B):
+        return int(L.lib().raw("cacto_workspace_bytes")(self.handle, int(B)))

@@ -1,0 +1,261 @@
+/*
+ * cacto_hip.h — C-ABI of libcacto_hip.so, the MI355X (gfx950) hot path of CACTO.
+ *
+ * Drop-in boundary for the data-parallel hot path of nadimkanazi/cacto (reference paths below are
+ * relative to its repository root). Each entry point replaces a Python/TF/Pinocchio call site:
+ *
+ *   cacto_env_step_batch   Env.simulate_batch + derivative_batch + reward_batch (+ dr/da tape)
+ *                          environment.py:134-144, :277-286 (and per-system overrides); as called
+ *                          from NN.compute_actor_grad NeuralNetwork.py:188, :199-204
+ *   cacto_env_step         Env.step + get_end_effector_position (float64 rollout semantics)
+ *                          environment.py:70-78, :146-156; plot_utils.py:262-264
+ *   cacto_rollout          RL_AC.create_TO_init loop RL.py:223-231 / PLOT.rollout plot_utils.py:245-279
+ *   cacto_mlp_pack         (layout transform for the kernels; no reference counterpart)
+ *   cacto_actor_forward    NN.eval(actor, s)  NeuralNetwork.py:130-138 (+ utils.py:17-24)
+ *   cacto_critic_forward   NN.eval(critic, s)
+ *   cacto_critic_input_grad tape.gradient(V, s)  NeuralNetwork.py:162-165, :190-195
+ *   cacto_critic_grad      NN.compute_critic_grad  NeuralNetwork.py:150-178
+ *   cacto_actor_grad       NN.compute_actor_grad   NeuralNetwork.py:180-233
+ *   cacto_adam_step        optimizer.apply_gradients RL.py:105, :109 (Keras-2.11 Adam, RL.py:79-88)
+ *   cacto_soft_update      RL_AC.update_target RL.py:113-118
+ *   cacto_update           RL_AC.update + update_target (one learn_and_update iteration, RL.py:122-137)
+ *   cacto_buffer_gather    ReplayBuffer.sample row gather replay_buffer.py:47-61
+ *   cacto_buffer_add       ReplayBuffer.add ring write replay_buffer.py:25-36
+ *   cacto_per_*            PrioritizedReplayBuffer + segment trees replay_buffer.py:87-218,
+ *                          segment_tree.py:4-145
+ *
+ * Conventions
+ *   - Every pointer argument named *_d is DEVICE memory (e.g. torch tensor .data_ptr()), contiguous
+ *     row-major. Host pointers are named *_h. The library never frees caller memory.
+ *   - Every call is asynchronous on `stream` (a hipStream_t passed as void*; NULL = default stream)
+ *     and enqueues no host synchronisation, so sequences can be captured into a hipGraph.
+ *   - Return 0 on success, <0 on error; cacto_last_error() returns a thread-local message.
+ *     No C++ exception crosses the ABI.
+ *   - Handles (cacto_sys) are created/destroyed by the caller; concurrent calls on one handle are
+ *     undefined (as in the reference's single-threaded loop).
+ */
+#ifndef CACTO_HIP_H
+#define CACTO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CACTO_ABI_VERSION 1
+
+/* error codes */
+#define CACTO_OK 0
+#define CACTO_EINVAL -1
+#define CACTO_EHIP -2
+#define CACTO_ENOMEM -3
+#define CACTO_EUNSUPPORTED -4
+
+/* dynamics kinds */
+#define CACTO_DYN_SINGLE_INTEGRATOR 0 /* environment.py:235-243 */
+#define CACTO_DYN_CHAIN 1             /* Pinocchio chain: robot_utils.py:348-432 */
+#define CACTO_DYN_CAR 2               /* environment.py:437-448 */
+#define CACTO_DYN_CAR_PARK 3          /* environment.py:584-595 */
+
+/* reward kinds */
+#define CACTO_REW_PLANAR 0      /* SI / DI / Car: environment.py:252-275, :329-351, :457-480 */
+#define CACTO_REW_MANIPULATOR 1 /* planar + w2*|v|^2 when w2 != 0: environment.py:695-723 */
+#define CACTO_REW_UR5 2         /* 3-D ellipsoids: environment.py:780-805 */
+#define CACTO_REW_CAR_PARK 3    /* smooth-box obstacles: environment.py:604-641 */
+
+#define CACTO_MAX_STATE 16
+#define CACTO_MAX_ACTION 8
+#define CACTO_MAX_JOINTS 6
+#define CACTO_JOINT_COLS 27 /* parent, type, axis[3], R[9], p[3], mass, com[3], I[6] */
+
+/* System description: the numeric content of a conf_*.py module the hot path reads. */
+typedef struct {
+  int32_t dyn_kind;
+  int32_t reward_kind;
+  int32_t nb_state;  /* ns = nx + 1 (time last) */
+  int32_t nb_action; /* na */
+  int32_t nq, nv;    /* chain only */
+  int32_t normalize; /* NORMALIZE_INPUTS */
+  int32_t n_joints;  /* chain only */
+  int32_t ee_parent; /* chain only: joint index of the 'EE' frame's parent */
+  int32_t n_check;   /* car_park only */
+  int32_t n_weights; /* length of cost_weights_* (7, car_park 8) */
+  int32_t pad0;
+  double dt;
+  double state_norm[CACTO_MAX_STATE];
+  double u_max[CACTO_MAX_ACTION];
+  double w_b;
+  double scale, offset;  /* cost_funct_param[1], [0] */
+  double alpha, alpha2;  /* soft_max_param */
+  double obs[18];        /* obs_param */
+  double target[3];      /* TARGET_STATE */
+  double w_running[8];   /* cost_weights_running */
+  double w_terminal[8];  /* cost_weights_terminal */
+  double L_delta, tau_delta, k_db; /* car / car_park */
+  double check_points[20];         /* car_park check_points_BF (x, y) pairs */
+  double ee_R[9], ee_p[3];         /* chain: EE frame placement in its parent joint frame */
+  double gravity[3];               /* chain: model.gravity linear part */
+} cacto_sys_params;
+
+typedef struct cacto_sys cacto_sys;
+
+const char* cacto_last_error(void);
+int cacto_abi_version(void);
+
+/* joint_table_h: n_joints x CACTO_JOINT_COLS float64 (host), see cacto_amd/robots.py */
+int cacto_sys_create(const cacto_sys_params* params_h, const double* joint_table_h, cacto_sys** out);
+int cacto_sys_destroy(cacto_sys* sys);
+
+/* ---------------------------------------------------------------- environment ------------ */
+
+/* compute_actor_grad's environment calls for a batch (float32 tensors in/out, float64 math):
+ *   S_next = simulate_batch(S, A); Fu = derivative_batch(S, A);
+ *   R = reward_batch(W, S, A); dR_dA = d R / d A  (TF tape over u_cost)
+ * W: W_d [B, n_weights] float64 if given, else term*cost_weights_terminal +
+ * (1-term)*cost_weights_running from term_d [B] (NeuralNetwork.py:197-201), else running weights.
+ * Any output pointer may be NULL. Shapes: S [B,ns], A [B,na], S_next [B,ns], Fu [B,ns,na], R [B],
+ * dR_dA [B,na]. */
+int cacto_env_step_batch(const cacto_sys* sys, const float* S_d, const float* A_d, const double* term_d,
+                         const double* W_d, float* S_next_d, float* Fu_d, float* R_d, float* dR_dA_d, int B,
+                         void* stream);
+
+/* get_end_effector_position for B float64 states: EE_d [B,3] (environment.py:146-156). */
+int cacto_env_ee(const cacto_sys* sys, const double* S_d, double* EE_d, int B, void* stream);
+
+/* Env.step(W, s, a) in float64 plus the EE position of the next state, for B independent rows.
+ * W_d may be NULL (running weights). EE_d [B,3], any output may be NULL. */
+int cacto_env_step(const cacto_sys* sys, const double* S_d, const double* A_d, const double* W_d,
+                   double* S_next_d, double* R_d, double* EE_d, int B, void* stream);
+
+/* ---------------------------------------------------------------- networks --------------- */
+
+/* Flat parameter layout = Keras trainable_variables order, kernels [in,out] row-major:
+ *   actor : W1[ns,256] b1 W2[256,256] b2 W3[256,na] b3            (NeuralNetwork.py:51-63)
+ *   critic: W1[ns,64] b1 W2[64,64] b2 W3[64,128] b3 W4[128,128] b4 W5[128,1] b5  (:95-108)
+ * A "net buffer" is one float32 device buffer [flat params | pad to 64 | packed MFMA fragments]
+ * of cacto_mlp_netbuf_floats() floats. cacto_mlp_pack() refreshes the packed part from the flat
+ * part (the Adam kernels keep both in sync during training). */
+#define CACTO_NET_ACTOR 0
+#define CACTO_NET_CRITIC 1
+int64_t cacto_mlp_param_count(const cacto_sys* sys, int net);
+int64_t cacto_mlp_netbuf_floats(const cacto_sys* sys, int net);
+int cacto_mlp_pack(const cacto_sys* sys, int net, float* netbuf_d, void* stream);
+
+/* NN.eval: normalisation inside, float32. A [B,na], V [B], dVdS [B,ns] (w.r.t. the raw state). */
+int cacto_actor_forward(const cacto_sys* sys, const float* actor_netbuf_d, const float* S_d, float* A_d,
+                        int B, void* stream);
+int cacto_critic_forward(const cacto_sys* sys, const float* critic_netbuf_d, const float* S_d, float* V_d,
+                         int B, void* stream);
+int cacto_critic_input_grad(const cacto_sys* sys, const float* critic_netbuf_d, const float* S_d,
+                            float* V_d, float* dVdS_d, int B, void* stream);
+
+/* ---------------------------------------------------------------- learner ---------------- */
+
+/* Network state for an update: flat params + Adam moments (+ packed copies maintained by Adam). */
+typedef struct {
+  float* actor_d;  float* actor_m_d;  float* actor_v_d;   /* net buffer + flat Adam moments */
+  float* critic_d; float* critic_m_d; float* critic_v_d;
+  float* target_d;                                        /* target critic net buffer */
+  int32_t* step_d; /* device counters = Keras optimizer iterations: [0] critic, [1] actor.
+                    * cacto_critic_grad / cacto_actor_grad increment their counter; the following
+                    * cacto_adam_step uses it as `iterations + 1`. */
+} cacto_nets;
+
+typedef struct {
+  double w_S;         /* Sobolev weight (main.py --w-S) */
+  double tau;         /* UPDATE_RATE */
+  double beta1, beta2, epsilon; /* Keras Adam defaults 0.9, 0.999, 1e-7 (python floats) */
+  double critic_lr[5]; /* PiecewiseConstantDecay values (all equal when LR_SCHEDULE = 0) */
+  double actor_lr[5];
+  double lr_bounds[4]; /* boundaries (in iterations) */
+  int32_t MC;         /* conf.MC */
+  int32_t B_global;   /* batch size the loss means are taken over (= B on one GPU) */
+  int32_t want_target_V; /* also compute V_tgt(s) (NeuralNetwork.py:178) */
+  int32_t pad;
+} cacto_update_cfg;
+
+/* Replay rows are float64 [s | R | s_next | dVdx | d | term] (3ns+3 columns, replay_buffer.py:20). */
+
+/* Bytes of workspace cacto_critic_grad / cacto_actor_grad / cacto_update need for batch B. */
+size_t cacto_workspace_bytes(const cacto_sys* sys, int B);
+
+/* Critic gradient (flat, Keras order, summed over the B local rows with 1/B_global scaling).
+ * rows: storage_d indexed by idx_d[B] (int32); is_w_d = IS weights [B] or NULL (= 1).
+ * Outputs: grad_d [PC]; y_d [B] (reward_to_go), V_d [B], Vt_d [B] (if cfg->want_target_V). */
+int cacto_critic_grad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                      const double* storage_d, const int32_t* idx_d, const float* is_w_d, int B,
+                      float* grad_d, float* y_d, float* V_d, float* Vt_d,
+                      void* workspace_d, size_t workspace_bytes, void* stream);
+
+/* Actor gradient against the CURRENT critic (call after the critic step, RL.py:104-109). */
+int cacto_actor_grad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                     const double* storage_d, const int32_t* idx_d, int B, float* grad_d,
+                     void* workspace_d, size_t workspace_bytes, void* stream);
+
+/* Keras-2.11 Adam on a flat tensor + packed copy refresh; `which` = CACTO_NET_*.
+ * The iteration counter nets->step_d[which] is read and incremented on the device.
+ * For the critic this also performs the soft target update when soft_update != 0. */
+int cacto_adam_step(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, int which,
+                    const float* grad_d, int soft_update, void* stream);
+
+/* target <- tau*critic + (1-tau)*target (and its packed copy) */
+int cacto_soft_update(const cacto_sys* sys, const cacto_nets* nets, float tau, void* stream);
+
+/* One full RL_AC.update + update_target (single device): critic grad -> Adam(critic) + soft
+ * update -> actor grad (new critic) -> Adam(actor). */
+int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                 const double* storage_d, const int32_t* idx_d, const float* is_w_d, int B,
+                 float* y_d, float* V_d, float* Vt_d, void* workspace_d, size_t workspace_bytes,
+                 void* stream);
+
+/* ---------------------------------------------------------------- rollouts --------------- */
+
+/* B episodes from S0_d [B,ns] (float64), each for nsteps_d[b] <= T steps:
+ *   a_t = actor(s_t) (float32; zeros when use_actor == 0, i.e. ep == 0 in RL.py:224-225),
+ *   s_{t+1}, r_t = Env.step(W, s_t, a_t), ee_{t+1} = EE(s_{t+1}).
+ * Outputs (any may be NULL): S_traj [B,T+1,ns] f64, A_traj [B,T,na] f32, R_traj [B,T] f64,
+ * EE_traj [B,T+1,3] f64. Steps past nsteps_d[b] are not written. W_d: weights [n_weights] or NULL
+ * (running). status_d [B] int32 (optional): 0 ok, 1 NaN state encountered (RL.py:229-231). */
+int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
+                  const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
+                  double* S_traj_d, float* A_traj_d, double* R_traj_d, double* EE_traj_d,
+                  int32_t* status_d, int B, void* stream);
+
+/* ---------------------------------------------------------------- replay ------------------ */
+
+/* rows_d [n, 3ns+3] f64 written at ring position next_idx (wraps modulo capacity). */
+int cacto_buffer_add(const cacto_sys* sys, double* storage_d, int64_t capacity, int64_t next_idx,
+                     const double* rows_d, int64_t n, void* stream);
+
+/* replay_buffer.py:47-61: S, R, S_next, dVdx, d as float32, term float64; any may be NULL. */
+int cacto_buffer_gather(const cacto_sys* sys, const double* storage_d, const int32_t* idx_d, int B,
+                        float* S_d, float* R_d, float* S_next_d, float* dVdx_d, float* d_d, double* term_d,
+                        void* stream);
+
+/* Prioritized replay. Trees are float64 arrays of 2*capacity (capacity a power of two), node 1 =
+ * root, leaves at [capacity, 2*capacity) — the layout of segment_tree.py:33. */
+int cacto_per_init(double* sum_tree_d, double* min_tree_d, int64_t capacity, void* stream);
+/* Set leaves [start, start+n) (mod ring_size) to `value` and refresh ancestors (replay_buffer.py:133-135). */
+int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
+                        int64_t start, int64_t n, double value, void* stream);
+/* Stratified proportional sampling (replay_buffer.py:139-188). uniforms_d [B] = random.random()
+ * draws. Outputs idx_d [B] int32, is_w_d [B] float32 (IS weights), and exp_counter_d (float64
+ * [ring]) incremented once per distinct index. */
+int cacto_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
+                     double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
+                     double* exp_counter_d, void* stream);
+/* update_priorities 'PER' (replay_buffer.py:190-218): p = fresh^count*|y-V| + eps; leaves p^alpha,
+ * duplicates last-write-wins; max_priority_d[0] = max(max_priority, p). */
+int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                     const float* y_d, const float* V_d, const double* exp_counter_d, double fresh_factor,
+                     double eps, double alpha, double* max_priority_d, int B, void* stream);
+/* Set arbitrary leaves (already raised to alpha) and refresh ancestors; duplicates last-write-wins. */
+int cacto_per_set_leaves(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                         const double* values_d, int n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CACTO_HIP_H */

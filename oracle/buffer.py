@@ -159,15 +159,20 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         return (pr * max_idx) ** (-self.beta) / max_weight
 
     def update_priorities(self, idxes, y, V):
-        """replay_buffer.py:190-218 ('PER' branch): p = fresh^count * |y - V| + eps."""
-        td = np.abs(np.asarray(y, dtype=np.float32) - np.asarray(V, dtype=np.float32))[:, 0]
-        fresh = self.fresh ** self.exp_counter[idxes]
-        new_p = fresh * td + self.eps
+        """replay_buffer.py:190-218 ('PER' branch): p = fresh^count * |y - V| + eps.
+        The reference multiplies a float64 numpy array by float32 TF tensors, so p is a float32
+        tensor (TF converts the numpy operand to the tensor dtype); leaves are float(p) ** alpha
+        as Python floats (the fixed semantics)."""
+        f32 = np.float32
+        td = np.abs(np.asarray(y, dtype=f32) - np.asarray(V, dtype=f32))[:, 0]
+        fresh = (self.fresh ** self.exp_counter[np.asarray(idxes)]).astype(f32)
+        new_p = (fresh * td).astype(f32) + f32(self.eps)
         for idx, p in zip(idxes, new_p):
             assert p > 0
-            self.it_sum[int(idx)] = p ** self.alpha
-            self.it_min[int(idx)] = p ** self.alpha
-            self.max_priority = max(self.max_priority, p)
+            leaf = float(p) ** self.alpha
+            self.it_sum[int(idx)] = leaf
+            self.it_min[int(idx)] = leaf
+            self.max_priority = max(self.max_priority, float(p))
         return new_p
 
 

@@ -1,0 +1,359 @@
+"""GPU parity: the HIP path (through the C-ABI) against the float64 oracle on the same inputs.
+
+Tolerances (float32 kernels vs float64 oracle):
+  * dynamics / Fu / EE in float64 kernels: bit-exact where the arithmetic is exact (SI, DI),
+    rel 1e-12 for the manipulator chain (CRBA/RNEA vs 6x6 restatement);
+  * float32 outputs of float64 math (S_next, Fu): exact f32 rounding for SI/DI, 2 ulp manipulator;
+  * MLP forward: |err| <= 2e-6 * (1 + |ref|) (K <= 256 float32 MFMA accumulation);
+  * gradients: relative L2 error per tensor <= 2e-4 (float32 chains with sin/cos and clog).
+"""
+import math
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_weights
+from oracle import buffer as obuf
+from oracle import env as oenv
+from oracle import nn as onn
+from oracle import rollout as oroll
+from cacto_amd.confs import load_conf
+
+pytestmark = pytest.mark.gpu
+
+SYSTEMS = ["single_integrator", "double_integrator", "manipulator"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _env(system):
+    from cacto_amd.environment import make_env
+    conf = load_conf(system)
+    return conf, make_env(conf), oenv.make_env(conf)
+
+
+def _states(conf, n, rng):
+    lo = np.array(conf.x_init_min, dtype=float)
+    hi = np.array(conf.x_init_max, dtype=float)
+    S = rng.uniform(lo, hi, size=(n, conf.nb_state))
+    S[:, :-1] *= 1.3
+    return S
+
+
+def _actions(conf, n, rng):
+    return rng.uniform(-1.2, 1.2, size=(n, conf.nb_action)) * conf.u_max
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+# ------------------------------------------------------------------ environment
+@pytest.mark.parametrize("system", SYSTEMS)
+def test_env_step_batch_f32(system):
+    conf, genv, oe = _env(system)
+    rng = np.random.default_rng(10)
+    B = 333
+    S = _states(conf, B, rng).astype(np.float32)
+    A = _actions(conf, B, rng).astype(np.float32)
+    term = (rng.uniform(size=B) < 0.3).astype(np.float64)
+    out = genv.batch_f32(S, A, term=term)
+    torch.cuda.synchronize()
+    Sn = out["S_next"].cpu().numpy()
+    Fu = out["Fu"].cpu().numpy()
+    ref_Sn = oe.simulate_batch(S, A)
+    ref_Fu = oe.derivative_batch(S, A)
+    if system == "manipulator":
+        np.testing.assert_allclose(Sn, ref_Sn, rtol=3e-7, atol=1e-6)
+        np.testing.assert_allclose(Fu, ref_Fu, rtol=3e-7, atol=1e-12)
+    else:
+        np.testing.assert_array_equal(Sn, ref_Sn)
+        np.testing.assert_array_equal(Fu, ref_Fu)
+    W = term[:, None] * conf.cost_weights_terminal + (1 - term[:, None]) * conf.cost_weights_running
+    ref_R = oe.reward_batch(W, S, A)[:, 0]
+    np.testing.assert_allclose(out["R"].cpu().numpy(), ref_R, rtol=2e-6, atol=1e-9)
+    np.testing.assert_allclose(out["dR_dA"].cpu().numpy(), oe.dr_da(W, A), rtol=2e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("system", SYSTEMS)
+def test_env_step_f64(system):
+    conf, genv, oe = _env(system)
+    rng = np.random.default_rng(11)
+    B = 257
+    S = _states(conf, B, rng)
+    A = _actions(conf, B, rng)
+    Sn, R, EE = genv.step_batch(S, A)
+    torch.cuda.synchronize()
+    ref = [oe.step(conf.cost_weights_running, s, a) for s, a in zip(S, A)]
+    ref_S = np.array([r[0] for r in ref])
+    ref_R = np.array([r[1] for r in ref])
+    ref_EE = np.array([oe.get_end_effector_position(s) for s in ref_S])
+    if system == "manipulator":
+        np.testing.assert_allclose(Sn.cpu().numpy(), ref_S, rtol=1e-12, atol=1e-12)
+    else:
+        np.testing.assert_array_equal(Sn.cpu().numpy(), ref_S)
+    np.testing.assert_allclose(R.cpu().numpy(), ref_R, rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(EE.cpu().numpy(), ref_EE, rtol=1e-13, atol=1e-12)
+
+
+# ------------------------------------------------------------------ networks
+def _nets(system, tag=None, seed=0):
+    from cacto_amd.neural_network import NN
+    from cacto_amd.rl import RL_AC
+    conf, genv, oe = _env(system)
+    nn = NN(genv, conf, w_S=1e-2, seed=seed)
+    rl = RL_AC(genv, nn, conf)
+    weights = load_weights(tag) if tag else None
+    rl.setup_model(weights=weights)
+    return conf, genv, oe, nn, rl
+
+
+@pytest.mark.parametrize("system,tag", [("double_integrator", "di_seed0_final"), ("single_integrator", "si_seed0_0"),
+                                        ("manipulator", None)])
+def test_forward_and_input_grad(system, tag):
+    conf, genv, oe, nn, rl = _nets(system, tag)
+    rng = np.random.default_rng(12)
+    B = 200
+    S = _states(conf, B, rng).astype(np.float32)
+    norm = conf.state_norm_arr.astype(np.float64)
+    A = nn.eval(rl.actor_model, S).cpu().numpy()
+    ref_A = onn.actor_forward(rl.actor_model.get_weights(), S.astype(np.float64), norm)
+    assert np.all(np.abs(A - ref_A) <= 2e-6 * (1 + np.abs(ref_A))), np.abs(A - ref_A).max()
+    V, g = nn.critic_input_grad(rl.critic_model, S)
+    ref_V = onn.critic_forward(rl.critic_model.get_weights(), S.astype(np.float64), norm)
+    ref_g, _ = onn.critic_input_grad(rl.critic_model.get_weights(), S.astype(np.float64), norm)
+    assert np.all(np.abs(V.cpu().numpy() - ref_V) <= 2e-6 * (1 + np.abs(ref_V)))
+    assert rel_l2(g.cpu().numpy(), ref_g) < 2e-5
+
+
+def _replay_rows(conf, B, rng):
+    ns = conf.nb_state
+    S = _states(conf, B, rng)
+    Sn = _states(conf, B, rng)
+    R = rng.normal(size=(B, 1)) * 0.5
+    dVdx = rng.normal(size=(B, ns)) * 0.3
+    d = (rng.uniform(size=(B, 1)) < 0.3).astype(float)
+    term = (rng.uniform(size=(B, 1)) < 0.2).astype(float)
+    return np.concatenate([S, R, Sn, dVdx, d, term], axis=1)
+
+
+@pytest.mark.parametrize("system,tag,w_S,B", [("double_integrator", "di_seed0_0", 1e-2, 128),
+                                              ("double_integrator", "di_seed0_final", 1e-2, 100),
+                                              ("double_integrator", "di_seed0_0", 0.0, 64),
+                                              ("manipulator", None, 1e-2, 64),
+                                              ("single_integrator", "si_seed0_0", 0.0, 128)])
+def test_critic_grad(system, tag, w_S, B):
+    conf, genv, oe, nn, rl = _nets(system, tag)
+    rl.w_S = w_S
+    rl.cfg = rl.make_cfg()
+    rng = np.random.default_rng(13)
+    rows = _replay_rows(conf, B, rng)
+    rows_f32 = rows.astype(np.float32).astype(np.float64)  # the reference converts the sample to f32
+    ns = conf.nb_state
+    g, y, V, Vt = rl.critic_grad_rows(torch.as_tensor(rows, device="cuda"),
+                                      torch.arange(B, dtype=torch.int32, device="cuda"))
+    norm = conf.state_norm_arr.astype(np.float64)
+    ref = onn.compute_critic_grad(rl.critic_model.get_weights(), rl.target_critic.get_weights(),
+                                  rows_f32[:, :ns], rows_f32[:, ns + 1:2 * ns + 1], rows_f32[:, ns:ns + 1],
+                                  rows_f32[:, 2 * ns + 1:3 * ns + 1], rows_f32[:, 3 * ns + 1:3 * ns + 2],
+                                  np.ones((B, 1)), w_S, norm)
+    for i, (a, b) in enumerate(zip(g, ref[0])):
+        assert rel_l2(a.cpu().numpy(), b) < 2e-4, (i, rel_l2(a.cpu().numpy(), b))
+    np.testing.assert_allclose(y.cpu().numpy(), ref[1], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(V.cpu().numpy(), ref[2], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(Vt.cpu().numpy(), ref[3], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("system,tag,B", [("double_integrator", "di_seed0_final", 128),
+                                          ("manipulator", None, 64), ("single_integrator", "si_seed0_0", 77)])
+def test_actor_grad(system, tag, B):
+    conf, genv, oe, nn, rl = _nets(system, tag)
+    rng = np.random.default_rng(14)
+    rows = _replay_rows(conf, B, rng)
+    ns = conf.nb_state
+    g = rl.actor_grad_rows(torch.as_tensor(rows, device="cuda"), torch.arange(B, dtype=torch.int32, device="cuda"))
+    S32 = rows[:, :ns].astype(np.float32)
+    ref = onn.compute_actor_grad(oe, rl.actor_model.get_weights(), rl.critic_model.get_weights(), S32,
+                                 rows[:, 3 * ns + 2:3 * ns + 3], conf.state_norm_arr.astype(np.float64))
+    for i, (a, b) in enumerate(zip(g, ref)):
+        assert rel_l2(a.cpu().numpy(), b) < 2e-4, (i, rel_l2(a.cpu().numpy(), b))
+
+
+def test_update_matches_oracle_sequence():
+    """Several fused cacto_update steps == the oracle's critic step -> actor step (new critic) ->
+    target update sequence with Keras-Adam (RL.py:101-118)."""
+    conf, genv, oe, nn, rl = _nets("double_integrator", "di_seed0_0")
+    norm = conf.state_norm_arr.astype(np.float64)
+    rng = np.random.default_rng(15)
+    N, B, steps = 512, 128, 5
+    rows = _replay_rows(conf, N, rng)
+    storage = torch.as_tensor(rows, device="cuda")
+    ns = conf.nb_state
+    crit, tgt, act = rl.critic_model.get_weights(), rl.target_critic.get_weights(), rl.actor_model.get_weights()
+    oc, oa = onn.KerasAdam(conf.CRITIC_LEARNING_RATE), onn.KerasAdam(conf.ACTOR_LEARNING_RATE)
+    for k in range(steps):
+        idx = rng.integers(0, N, size=B)
+        rl.update_rows(storage, torch.as_tensor(idx.astype(np.int32), device="cuda"))
+        r = rows[idx].astype(np.float32).astype(np.float64)
+        gc = onn.compute_critic_grad(crit, tgt, r[:, :ns], r[:, ns + 1:2 * ns + 1], r[:, ns:ns + 1],
+                                     r[:, 2 * ns + 1:3 * ns + 1], r[:, 3 * ns + 1:3 * ns + 2], np.ones((B, 1)),
+                                     1e-2, norm)[0]
+        crit = oc.apply(crit, gc)
+        ga = onn.compute_actor_grad(oe, act, crit, r[:, :ns].astype(np.float32), rows[idx, 3 * ns + 2:], norm)
+        act = oa.apply(act, ga)
+        tgt = onn.soft_update(tgt, crit, conf.UPDATE_RATE)
+    torch.cuda.synchronize()
+    assert rl.steps.cpu().tolist() == [steps, steps]
+    for name, got, ref in (("critic", rl.critic_model.get_weights(), crit), ("actor", rl.actor_model.get_weights(), act),
+                           ("target", rl.target_critic.get_weights(), tgt)):
+        for i, (a, b) in enumerate(zip(got, ref)):
+            # Adam normalises the step, so compare the accumulated parameter change
+            assert np.abs(a - b).max() < 5e-6 * steps, (name, i, np.abs(a - b).max())
+    # packed copies were refreshed: forward with the updated weights matches the oracle
+    S = _states(conf, 64, rng).astype(np.float32)
+    A = nn.eval(rl.actor_model, S).cpu().numpy()
+    refA = onn.actor_forward(rl.actor_model.get_weights(), S.astype(np.float64), norm)
+    assert np.all(np.abs(A - refA) <= 2e-6 * (1 + np.abs(refA)))
+
+
+# ------------------------------------------------------------------ rollout
+def test_rollout_di_known_answer():
+    conf, genv, oe, nn, rl = _nets("double_integrator", "di_seed0_final")
+    S0 = np.array(conf.init_states_sim)
+    T = conf.NSTEPS
+    out = rl.rollout_batch(S0, [T] * len(S0), T)
+    torch.cuda.synchronize()
+    EE = out["EE"].cpu().numpy()
+    S = out["S"].cpu().numpy()
+    maxy = {(s[0], s[1]): EE[k, :, 1].max() for k, s in enumerate(S0)}
+    assert abs(maxy[(2.0, 0.0)] - 3.74) < 0.01
+    assert abs(maxy[(10.0, 0.0)] - 7.88) < 0.01
+    assert abs(maxy[(10.0, 10.0)] - 10.0) < 0.01
+    assert abs(maxy[(12.0, 2.0)] - 8.70) < 0.01
+    assert abs(maxy[(15.0, 0.0)] - 9.44) < 0.01
+    actor = rl.actor_model.get_weights()
+    for k, s0 in enumerate(S0):
+        rS, rA, rR, rEE = oroll.policy_rollout(oe, actor, s0, T)
+        np.testing.assert_allclose(S[k], rS, rtol=1e-4, atol=2e-4)
+        np.testing.assert_allclose(out["R"].cpu().numpy()[k], rR, rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("system", ["double_integrator", "manipulator"])
+def test_rollout_variable_lengths(system):
+    conf, genv, oe, nn, rl = _nets(system, None, seed=3)
+    rng = random.Random(5)
+    S0 = np.array([oe.reset(rng) for _ in range(37)])
+    ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    T = max(ns_)
+    out = rl.rollout_batch(S0, ns_, T)
+    torch.cuda.synchronize()
+    S = out["S"].cpu().numpy()
+    actor = rl.actor_model.get_weights()
+    for k in range(0, 37, 6):
+        ref = oroll.to_init_rollout(oe, actor, S0[k], 1)
+        rS, rU, rT = ref
+        assert rT == ns_[k]
+        np.testing.assert_allclose(S[k, :rT + 1], rS, rtol=1e-4, atol=2e-4)
+    assert (out["status"].cpu().numpy() == 0).all()
+
+
+def test_rollout_zero_controls_ep0_exact():
+    conf, genv, oe, nn, rl = _nets("double_integrator", None)
+    rng = random.Random(6)
+    S0 = np.array([oe.reset(rng) for _ in range(20)])
+    ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    out = rl.rollout_batch(S0, ns_, max(ns_), ep=0)
+    S = out["S"].cpu().numpy()
+    for k in range(20):
+        rS, rU, rT = oroll.to_init_rollout(oe, None, S0[k], 0)
+        np.testing.assert_array_equal(S[k, :rT + 1], rS)
+
+
+# ------------------------------------------------------------------ replay
+def test_buffer_add_gather_bit_exact(ref_vectors):
+    from cacto_amd.replay_buffer import ReplayBuffer
+    from cacto_amd.system import System
+    conf = load_conf("double_integrator")
+
+    class C:
+        pass
+    c = C()
+    c.__dict__.update({k: getattr(conf, k) for k in dir(conf) if not k.startswith("__")})
+    c.REPLAY_SIZE, c.BATCH_SIZE = 64, 16
+    rb = ReplayBuffer(c, System(conf))
+    rows = ref_vectors["rb_adds"]
+    off = 0
+    for L in ref_vectors["rb_eplens"]:
+        rb.add_rows(rows[off:off + L])
+        off += L
+    np.testing.assert_array_equal(rb.storage.cpu().numpy(), ref_vectors["rb_storage"])
+    assert [rb.next_idx, rb.full] == list(ref_vectors["rb_next_full"])
+    out = rb.sample(torch.as_tensor(ref_vectors["rb_sidx"].astype(np.int32), device="cuda"))
+    for name, got in zip(["s", "r", "sn", "dvdx", "d", "term", "w"], out[:7]):
+        np.testing.assert_array_equal(got.cpu().numpy(), ref_vectors["rb_sample_" + name])
+
+
+def test_per_sampling_bit_exact(ref_vectors):
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    from cacto_amd.system import System
+    conf = load_conf("double_integrator")
+
+    class C:
+        pass
+    c = C()
+    c.__dict__.update({k: getattr(conf, k) for k in dir(conf) if not k.startswith("__")})
+    c.BATCH_SIZE, c.prioritized_replay_alpha = 64, 0.6
+    per = PrioritizedReplayBuffer(c, System(conf))
+    leaves = ref_vectors["per_leaves"]
+    per.set_leaves(np.arange(len(leaves)), leaves)
+    per.next_idx = len(leaves)
+    idx, w = per.sample_device(list(ref_vectors["per_u"]))
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref_vectors["per_idx"])
+    assert per.sum_tree[1].item() == ref_vectors["per_ptotal"][1]
+    # IS weights and exp_counter against the oracle
+    o = obuf.PrioritizedReplayBuffer(65536, 5, 0.6, 0.6, 1e-2, 0.95, 64)
+    for i, v in enumerate(leaves):
+        o.it_sum[i] = float(v)
+        o.it_min[i] = float(v)
+    o.next_idx = len(leaves)
+    ow = o.sample_weights(ref_vectors["per_idx"])
+    np.testing.assert_allclose(w.cpu().numpy(), ow.astype(np.float32), rtol=1e-6)
+    np.testing.assert_array_equal(per.exp_counter.cpu().numpy()[:len(leaves)], o.exp_counter[:len(leaves)])
+
+
+def test_per_update_priorities_matches_oracle():
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    from cacto_amd.system import System
+    conf = load_conf("manipulator")
+    per = PrioritizedReplayBuffer(conf, System(conf))
+    o = obuf.PrioritizedReplayBuffer(conf.REPLAY_SIZE, conf.nb_state, 0.6, 0.6, conf.prioritized_replay_eps,
+                                     conf.fresh_factor, conf.BATCH_SIZE)
+    per.alpha = 0.6
+    rng = np.random.default_rng(16)
+    rows = rng.normal(size=(3000, 3 * conf.nb_state + 3))
+    per.add_rows(rows)
+    o.add_rows(rows)
+    for it in range(3):
+        u = list(rng.uniform(size=conf.BATCH_SIZE))
+        idx, w = per.sample_device(u)
+        oidx = o.sample_proportional(u)
+        np.testing.assert_array_equal(idx.cpu().numpy(), oidx)
+        o.sample_weights(oidx)
+        y = rng.normal(size=(conf.BATCH_SIZE, 1)).astype(np.float32)
+        V = rng.normal(size=(conf.BATCH_SIZE, 1)).astype(np.float32)
+        idx[5] = idx[9]  # duplicates: last write wins
+        oidx[5] = oidx[9]
+        per.update_priorities_device(idx, torch.as_tensor(y, device="cuda"), torch.as_tensor(V, device="cuda"))
+        o.update_priorities(oidx, y, V)
+        torch.cuda.synchronize()
+        st = per.sum_tree.cpu().numpy()
+        np.testing.assert_allclose(st[65536:65536 + 3000], o.it_sum.value[65536:65536 + 3000], rtol=1e-6)
+        np.testing.assert_allclose(st[1], o.it_sum.value[1], rtol=1e-6)
