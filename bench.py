@@ -1,0 +1,321 @@
+#!/usr/bin/env python
+"""CACTO hot-path benchmark on MI355X (BASELINE.json metric: env-steps/sec + critic-updates/sec).
+
+Workload (BASELINE.json configs[1]): double_integrator, w_S = 1e-2, 4096 rollouts per GPU.
+  * step = one batched rollout of the 4096 episodes (RL_AC.create_TO_init / PLOT.rollout loop:
+    actor MFMA tile + float64 dynamics + reward + EE per env-step, all in one persistent kernel);
+    initial states from Env.reset (CPython random seeded per rank), NSTEPS_SH = NSTEPS - int(t/dt).
+    `value` = env-steps/s summed over ranks (weak scaling: every rank rolls out its own episodes).
+  * critic_updates: the learn_and_update loop (RL_AC.update + update_target) at the reference
+    minibatch (128) and a scaled one (4096), on a 65,536-row replay buffer filled from the
+    rollouts; with N > 1 ranks each rank takes the minibatch locally and the gradients are
+    all-reduced over RCCL (data parallel, one global update per iteration).
+Inputs are resident in HBM before timing. Weights: the reference's DI seed-0 initial weights
+(tests/golden/weights/di_seed0_0.npz); dVdx labels are synthetic N(0,1) (TO/CasADi is host-side
+and absent here).
+
+    python bench.py [--gpus N --steps K --warmup W]
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec + critic-updates/sec per node, double_integrator & manipulator"
+FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF spec (dense)
+
+
+def fa_flops(ns, na):
+    return 2 * (ns * 256 + 256 * 256 + 256 * na)
+
+
+def fc_flops(ns):
+    return 2 * (ns * 64 + 64 * 64 + 64 * 128 + 128 * 128 + 128)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--system", default="double_integrator")
+    p.add_argument("--rollouts", type=int, default=4096)
+    p.add_argument("--update-steps", type=int, default=200)
+    p.add_argument("--batches", default="128,4096")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--extra-systems", default="manipulator")
+    return p.parse_args()
+
+
+def init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    return world, rank
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def make_learner(system, w_S=1e-2):
+    from cacto_amd.confs import load_conf
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.rl import RL_AC
+    conf = load_conf(system)
+    env = make_env(conf)
+    nn = NN(env, conf, w_S=w_S, seed=0)
+    rl = RL_AC(env, nn, conf)
+    weights = None
+    if system == "double_integrator":
+        z = np.load(os.path.join(ROOT, "tests", "golden", "weights", "di_seed0_0.npz"))
+        weights = {k: [z["%s_%d" % (k, i)] for i in range(6 if k == "actor" else 10)]
+                   for k in ("actor", "critic", "target")}
+    rl.setup_model(weights=weights)
+    return conf, env, rl
+
+
+def initial_states(env, conf, R, seed):
+    random.seed(seed)
+    S0, n = [], []
+    while len(S0) < R:
+        s = env.reset()
+        k = conf.NSTEPS - int(s[-1] / conf.dt)
+        if k > 0:                      # NSTEPS_SH == 0 episodes are dropped (RL.py:202-203)
+            S0.append(s)
+            n.append(k)
+    return np.array(S0), np.array(n, dtype=np.int32)
+
+
+def rollout_phase(rl, conf, env, R, K, W, world, rank):
+    S0, nsteps = initial_states(env, conf, R, seed=rank)
+    T = int(nsteps.max())
+    inputs = rl.rollout_inputs(S0, nsteps)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    out = {"S": torch.empty(R, T + 1, conf.nb_state, **f64), "A": torch.empty(R, T, conf.nb_action,
+                                                                              dtype=torch.float32, device="cuda"),
+           "R": torch.empty(R, T, **f64), "EE": torch.empty(R, T + 1, 3, **f64),
+           "status": torch.empty(R, dtype=torch.int32, device="cuda")}
+    for _ in range(W):
+        rl.rollout_batch(None, None, T, inputs=inputs, out=out)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(K):
+        rl.rollout_batch(None, None, T, inputs=inputs, out=out)
+    ev1.record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    wall = max_over_ranks(t1 - t0, world)
+    kern_ms = ev0.elapsed_time(ev1) / K
+    steps_per_call = int(nsteps.sum())
+    return dict(out=out, S0=S0, nsteps=nsteps, T=T, wall=wall, kernel_ms=kern_ms, steps_per_call=steps_per_call,
+                total_steps=sum_over_ranks(steps_per_call * K, world))
+
+
+def fill_buffer(rl, conf, roll, seed):
+    """Replay rows from the rollouts (RL_Solve n-step targets, RL.py:145-189, vectorised over
+    episodes; rewards = the rollout rewards, dVdx synthetic N(0,1))."""
+    from cacto_amd.replay_buffer import ReplayBuffer
+    S = roll["out"]["S"].cpu().numpy()
+    Rw = roll["out"]["R"].cpu().numpy()
+    nsteps = roll["nsteps"]
+    ns, nTD = conf.nb_state, conf.nsteps_TD_N
+    gen = np.random.Generator(np.random.PCG64(seed))
+    rows = []
+    for e in range(len(nsteps)):
+        T = int(nsteps[e])
+        r = np.concatenate([Rw[e, :T], [0.0]])
+        c = np.concatenate([[0.0], np.cumsum(r)])
+        i = np.arange(T + 1)
+        fin = np.minimum(i + nTD, T)
+        partial = (c[fin + 1] - c[i]).astype(np.float32).astype(np.float64)
+        done = (fin == T).astype(np.float64)
+        snext = np.zeros((T + 1, ns))
+        m = fin < T
+        snext[m] = S[e, fin[m] + 1]
+        term = np.zeros(T + 1)
+        term[-1] = 1
+        rows.append(np.concatenate([S[e, :T + 1], partial[:, None], snext, gen.standard_normal((T + 1, ns)),
+                                    done[:, None], term[:, None]], axis=1))
+        if sum(len(x) for x in rows) >= conf.REPLAY_SIZE:
+            break
+    rows = np.concatenate(rows)[:conf.REPLAY_SIZE]
+    buf = ReplayBuffer(conf, rl.sys)
+    buf.add_rows(rows)
+    return buf
+
+
+def update_phase(rl, buf, B, K, W, world, seed):
+    gen = np.random.Generator(np.random.PCG64(seed))
+    idx = torch.as_tensor(gen.integers(0, buf.max_idx(), size=(K + W, B)).astype(np.int32), device="cuda")
+    for i in range(W):
+        rl.update_rows(buf.storage, idx[i])
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        rl.update_rows(buf.storage, idx[W + i])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    wall = max_over_ranks(t1 - t0, world)
+    return wall
+
+
+def cpu_baseline_rollout(conf, rl, roll, seconds):
+    """The oracle's per-sample port (PLOT.rollout loop: float32 actor at batch 1 + float64 env.step),
+    single core, on the first episodes of the same workload until `seconds` elapse."""
+    from oracle import env as oenv
+    from oracle import rollout as oroll
+    oe = oenv.make_env(conf)
+    actor = rl.actor_model.get_weights()
+    steps, t0, e = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds and e < len(roll["S0"]):
+        oroll.policy_rollout(oe, actor, roll["S0"][e], int(roll["nsteps"][e]))
+        steps += int(roll["nsteps"][e])
+        e += 1
+    dt = time.perf_counter() - t0
+    return dict(value=steps / dt, unit="env-steps/s", cores=1, kind="port",
+                sample="%d of the %d episodes (%d env-steps, %.1f s), oracle/rollout.py policy_rollout"
+                       % (e, len(roll["S0"]), steps, dt))
+
+
+def cpu_baseline_update(conf, rl, buf, B, seconds):
+    from oracle import env as oenv
+    from oracle import nn as onn
+    oe = oenv.make_env(conf)
+    norm = conf.state_norm_arr.astype(np.float64)
+    rows = buf.storage[:4096].cpu().numpy()
+    ns = conf.nb_state
+    crit, tgt, act = rl.critic_model.get_weights(), rl.target_critic.get_weights(), rl.actor_model.get_weights()
+    oc, oa = onn.KerasAdam(conf.CRITIC_LEARNING_RATE), onn.KerasAdam(conf.ACTOR_LEARNING_RATE)
+    gen = np.random.default_rng(0)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        r = rows[gen.integers(0, len(rows), B)].astype(np.float32).astype(np.float64)
+        g = onn.compute_critic_grad(crit, tgt, r[:, :ns], r[:, ns + 1:2 * ns + 1], r[:, ns:ns + 1],
+                                    r[:, 2 * ns + 1:3 * ns + 1], r[:, 3 * ns + 1:3 * ns + 2], np.ones((B, 1)),
+                                    rl.w_S, norm)[0]
+        crit = oc.apply(crit, g)
+        ga = onn.compute_actor_grad(oe, act, crit, r[:, :ns].astype(np.float32), r[:, 3 * ns + 2:], norm)
+        act = oa.apply(act, ga)
+        tgt = onn.soft_update(tgt, crit, conf.UPDATE_RATE)
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="critic-updates/s", cores=1, kind="port", batch=B,
+                sample="%d updates at B=%d in %.1f s (oracle/nn.py, numpy float64)" % (n, B, dt))
+
+
+def main():
+    args = parse()
+    world, rank = init_dist()
+    torch.backends.cuda.matmul.allow_tf32 = False
+    conf, env, rl = make_learner(args.system)
+    if world > 1:
+        rl.set_data_parallel(world)
+    ns, na = conf.nb_state, conf.nb_action
+    roll = rollout_phase(rl, conf, env, args.rollouts, args.steps, args.warmup, world, rank)
+    value = roll["total_steps"] / roll["wall"]
+    achieved = roll["steps_per_call"] * fa_flops(ns, na) / (roll["kernel_ms"] * 1e-3)
+    buf = fill_buffer(rl, conf, roll, seed=rank)
+    updates = {}
+    for B in [int(b) for b in args.batches.split(",") if b]:
+        K = args.update_steps
+        wall = update_phase(rl, buf, B, K, max(3, args.warmup), world, seed=100 + rank)
+        flop = B * world * (9 * fc_flops(ns) + 3 * fa_flops(ns, na))
+        updates["B=%d" % B] = dict(value=K / wall, unit="critic-updates/s", global_batch=B * world,
+                                   ms_per_update=1e3 * wall / K, tflops=flop * K / wall / 1e12,
+                                   mfma_frac=flop * K / wall / (FP32_MFMA_PEAK * world))
+    extra = {}
+    for sysname in [s for s in args.extra_systems.split(",") if s and s != args.system]:
+        c2, e2, rl2 = make_learner(sysname, w_S=0.0)
+        if world > 1:
+            rl2.set_data_parallel(world)
+        R2 = 8192 if sysname == "manipulator" else args.rollouts
+        r2 = rollout_phase(rl2, c2, e2, R2, args.steps, args.warmup, world, rank)
+        b2 = fill_buffer(rl2, c2, r2, seed=rank)
+        u2 = {}
+        for B in (64, 8192):
+            wall = update_phase(rl2, b2, B, args.update_steps, 3, world, seed=200 + rank)
+            u2["B=%d" % B] = dict(value=args.update_steps / wall, unit="critic-updates/s", global_batch=B * world)
+        extra[sysname] = dict(env_steps_per_s=r2["total_steps"] / r2["wall"], rollouts_per_gpu=R2,
+                              rollout_kernel_ms=r2["kernel_ms"], critic_updates=u2)
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_rollout(conf, rl, roll, args.cpu_seconds)
+        cpu["update"] = cpu_baseline_update(conf, rl, buf, 128, args.cpu_seconds / 2)
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * roll["wall"] / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (MLP, MFMA) / f64 (dynamics)",
+            "data": "synthetic: Env.reset initial states (random.seed(rank)), reference DI seed-0 weights, "
+                    "N(0,1) dVdx labels",
+            "config": {"workload": "double_integrator, w-S=1e-2, %d rollouts per GPU (BASELINE configs[1])"
+                                   % args.rollouts,
+                       "system": args.system, "rollouts_per_gpu": args.rollouts,
+                       "env_steps_per_rollout_batch": roll["steps_per_call"], "T_max": roll["T"],
+                       "parallelism": "dp%d" % world},
+            "roofline": {"kernel": "k_rollout", "bound": "mfma", "achieved": achieved / 1e12,
+                         "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK,
+                         "traffic": None, "kernel_ms": roll["kernel_ms"],
+                         "flop_per_env_step": fa_flops(ns, na)},
+            "critic_updates": updates,
+            "cpu_baseline": cpu,
+            "extra_systems": extra,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

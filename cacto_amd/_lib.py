@@ -73,7 +73,7 @@ _SIGS = {
     "cacto_soft_update": (C.c_int, [vp, C.POINTER(Nets), flt, vp]),
     "cacto_update": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, C.c_int, vp, vp, vp,
                                vp, sz, vp]),
-    "cacto_rollout": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
+    "cacto_rollout": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
     "cacto_buffer_add": (C.c_int, [vp, vp, i64, i64, vp, i64, vp]),
     "cacto_buffer_gather": (C.c_int, [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp]),
     "cacto_per_init": (C.c_int, [vp, vp, i64, vp]),

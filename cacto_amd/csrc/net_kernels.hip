@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(CACTO_THREADS) k_rollout(const SysDevice* __re
                                                            const double* __restrict__ Wext, double* __restrict__ Straj,
                                                            float* __restrict__ Atraj, double* __restrict__ Rtraj,
                                                            double* __restrict__ EEtraj, int32_t* __restrict__ status,
-                                                           int B) {
+                                                           const int32_t* __restrict__ order, int B) {
   __shared__ float4 X0[64];
   __shared__ float4 H[2 * 16 * 64];
   __shared__ float4 red[4 * 64];
@@ -115,8 +115,8 @@ __global__ void __launch_bounds__(CACTO_THREADS) k_rollout(const SysDevice* __re
   const cacto_sys_params& p = sd.p;
   const Lane L;
   const int ns = p.nb_state, na = p.nb_action, s0 = blockIdx.x * CACTO_TILE;
-  const int b = s0 + L.tid;
-  const bool owner = L.tid < 16 && b < B;
+  const bool owner = L.tid < 16 && s0 + L.tid < B;
+  const int b = owner ? (order ? order[s0 + L.tid] : s0 + L.tid) : 0;
   double s[CACTO_MAX_STATE], w[8];
   int my_n = 0;
   bool alive = false;
@@ -241,14 +241,14 @@ extern "C" int cacto_critic_input_grad(const cacto_sys* sys, const float* critic
 
 extern "C" int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
                              const int32_t* nsteps_d, int T, int use_actor, const double* W_d, double* S_traj_d,
-                             float* A_traj_d, double* R_traj_d, double* EE_traj_d, int32_t* status_d, int B,
-                             void* stream) {
+                             float* A_traj_d, double* R_traj_d, double* EE_traj_d, int32_t* status_d,
+                             const int32_t* order_d, int B, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
   if (B == 0) return CACTO_OK;
   NetView v = cacto_make_view(sys, CACTO_NET_ACTOR, actor_netbuf_d);
   hipLaunchKernelGGL(k_rollout, dim3(ceil_div(B, CACTO_TILE)), dim3(CACTO_THREADS), 0, as_stream(stream), sys->dev, v,
-                     S0_d, nsteps_d, T, use_actor, W_d, S_traj_d, A_traj_d, R_traj_d, EE_traj_d, status_d, B);
+                     S0_d, nsteps_d, T, use_actor, W_d, S_traj_d, A_traj_d, R_traj_d, EE_traj_d, status_d, order_d, B);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }

@@ -92,34 +92,50 @@ class RL_AC:
         return self._ws
 
     def _cfg_for(self, B, want_vt=False):
+        """Loss means are over the global batch: B per rank times the data-parallel world."""
         cfg = L.UpdateCfg.from_buffer_copy(self.cfg)
-        if self.cfg.B_global <= 0 or getattr(self, "_dp_world", 1) == 1:
-            cfg.B_global = B
+        cfg.B_global = B * self.dp_world
         cfg.want_target_V = int(want_vt)
         return cfg
 
+    dp_world = 1
+    dp_group = None
+
+    def set_data_parallel(self, world_size, group=None):
+        """Replicated weights, local minibatch per rank, RCCL all-reduce of both gradients (the
+        critic's before its Adam step, then the actor's against the updated critic, RL.py:104-109)."""
+        self.dp_world = int(world_size)
+        self.dp_group = group
+
     # ---- gradient pieces (explicit rows; used by the DP path and the parity tests) ----
-    def critic_grad_rows(self, rows, idx, w=None, want_vt=True):
+    def critic_grad_flat(self, rows, idx, w=None, y=None, V=None, Vt=None):
         B = idx.shape[0]
         ws = self.workspace(B)
         grad = torch.empty(self.critic_model.P, dtype=torch.float32, device=DEVICE)
-        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
-        V = torch.empty_like(y)
-        Vt = torch.empty_like(y)
-        cfg = self._cfg_for(B, want_vt)
+        cfg = self._cfg_for(B, Vt is not None)
         L.lib().call("cacto_critic_grad", self.sys.handle, C.byref(self.nets), C.byref(cfg),
                      dptr(rows, torch.float64), dptr(idx, torch.int32), dptr(w), B, dptr(grad), dptr(y), dptr(V),
                      dptr(Vt), dptr(ws), ws.numel() * 4, stream())
-        return self._split(grad, self.critic_model), y.reshape(B, 1), V.reshape(B, 1), Vt.reshape(B, 1)
+        return grad
 
-    def actor_grad_rows(self, rows, idx, batch_size=None):
+    def actor_grad_flat(self, rows, idx):
         B = idx.shape[0]
         ws = self.workspace(B)
         grad = torch.empty(self.actor_model.P, dtype=torch.float32, device=DEVICE)
-        cfg = self._cfg_for(batch_size or B)
+        cfg = self._cfg_for(B)
         L.lib().call("cacto_actor_grad", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(rows, torch.float64),
                      dptr(idx, torch.int32), B, dptr(grad), dptr(ws), ws.numel() * 4, stream())
-        return self._split(grad, self.actor_model)
+        return grad
+
+    def critic_grad_rows(self, rows, idx, w=None, want_vt=True):
+        B = idx.shape[0]
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        V, Vt = torch.empty_like(y), torch.empty_like(y)
+        grad = self.critic_grad_flat(rows, idx, w, y, V, Vt if want_vt else None)
+        return self._split(grad, self.critic_model), y.reshape(B, 1), V.reshape(B, 1), Vt.reshape(B, 1)
+
+    def actor_grad_rows(self, rows, idx, batch_size=None):
+        return self._split(self.actor_grad_flat(rows, idx), self.actor_model)
 
     @staticmethod
     def _split(flat, net):
@@ -138,12 +154,23 @@ class RL_AC:
 
     # ---- RL.py:101-111 on replay rows ----
     def update_rows(self, storage, idx, is_w=None, y=None, V=None, Vt=None):
+        if self.dp_world > 1:
+            return self._update_rows_dp(storage, idx, is_w, y, V, Vt)
         B = idx.shape[0]
         ws = self.workspace(B)
         cfg = self._cfg_for(B, Vt is not None)
         L.lib().call("cacto_update", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(storage, torch.float64),
                      dptr(idx, torch.int32), dptr(is_w), B, dptr(y), dptr(V), dptr(Vt), dptr(ws), ws.numel() * 4,
                      stream())
+
+    def _update_rows_dp(self, storage, idx, is_w=None, y=None, V=None, Vt=None):
+        import torch.distributed as dist
+        gc = self.critic_grad_flat(storage, idx, is_w, y, V, Vt)
+        dist.all_reduce(gc, group=self.dp_group)                 # sum of (1/B_global)-scaled shards
+        self.apply_gradients(CRITIC, gc, soft_update=not self.conf.MC)
+        ga = self.actor_grad_flat(storage, idx)
+        dist.all_reduce(ga, group=self.dp_group)
+        self.apply_gradients(ACTOR, ga)
 
     def update(self, state_batch, state_next_rollout_batch, partial_reward_to_go_batch, dVdx_batch, d_batch,
                term_batch, weights_batch, batch_size=None):
@@ -222,12 +249,20 @@ class RL_AC:
         self.target_critic.save_weights(base + "target_critic_%s.npz" % update_step_counter)
 
     # ---- RL.py:197-233, batched over episodes on the GPU ----
-    def rollout_batch(self, S0, nsteps, T, ep=1, weights=None, want=("S", "A", "R", "EE")):
-        """Roll out len(S0) episodes in one persistent kernel (K18)."""
-        S0 = torch.as_tensor(np.asarray(S0, dtype=np.float64), device=DEVICE).contiguous()
+    def rollout_inputs(self, S0, nsteps):
+        """Device copies of the start states, lengths and the length-sorted episode order."""
+        nsteps = np.asarray(nsteps, dtype=np.int32)
+        order = np.argsort(-nsteps, kind="stable").astype(np.int32)
+        return (torch.as_tensor(np.asarray(S0, dtype=np.float64), device=DEVICE).contiguous(),
+                torch.as_tensor(nsteps, device=DEVICE).contiguous(), torch.as_tensor(order, device=DEVICE))
+
+    def rollout_batch(self, S0, nsteps, T, ep=1, weights=None, want=("S", "A", "R", "EE"), inputs=None, out=None):
+        """Roll out len(S0) episodes in one persistent kernel (K18), episodes packed by length."""
+        S0, n, order = inputs if inputs is not None else self.rollout_inputs(S0, nsteps)
         R = S0.shape[0]
         ns, na = self.conf.nb_state, self.conf.nb_action
-        n = torch.as_tensor(np.asarray(nsteps, dtype=np.int32), device=DEVICE).contiguous()
+        if out is not None:
+            return self._launch_rollout(S0, n, order, T, ep, weights, out)
         f64 = dict(dtype=torch.float64, device=DEVICE)
         out = {}
         if "S" in want:
@@ -239,10 +274,13 @@ class RL_AC:
         if "EE" in want:
             out["EE"] = torch.empty(R, T + 1, 3, **f64)
         out["status"] = torch.empty(R, dtype=torch.int32, device=DEVICE)
+        return self._launch_rollout(S0, n, order, T, ep, weights, out)
+
+    def _launch_rollout(self, S0, n, order, T, ep, weights, out):
         W = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float64), device=DEVICE)
         L.lib().call("cacto_rollout", self.sys.handle, dptr(self.actor_model.buf), dptr(S0), dptr(n), T,
                      int(ep != 0), dptr(W), dptr(out.get("S")), dptr(out.get("A")), dptr(out.get("R")),
-                     dptr(out.get("EE")), dptr(out["status"]), R, stream())
+                     dptr(out.get("EE")), dptr(out.get("status")), dptr(order), S0.shape[0], stream())
         return out
 
     def nsteps_sh(self, s0):

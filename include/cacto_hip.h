@@ -217,11 +217,13 @@ int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_updat
  *   s_{t+1}, r_t = Env.step(W, s_t, a_t), ee_{t+1} = EE(s_{t+1}).
  * Outputs (any may be NULL): S_traj [B,T+1,ns] f64, A_traj [B,T,na] f32, R_traj [B,T] f64,
  * EE_traj [B,T+1,3] f64. Steps past nsteps_d[b] are not written. W_d: weights [n_weights] or NULL
- * (running). status_d [B] int32 (optional): 0 ok, 1 NaN state encountered (RL.py:229-231). */
+ * (running). status_d [B] int32 (optional): 0 ok, 1 NaN state encountered (RL.py:229-231).
+ * order_d [B] int32 (optional): workgroup slot k runs episode order_d[k] (a permutation). Passing
+ * the episodes sorted by length packs equal-length episodes into the same 16-episode MFMA tile. */
 int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
                   const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
                   double* S_traj_d, float* A_traj_d, double* R_traj_d, double* EE_traj_d,
-                  int32_t* status_d, int B, void* stream);
+                  int32_t* status_d, const int32_t* order_d, int B, void* stream);
 
 /* ---------------------------------------------------------------- replay ------------------ */
 
