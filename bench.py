@@ -176,11 +176,12 @@ def fill_buffer(rl, conf, roll, seed):
         term[-1] = 1
         rows.append(np.concatenate([S[e, :T + 1], partial[:, None], snext, gen.standard_normal((T + 1, ns)),
                                     done[:, None], term[:, None]], axis=1))
-        if sum(len(x) for x in rows) >= conf.REPLAY_SIZE:
+        if sum(len(x) for x in rows) >= conf.REPLAY_SIZE + 8192:
             break
-    rows = np.concatenate(rows)[:conf.REPLAY_SIZE]
+    rows = np.concatenate(rows)
     buf = ReplayBuffer(conf, rl.sys)
-    buf.add_rows(rows)
+    for k in range(0, len(rows), 8192):     # per-batch adds, so the ring wraps and `full` latches
+        buf.add_rows(rows[k:k + 8192])
     return buf
 
 
