@@ -151,6 +151,26 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
                 total_steps=sum_over_ranks(steps_per_call * K, world))
 
 
+def rollout_diagnostics(rl, conf, roll, K=5):
+    """Kernel time of variants of the same rollout batch: states+actions only (create_TO_init
+    outputs), zero controls (ep == 0: dynamics/reward/EE only)."""
+    T = roll["T"]
+    inputs = rl.rollout_inputs(roll["S0"], roll["nsteps"])
+    out = roll["out"]
+    res = {}
+    for name, o, ep in (("states_actions_only", {"S": out["S"], "A": out["A"]}, 1),
+                        ("ep0_zero_controls", out, 0)):
+        rl.rollout_batch(None, None, T, ep=ep, inputs=inputs, out=o)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(K):
+            rl.rollout_batch(None, None, T, ep=ep, inputs=inputs, out=o)
+        e1.record()
+        torch.cuda.synchronize()
+        res[name + "_kernel_ms"] = e0.elapsed_time(e1) / K
+    return res
+
+
 def fill_buffer(rl, conf, roll, seed):
     """Replay rows from the rollouts (RL_Solve n-step targets, RL.py:145-189, vectorised over
     episodes; rewards = the rollout rewards, dVdx synthetic N(0,1))."""
@@ -257,6 +277,7 @@ def main():
     roll = rollout_phase(rl, conf, env, args.rollouts, args.steps, args.warmup, world, rank)
     value = roll["total_steps"] / roll["wall"]
     achieved = roll["steps_per_call"] * fa_flops(ns, na) / (roll["kernel_ms"] * 1e-3)
+    diag = rollout_diagnostics(rl, conf, roll)
     buf = fill_buffer(rl, conf, roll, seed=rank)
     updates = {}
     for B in [int(b) for b in args.batches.split(",") if b]:
@@ -309,6 +330,7 @@ def main():
                          "traffic": None, "kernel_ms": roll["kernel_ms"],
                          "flop_per_env_step": fa_flops(ns, na)},
             "critic_updates": updates,
+            "rollout_diagnostics": diag,
             "cpu_baseline": cpu,
             "extra_systems": extra,
         }

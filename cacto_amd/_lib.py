@@ -23,7 +23,7 @@ class SysParams(C.Structure):
         ("dyn_kind", C.c_int32), ("reward_kind", C.c_int32), ("nb_state", C.c_int32),
         ("nb_action", C.c_int32), ("nq", C.c_int32), ("nv", C.c_int32), ("normalize", C.c_int32),
         ("n_joints", C.c_int32), ("ee_parent", C.c_int32), ("n_check", C.c_int32),
-        ("n_weights", C.c_int32), ("pad0", C.c_int32),
+        ("n_weights", C.c_int32), ("const_dyn", C.c_int32),
         ("dt", C.c_double), ("state_norm", C.c_double * MAX_STATE), ("u_max", C.c_double * MAX_ACTION),
         ("w_b", C.c_double), ("scale", C.c_double), ("offset", C.c_double), ("alpha", C.c_double),
         ("alpha2", C.c_double), ("obs", C.c_double * 18), ("target", C.c_double * 3),

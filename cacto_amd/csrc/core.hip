@@ -40,7 +40,8 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
     }
     if (p.dyn_kind == CACTO_DYN_CHAIN) {
       CACTO_REQUIRE(joint_table_h != nullptr, "cacto_sys_create: chain dynamics needs a joint table");
-      CACTO_REQUIRE(p.n_joints >= 1 && p.n_joints <= CACTO_MAX_JOINTS, "cacto_sys_create: n_joints out of range");
+      CACTO_REQUIRE(p.n_joints == 2 || p.n_joints == 3 || p.n_joints == 6,
+                    "cacto_sys_create: chains of 2, 3 or 6 joints are instantiated in this build");
       CACTO_REQUIRE(p.nq == p.n_joints && p.nv == p.n_joints && p.nb_state == 2 * p.n_joints + 1 &&
                         p.nb_action == p.n_joints,
                     "cacto_sys_create: chain needs nq = nv = na = n_joints, ns = 2n + 1");
@@ -48,13 +49,19 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
       for (int i = 0; i < p.n_joints; ++i) {
         const int parent = (int)joint_table_h[i * CACTO_JOINT_COLS];
         const int kind = (int)joint_table_h[i * CACTO_JOINT_COLS + 1];
-        CACTO_REQUIRE(parent >= -1 && parent < i, "cacto_sys_create: joints must be in depth-first order");
+        CACTO_REQUIRE(parent == i - 1, "cacto_sys_create: only serial chains (parent = i - 1) are supported");
         CACTO_REQUIRE(kind == 0 || kind == 1, "cacto_sys_create: joint type must be revolute(0)/prismatic(1)");
       }
     }
     CACTO_REQUIRE(p.n_weights >= 7 && p.n_weights <= 8, "cacto_sys_create: n_weights must be 7 or 8");
     SysDevice host{};
     host.p = p;
+    host.p.const_dyn = 0;
+    if (p.dyn_kind == CACTO_DYN_CHAIN) {
+      bool all_prismatic = true;
+      for (int i = 0; i < p.n_joints; ++i) all_prismatic = all_prismatic && (int)joint_table_h[i * CACTO_JOINT_COLS + 1] == 1;
+      host.p.const_dyn = all_prismatic ? 1 : 0;
+    }
     if (joint_table_h && p.dyn_kind == CACTO_DYN_CHAIN)
       std::memcpy(host.joints, joint_table_h, sizeof(double) * p.n_joints * CACTO_JOINT_COLS);
     cacto_sys* s = new cacto_sys();

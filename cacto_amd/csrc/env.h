@@ -215,117 +215,126 @@ __device__ __forceinline__ SV joint_S(const JointView& j) {
 }
 __device__ __forceinline__ double sdot(const SV& S, const SV& f) { return dot(S.l, f.l) + dot(S.a, f.a); }
 
-// M(q) via CRBA and h(q, v) via RNEA (qdd = 0, a_0 = -gravity), Featherstone / Pinocchio.
-__device__ inline void chain_terms(const SysDevice& sd, const double* q, const double* v, double* M,
-                                   double* h) {
-  const int n = sd.p.n_joints;
-  SE3 X[CACTO_MAX_JOINTS];
-  SV vel[CACTO_MAX_JOINTS], acc[CACTO_MAX_JOINTS], f[CACTO_MAX_JOINTS];
-  Inertia Ic[CACTO_MAX_JOINTS];
+// M(q) via CRBA and h(q, v) via RNEA (qdd = 0, a_0 = -gravity), Featherstone / Pinocchio, for a
+// serial chain of NJ joints (parent(i) = i - 1, validated at cacto_sys_create). NJ is a template
+// parameter so every per-joint array lives in registers.
+template <int NJ>
+__device__ inline void chain_terms(const SysDevice& sd, const double* q, const double* v, double* M, double* h) {
+  SE3 X[NJ];
+  SV vel[NJ], acc[NJ], f[NJ];
+  Inertia Ic[NJ];
   const SV gacc{v3(-sd.p.gravity[0], -sd.p.gravity[1], -sd.p.gravity[2]), v3(0, 0, 0)};
-  for (int i = 0; i < n; ++i) {
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
     JointView j{sd.joints + i * CACTO_JOINT_COLS};
     X[i] = joint_placement(j, q[i]);
     const SV S = joint_S(j);
-    const int pa = j.parent();
-    SV vp = pa < 0 ? SV{v3(0, 0, 0), v3(0, 0, 0)} : vel[pa];
-    SV ap = pa < 0 ? gacc : acc[pa];
+    const SV vp = i == 0 ? SV{v3(0, 0, 0), v3(0, 0, 0)} : vel[i - 1];
+    const SV ap = i == 0 ? gacc : acc[i - 1];
     SV vi = act_motion_inv(X[i], vp);
-    SV Sq{v[i] * S.l, v[i] * S.a};
+    const SV Sq{v[i] * S.l, v[i] * S.a};
     vi.l = vi.l + Sq.l;
     vi.a = vi.a + Sq.a;
     SV ai = act_motion_inv(X[i], ap);
-    SV c = cross_motion(vi, Sq);
+    const SV c = cross_motion(vi, Sq);
     ai.l = ai.l + c.l;
     ai.a = ai.a + c.a;
     vel[i] = vi;
     acc[i] = ai;
     Ic[i] = j.inertia();
-    SV Iv = inertia_mul(Ic[i], vi);
-    SV Ia = inertia_mul(Ic[i], ai);
-    SV vf = cross_force(vi, Iv);
+    const SV Iv = inertia_mul(Ic[i], vi);
+    const SV Ia = inertia_mul(Ic[i], ai);
+    const SV vf = cross_force(vi, Iv);
     f[i].l = Ia.l + vf.l;
     f[i].a = Ia.a + vf.a;
   }
-  for (int i = n - 1; i >= 0; --i) {
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
     JointView j{sd.joints + i * CACTO_JOINT_COLS};
     h[i] = sdot(joint_S(j), f[i]);
-    const int pa = j.parent();
-    if (pa >= 0) {
-      SV fp = act_force(X[i], f[i]);
-      f[pa].l = f[pa].l + fp.l;
-      f[pa].a = f[pa].a + fp.a;
-      add_inertia(Ic[pa], act_inertia(X[i], Ic[i]));
+    if (i > 0) {
+      const SV fp = act_force(X[i], f[i]);
+      f[i - 1].l = f[i - 1].l + fp.l;
+      f[i - 1].a = f[i - 1].a + fp.a;
+      add_inertia(Ic[i - 1], act_inertia(X[i], Ic[i]));
     }
   }
-  // CRBA with the composite inertias (accumulated above, children before parents)
-  for (int i = 0; i < n; ++i) {
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
     JointView j{sd.joints + i * CACTO_JOINT_COLS};
     SV F = inertia_mul(Ic[i], joint_S(j));
-    M[i * n + i] = sdot(joint_S(j), F);
-    int k = i;
-    while (true) {
-      JointView jk{sd.joints + k * CACTO_JOINT_COLS};
-      const int pk = jk.parent();
-      if (pk < 0) break;
+    M[i * NJ + i] = sdot(joint_S(j), F);
+#pragma unroll
+    for (int k = i; k > 0; --k) {
       F = act_force(X[k], F);
-      k = pk;
-      JointView jp{sd.joints + k * CACTO_JOINT_COLS};
+      JointView jp{sd.joints + (k - 1) * CACTO_JOINT_COLS};
       const double mij = sdot(joint_S(jp), F);
-      M[i * n + k] = mij;
-      M[k * n + i] = mij;
+      M[i * NJ + (k - 1)] = mij;
+      M[(k - 1) * NJ + i] = mij;
     }
   }
 }
 
-// In-place Cholesky of SPD M (n x n); returns false if not positive definite.
-__device__ inline bool cholesky(double* L, int n) {
-  for (int j = 0; j < n; ++j) {
-    double d = L[j * n + j];
-    for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
-    if (!(d > 0.0)) return false;
+// In-place Cholesky of SPD M (NJ x NJ); returns false if not positive definite.
+template <int NJ>
+__device__ inline bool cholesky(double* L) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    double d = L[j * NJ + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= L[j * NJ + k] * L[j * NJ + k];
+    ok = ok && d > 0.0;
     d = sqrt(d);
-    L[j * n + j] = d;
-    for (int i = j + 1; i < n; ++i) {
-      double s = L[i * n + j];
-      for (int k = 0; k < j; ++k) s -= L[i * n + k] * L[j * n + k];
-      L[i * n + j] = s / d;
+    L[j * NJ + j] = d;
+#pragma unroll
+    for (int i = j + 1; i < NJ; ++i) {
+      double s = L[i * NJ + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) s -= L[i * NJ + k] * L[j * NJ + k];
+      L[i * NJ + j] = s / d;
     }
   }
-  return true;
+  return ok;
 }
-__device__ inline void chol_solve(const double* L, int n, double* x) {
-  for (int i = 0; i < n; ++i) {
+template <int NJ>
+__device__ inline void chol_solve(const double* L, double* x) {
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
     double s = x[i];
-    for (int k = 0; k < i; ++k) s -= L[i * n + k] * x[k];
-    x[i] = s / L[i * n + i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= L[i * NJ + k] * x[k];
+    x[i] = s / L[i * NJ + i];
   }
-  for (int i = n - 1; i >= 0; --i) {
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
     double s = x[i];
-    for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * x[k];
-    x[i] = s / L[i * n + i];
+#pragma unroll
+    for (int k = i + 1; k < NJ; ++k) s -= L[k * NJ + i] * x[k];
+    x[i] = s / L[i * NJ + i];
   }
 }
 
 // EE frame translation (forward kinematics to the EE parent joint, then the fixed placement).
+template <int NJ>
 __device__ inline V3 chain_ee(const SysDevice& sd, const double* q) {
-  const int n = sd.p.n_joints;
-  M3 oR[CACTO_MAX_JOINTS];
-  V3 op[CACTO_MAX_JOINTS];
-  for (int i = 0; i < n; ++i) {
-    JointView j{sd.joints + i * CACTO_JOINT_COLS};
-    SE3 X = joint_placement(j, q[i]);
-    const int pa = j.parent();
-    if (pa < 0) {
-      oR[i] = X.R;
-      op[i] = X.p;
-    } else {
-      oR[i] = mul(oR[pa], X.R);
-      op[i] = mul(oR[pa], X.p) + op[pa];
-    }
-  }
+  M3 oR;
+  V3 op, ee = v3(0, 0, 0);
   const int e = sd.p.ee_parent;
-  return mul(oR[e], v3(sd.p.ee_p[0], sd.p.ee_p[1], sd.p.ee_p[2])) + op[e];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    const SE3 X = joint_placement(j, q[i]);
+    if (i == 0) {
+      oR = X.R;
+      op = X.p;
+    } else {
+      op = mul(oR, X.p) + op;
+      oR = mul(oR, X.R);
+    }
+    if (i == e) ee = mul(oR, v3(sd.p.ee_p[0], sd.p.ee_p[1], sd.p.ee_p[2])) + op;
+  }
+  return ee;
 }
 
 // ------------------------------------------------------------------ environment functions
@@ -333,73 +342,117 @@ __device__ inline V3 chain_ee(const SysDevice& sd, const double* q) {
 // Env.simulate. `f32in`: state/action originate from float32 tensors (compute_actor_grad path),
 // which makes `v*dt` a float32 product and `self.v += dv*dt` round to float32 (numpy in-place on a
 // float32 view, robot_utils.py:403-405); otherwise all float64 (rollouts). environment.py:80-91.
-__device__ inline bool env_simulate(const SysDevice& sd, const double* s, const double* a, bool f32in,
-                                    double* out) {
-  const cacto_sys_params& p = sd.p;
-  const int ns = p.nb_state;
-  const double dt = p.dt;
-  if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) {  // environment.py:235-243
+// NJ = 0: single integrator (environment.py:235-243); NJ > 0: Pinocchio chain with NJ joints.
+template <int NJ>
+__device__ inline bool env_simulate(const SysDevice& sd, const double* s, const double* a, bool f32in, double* out) {
+  const double dt = sd.p.dt;
+  if constexpr (NJ == 0) {
     out[0] = s[0] + dt * a[0];
     out[1] = s[1] + dt * a[1];
     out[2] = s[2] + dt;
     return true;
-  }
-  if (p.dyn_kind == CACTO_DYN_CHAIN) {
-    const int n = p.n_joints;
-    double M[CACTO_MAX_JOINTS * CACTO_MAX_JOINTS], h[CACTO_MAX_JOINTS], dv[CACTO_MAX_JOINTS];
-    chain_terms(sd, s, s + n, M, h);
-    for (int i = 0; i < n; ++i) dv[i] = a[i] - h[i];
-    bool ok = cholesky(M, n);
-    chol_solve(M, n, dv);
-    for (int i = 0; i < n; ++i) {
-      const double v = s[n + i];
+  } else {
+    double M[NJ * NJ], h[NJ], dv[NJ];
+    chain_terms<NJ>(sd, s, s + NJ, M, h);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) dv[i] = a[i] - h[i];
+    const bool ok = cholesky<NJ>(M);
+    chol_solve<NJ>(M, dv);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      const double v = s[NJ + i];
       if (f32in) {
         const float vdt = __fmul_rn((float)v, (float)dt);
         out[i] = s[i] + (double)vdt;
-        out[n + i] = (double)(float)(v + dv[i] * dt);
+        out[NJ + i] = (double)(float)(v + dv[i] * dt);
       } else {
         out[i] = s[i] + v * dt;
-        out[n + i] = v + dv[i] * dt;
+        out[NJ + i] = v + dv[i] * dt;
       }
     }
-    out[ns - 1] = s[ns - 1] + dt;
+    out[2 * NJ] = s[2 * NJ] + dt;
     return ok;
   }
-  return false;
+}
+
+// Prismatic-only chains (const_dyn): M and nle do not depend on (q, v) (no rotation; see
+// DESIGN.md), so the rollout factors M once per episode and reuses it every step.
+template <int NJ>
+struct ConstDyn {
+  double L[NJ > 0 ? NJ * NJ : 1];
+  double h[NJ > 0 ? NJ : 1];
+};
+template <int NJ>
+__device__ inline void const_dyn_init(const SysDevice& sd, const double* s, ConstDyn<NJ>& cd) {
+  if constexpr (NJ > 0) {
+    chain_terms<NJ>(sd, s, s + NJ, cd.L, cd.h);
+    cholesky<NJ>(cd.L);
+  }
+}
+template <int NJ>
+__device__ inline void env_simulate_const(const SysDevice& sd, const ConstDyn<NJ>& cd, const double* s, const double* a,
+                                          double* out) {
+  if constexpr (NJ > 0) {
+    const double dt = sd.p.dt;
+    double dv[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) dv[i] = a[i] - cd.h[i];
+    chol_solve<NJ>(cd.L, dv);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      const double v = s[NJ + i];
+      out[i] = s[i] + v * dt;
+      out[NJ + i] = v + dv[i] * dt;
+    }
+    out[2 * NJ] = s[2 * NJ] + dt;
+  }
 }
 
 // Env.derivative (environment.py:93-109 / SI :209-219): Fu[ns, na] row-major, rows scaled by
 // 1/state_norm when NORMALIZE_INPUTS.
+template <int NJ>
 __device__ inline void env_derivative(const SysDevice& sd, const double* s, double* Fu) {
   const cacto_sys_params& p = sd.p;
-  const int ns = p.nb_state, na = p.nb_action;
-  for (int k = 0; k < ns * na; ++k) Fu[k] = 0.0;
-  if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) {
-    Fu[0 * na + 0] = p.dt;
-    Fu[1 * na + 1] = p.dt;
-  } else if (p.dyn_kind == CACTO_DYN_CHAIN) {
-    const int n = p.n_joints;
-    double M[CACTO_MAX_JOINTS * CACTO_MAX_JOINTS], h[CACTO_MAX_JOINTS], zero[CACTO_MAX_JOINTS];
-    for (int i = 0; i < n; ++i) zero[i] = 0.0;
-    chain_terms(sd, s, zero, M, h);
-    cholesky(M, n);
-    for (int c = 0; c < n; ++c) {  // column c of Minv
-      double x[CACTO_MAX_JOINTS];
-      for (int i = 0; i < n; ++i) x[i] = (i == c) ? 1.0 : 0.0;
-      chol_solve(M, n, x);
-      for (int i = 0; i < n; ++i) Fu[(p.nv + i) * na + c] = x[i] * p.dt;
+  constexpr int NS = NJ == 0 ? 3 : 2 * NJ + 1;
+  constexpr int NA = NJ == 0 ? 2 : NJ;
+#pragma unroll
+  for (int k = 0; k < NS * NA; ++k) Fu[k] = 0.0;
+  if constexpr (NJ == 0) {
+    Fu[0 * NA + 0] = p.dt;
+    Fu[1 * NA + 1] = p.dt;
+  } else {
+    double M[NJ * NJ], h[NJ], zero[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) zero[i] = 0.0;
+    chain_terms<NJ>(sd, s, zero, M, h);
+    cholesky<NJ>(M);
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {  // column c of Minv
+      double x[NJ];
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) x[i] = (i == c) ? 1.0 : 0.0;
+      chol_solve<NJ>(M, x);
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) Fu[(NJ + i) * NA + c] = x[i] * p.dt;
     }
   }
-  if (p.normalize)
-    for (int r = 0; r < ns - 1; ++r) {
+  if (p.normalize) {
+#pragma unroll
+    for (int r = 0; r < NS - 1; ++r) {
       const double inv = 1.0 / p.state_norm[r];
-      for (int c = 0; c < na; ++c) Fu[r * na + c] *= inv;
+#pragma unroll
+      for (int c = 0; c < NA; ++c) Fu[r * NA + c] *= inv;
     }
+  }
 }
 
+template <int NJ>
 __device__ inline V3 env_ee(const SysDevice& sd, const double* s) {
-  if (sd.p.dyn_kind == CACTO_DYN_CHAIN) return chain_ee(sd, s);
-  return v3(s[0], s[1], 0.0);  // SI / car: environment.py:245-250
+  if constexpr (NJ == 0) {
+    return v3(s[0], s[1], 0.0);  // SI / car: environment.py:245-250
+  } else {
+    return chain_ee<NJ>(sd, s);
+  }
 }
 
 __device__ __forceinline__ double ell_cost(const cacto_sys_params& p, double x, double y, double xc,
@@ -409,18 +462,47 @@ __device__ __forceinline__ double ell_cost(const cacto_sys_params& p, double x, 
 }
 
 // bound_control_cost (environment.py:158-163), float64
+template <int NA>
 __device__ inline double bound_control_cost(const cacto_sys_params& p, const double* a) {
   double u = 0.0;
-  for (int i = 0; i < p.nb_action; ++i) u += a[i] * a[i] + p.w_b * pow(a[i] / p.u_max[i], 10.0);
+#pragma unroll
+  for (int i = 0; i < NA; ++i) u += a[i] * a[i] + p.w_b * pow(a[i] / p.u_max[i], 10.0);
   return u;
 }
 
 // Env.reward (float64). `f32state`: the state came from a float32 tensor (affects the float32
 // numpy dot of the manipulator velocity term). a may be nullptr (reward(w, s) with action=None).
+// Reward pieces that the rollout kernel evaluates on different waves (same formulas as env_reward).
+__device__ __forceinline__ double peak_cost(const cacto_sys_params& p, double x, double y) {
+  const double dx = x - p.target[0], dy = y - p.target[1];
+  const double s01 = sqrt(0.1);
+  double pk = sqrt(dx * dx + 0.1);
+  pk = pk - s01;
+  pk = pk - 0.1;
+  pk = pk + sqrt(dy * dy + 0.1);
+  pk = pk - s01;
+  pk = pk - 0.1;
+  return log(exp(p.alpha2 * -pk) + 1.0) / p.alpha2;
+}
+// r = scale*(-w0*dist + w1*peak [- w2*vel] - w3*ell1 - w4*ell2 - w5*ell3 - w6*u_cost + offset),
+// evaluated left to right as the reference's Python expression.
+__device__ __forceinline__ double combine_reward(const cacto_sys_params& p, const double* w, double x, double y,
+                                                 double peak, double vel, bool has_vel, double ell1, double ell2,
+                                                 double ell3, double u_cost) {
+  const double dx = x - p.target[0], dy = y - p.target[1];
+  const double dist = dx * dx + dy * dy;
+  double r = -w[0] * dist + w[1] * peak;
+  if (has_vel) r = r - w[2] * vel;
+  r = r - w[3] * ell1 - w[4] * ell2 - w[5] * ell3 - w[6] * u_cost + p.offset;
+  return p.scale * r;
+}
+
+template <int NJ>
 __device__ inline double env_reward(const SysDevice& sd, const double* w, const double* s, const double* a,
                                     bool f32state) {
+  constexpr int NA = NJ == 0 ? 2 : NJ;
   const cacto_sys_params& p = sd.p;
-  const V3 e = env_ee(sd, s);
+  const V3 e = env_ee<NJ>(sd, s);
   const double x = e.x, y = e.y;
   const double* o = p.obs;
   const double ell1 = ell_cost(p, x, y, o[0], o[1], o[6], o[7]);
@@ -435,19 +517,20 @@ __device__ inline double env_reward(const SysDevice& sd, const double* w, const 
   pk = pk - s01;
   pk = pk - 0.1;
   const double peak = log(exp(p.alpha2 * -pk) + 1.0) / p.alpha2;
-  const double u_cost = a ? bound_control_cost(p, a) : 0.0;
+  const double u_cost = a ? bound_control_cost<NA>(p, a) : 0.0;
   const double dist = dx * dx + dy * dy;
   double r = -w[0] * dist + w[1] * peak;
-  if (p.reward_kind == CACTO_REW_MANIPULATOR) {
+  if (NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR) {
     double vel = 0.0;
     if (w[2] != 0.0) {
-      const int nq = p.nq;
       if (f32state) {
         float acc = 0.0f;
-        for (int k = 0; k < p.nv; ++k) acc = __fadd_rn(acc, __fmul_rn((float)s[nq + k], (float)s[nq + k]));
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) acc = __fadd_rn(acc, __fmul_rn((float)s[NJ + k], (float)s[NJ + k]));
         vel = acc;
       } else {
-        for (int k = 0; k < p.nv; ++k) vel += s[nq + k] * s[nq + k];
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) vel += s[NJ + k] * s[NJ + k];
       }
     }
     r = r - w[2] * vel;
@@ -459,12 +542,14 @@ __device__ inline double env_reward(const SysDevice& sd, const double* w, const 
 // reward_batch's TF float32 part and its tape gradient (environment.py:282-286 and the dr_da tape
 // of NeuralNetwork.py:199-204): r = scale*(-w6*u_cost) + f32(partial);
 // u_cost = sum(a^2 + w_b*(a/u_max)^10); gradient in TF's op order (Mul/Pow/RealDiv grads).
+template <int NA>
 __device__ inline float reward_batch_f32(const cacto_sys_params& p, double w6, const float* a, double partial,
                                          float* dr_da) {
   const float scale = (float)p.scale, wb = (float)p.w_b, nw6 = (float)(-w6);
   float u = 0.0f;
   const float g = __fmul_rn(nw6, scale);
-  for (int i = 0; i < p.nb_action; ++i) {
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
     const float umax = (float)p.u_max[i];
     const float D = __fdiv_rn(a[i], umax);
     const float t = __fadd_rn(__fmul_rn(a[i], a[i]), __fmul_rn(wb, powf(D, 10.0f)));
@@ -476,6 +561,26 @@ __device__ inline float reward_batch_f32(const cacto_sys_params& p, double w6, c
     }
   }
   return __fadd_rn(__fmul_rn(scale, __fmul_rn(nw6, u)), (float)partial);
+}
+
+template <int NJ>
+struct Dims {
+  static constexpr int NS = NJ == 0 ? 3 : 2 * NJ + 1;
+  static constexpr int NA = NJ == 0 ? 2 : NJ;
+};
+
+// Dispatch a templated launcher on the system's dynamics: F<NJ>::run(args...).
+template <template <int> class F, typename... Args>
+inline int dispatch_nj(const cacto_sys_params& p, Args&&... args) {
+  if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) return F<0>::run(args...);
+  switch (p.n_joints) {
+    case 2: return F<2>::run(args...);
+    case 3: return F<3>::run(args...);
+    case 6: return F<6>::run(args...);
+    default: break;
+  }
+  set_error("unsupported joint count (this build instantiates 2, 3 and 6)");
+  return CACTO_EUNSUPPORTED;
 }
 
 }  // namespace cacto

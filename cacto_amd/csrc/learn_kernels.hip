@@ -214,6 +214,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
 }
 
 // ---------------------------------------------------------------- actor chain (a12)
+template <int NJ>
 __global__ void __launch_bounds__(CACTO_THREADS)
     k_actor_grad(const SysDevice* __restrict__ sdp, NetView Ac, NetView C, ChainScalars cs,
                  const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
@@ -255,22 +256,29 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   __syncthreads();
   // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
   if (L.tid < 16) {
+    constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
     const int c = L.tid;
-    double s[CACTO_MAX_STATE], a[CACTO_MAX_ACTION], sn[CACTO_MAX_STATE], F[CACTO_MAX_STATE * CACTO_MAX_ACTION], w[8];
-    float af[CACTO_MAX_ACTION], g[CACTO_MAX_ACTION];
-    for (int f = 0; f < ns; ++f) s[f] = (double)st[c * 16 + f];
-    for (int i = 0; i < na; ++i) {
+    double s[NS], a[NA], sn[NS], F[NS * NA], w[8];
+    float af[NA], g[NA];
+#pragma unroll
+    for (int f = 0; f < NS; ++f) s[f] = (double)st[c * 16 + f];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
       af[i] = A[c * na + i];
       a[i] = (double)af[i];
     }
-    env_simulate(sd, s, a, true, sn);
-    for (int f = 0; f < 16; ++f) stn[c * 16 + f] = f < ns ? (float)sn[f] : 0.f;
-    env_derivative(sd, s, F);
-    for (int k = 0; k < ns * na; ++k) Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
-    for (int k = 0; k < p.n_weights; ++k) w[k] = term_c * p.w_terminal[k] + (1.0 - term_c) * p.w_running[k];
-    const double partial = env_reward(sd, w, s, nullptr, true);
-    (void)reward_batch_f32(p, w[6], af, partial, g);
-    for (int i = 0; i < na; ++i) dra[c * na + i] = g[i];
+    env_simulate<NJ>(sd, s, a, true, sn);
+#pragma unroll
+    for (int f = 0; f < 16; ++f) stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
+    env_derivative<NJ>(sd, s, F);
+#pragma unroll
+    for (int k = 0; k < NS * NA; ++k) Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = k >= p.n_weights ? 0.0 : term_c * p.w_terminal[k] + (1.0 - term_c) * p.w_running[k];
+    const double partial = env_reward<NJ>(sd, w, s, nullptr, true);
+    (void)reward_batch_f32<NA>(p, w[6], af, partial, g);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) dra[c * na + i] = g[i];
   }
   __syncthreads();
   if (L.wave == 0) fill_input_tile(p, stn, XS, L);
@@ -461,6 +469,18 @@ using namespace cacto;
 
 namespace {
 
+template <int NJ>
+struct LaunchActorChain {
+  static int run(const cacto_sys* sys, NetView Ac, NetView C, ChainScalars cs, const double* storage,
+                 const int32_t* idx, int B, GradBufs gb, int32_t* step, hipStream_t st) {
+    const int Bp = (B + 15) / 16 * 16;
+    hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage, idx,
+                       B, gb, step);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
+};
+
 constexpr int WG_CHUNK = 256;
 
 struct Workspace {
@@ -588,9 +608,8 @@ int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, c
   NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
   NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
   const ChainScalars cs = chain_scalars(cfg, B);
-  hipLaunchKernelGGL(k_actor_grad, dim3(w.Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage, idx, B,
-                     w.act, nets->step_d);
-  CACTO_CHECK_HIP(hipGetLastError());
+  if (int e = dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st))
+    return e;
   WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
   const int waves = a.nch * a.tpc;
   hipLaunchKernelGGL(k_wgrad, dim3((waves + 3) / 4), dim3(256), 0, st, a, w.slab);

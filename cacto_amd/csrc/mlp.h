@@ -73,25 +73,55 @@ struct NetView {
 };
 
 // out-tile loop of one layer: each wave takes out tiles ot = wave, wave+4, ...; X = LDS tiles.
-template <typename Epi>
-__device__ __forceinline__ void mm_layer(const float4* __restrict__ A, int OT, int KT, const float4* X,
-                                         int wave, int lane, Epi&& epi) {
-  for (int ot = wave; ot < OT; ot += CACTO_NWAVES) {
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float4* Ap = A + (size_t)ot * KT * 64 + lane;
-    if (KT >= 2) {
-      floatx4 acc2 = {0.f, 0.f, 0.f, 0.f};
-      int kt = 0;
-      for (; kt + 1 < KT; kt += 2) {
-        acc = mfma_block(Ap[kt * 64], X[kt * 64 + lane], acc);
-        acc2 = mfma_block(Ap[(kt + 1) * 64], X[(kt + 1) * 64 + lane], acc2);
-      }
-      if (kt < KT) acc = mfma_block(Ap[kt * 64], X[kt * 64 + lane], acc);
-      acc = acc + acc2;
-    } else {
-      acc = mfma_block(Ap[0], X[lane], acc);
+// All KT weight fragments of a tile are issued before its MFMAs, and the next tile's fragments
+// are in flight while the current tile's MFMAs run (the A operand comes from L2, so the load
+// latency is paid once per layer rather than once per k-step).
+template <int KT, typename Epi>
+__device__ __forceinline__ void mm_layer_t(const float4* __restrict__ A, int OT, const float4* X, int wave, int lane,
+                                           Epi&& epi) {
+  int ot = wave;
+  if (ot >= OT) return;
+  float4 a[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) a[k] = A[((size_t)ot * KT + k) * 64 + lane];
+  while (true) {
+    const int nxt = ot + CACTO_NWAVES;
+    float4 an[KT];
+    if (nxt < OT) {
+#pragma unroll
+      for (int k = 0; k < KT; ++k) an[k] = A[((size_t)nxt * KT + k) * 64 + lane];
     }
-    epi(ot, acc);
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const float4 b = X[k * 64 + lane];
+      if (k & 1)
+        acc1 = mfma_block(a[k], b, acc1);
+      else
+        acc0 = mfma_block(a[k], b, acc0);
+    }
+    epi(ot, acc0 + acc1);
+    if (nxt >= OT) break;
+    ot = nxt;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) a[k] = an[k];
+  }
+}
+
+template <typename Epi>
+__device__ __forceinline__ void mm_layer(const float4* __restrict__ A, int OT, int KT, const float4* X, int wave,
+                                         int lane, Epi&& epi) {
+  switch (KT) {
+    case 1: mm_layer_t<1>(A, OT, X, wave, lane, epi); break;
+    case 4: mm_layer_t<4>(A, OT, X, wave, lane, epi); break;
+    case 8: mm_layer_t<8>(A, OT, X, wave, lane, epi); break;
+    case 16: mm_layer_t<16>(A, OT, X, wave, lane, epi); break;
+    default:
+      for (int ot = wave; ot < OT; ot += CACTO_NWAVES) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < KT; ++kt) acc = mfma_block(A[((size_t)ot * KT + kt) * 64 + lane], X[kt * 64 + lane], acc);
+        epi(ot, acc);
+      }
   }
 }
 

@@ -24,7 +24,17 @@ template <typename Epi>
 __device__ __forceinline__ void mm_single_tile(const float4* __restrict__ A, int KT, const float4* X, float4* red,
                                                const Lane& L, Epi&& epi) {
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int kt = L.wave; kt < KT; kt += CACTO_NWAVES) acc = mfma_block(A[kt * 64 + L.lane], X[kt * 64 + L.lane], acc);
+  float4 a[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kt = L.wave + 4 * i;
+    a[i] = kt < KT ? A[kt * 64 + L.lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kt = L.wave + 4 * i;
+    if (kt < KT) acc = mfma_block(a[i], X[kt * 64 + L.lane], acc);
+  }
   red[L.wave * 64 + L.lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
   __syncthreads();
   if (L.wave == 0) {

@@ -96,91 +96,288 @@ __global__ void __launch_bounds__(CACTO_THREADS) k_critic_forward(const SysDevic
 }
 
 // ---------------------------------------------------------------- rollout (K18)
-// One workgroup = 16 episodes. Threads 0..15 own one episode's float64 state; the 4 waves run the
-// actor MFMA tile each step.
-__global__ void __launch_bounds__(CACTO_THREADS) k_rollout(const SysDevice* __restrict__ sdp, NetView N,
-                                                           const double* __restrict__ S0,
-                                                           const int32_t* __restrict__ nsteps, int T, int use_actor,
-                                                           const double* __restrict__ Wext, double* __restrict__ Straj,
-                                                           float* __restrict__ Atraj, double* __restrict__ Rtraj,
-                                                           double* __restrict__ EEtraj, int32_t* __restrict__ status,
-                                                           const int32_t* __restrict__ order, int B) {
+// Weight-stationary actor: each wave keeps its share of the actor's MFMA A-fragments in
+// registers for the whole rollout (layer 2: out tiles wave, wave+4, wave+8, wave+12 x 16 k-tiles =
+// 64 float4; layers 1/3 and biases 12 more), so a step issues only LDS reads and MFMAs.
+constexpr int A2_REG_TILES = 3;  // layer-2 out tiles per wave held in registers; the 4th in LDS
+struct ActorRegs {
+  float4 a2[A2_REG_TILES][16];  // layer 2: out tiles ot = wave + 4i (i < 3), all 16 k-tiles
+};
+// Layers 1 and 3, the 4th layer-2 out tile of every wave, and all biases live in LDS.
+struct ActorLds {
+  float4 a1[16 * 64];  // layer-1 blocks (KT = 1)
+  float4 a3[16 * 64];  // layer-3 blocks (one out tile, 16 k-tiles)
+  float4 a2[4 * 16 * 64];  // layer-2 blocks of out tiles 12..15 (wave + 12), [wave][k][lane]
+  float b1[256], b2[256], b3[16];
+};
+
+__device__ __forceinline__ void load_actor_regs(const NetView& N, int na, const Lane& L, ActorRegs& R, ActorLds& S) {
+  const float4* A1 = N.fwd(0);
+  const float4* A2 = N.fwd(1);
+  const float4* A3 = N.fwd(2);
+#pragma unroll
+  for (int i = 0; i < A2_REG_TILES; ++i) {
+    const int ot = L.wave + 4 * i;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) R.a2[i][k] = A2[(ot * 16 + k) * 64 + L.lane];
+  }
+  for (int k = 0; k < 16; ++k) S.a2[(L.wave * 16 + k) * 64 + L.lane] = A2[((L.wave + 12) * 16 + k) * 64 + L.lane];
+  for (int k = L.tid; k < 16 * 64; k += CACTO_THREADS) {
+    S.a1[k] = A1[k];
+    S.a3[k] = A3[k];
+  }
+  for (int f = L.tid; f < 256; f += CACTO_THREADS) {
+    S.b1[f] = N.bias(0, f);
+    S.b2[f] = N.bias(1, f);
+  }
+  if (L.tid < 16) S.b3[L.tid] = L.tid < na ? N.bias(2, L.tid) : 0.f;
+}
+
+__device__ __forceinline__ float4 lrelu_bias(const floatx4& acc, const float* bias, int f) {
+  float z[4] = {fadd(acc[0], bias[f]), fadd(acc[1], bias[f + 1]), fadd(acc[2], bias[f + 2]), fadd(acc[3], bias[f + 3])};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) z[r] = z[r] > 0.f ? z[r] : fmul(z[r], 0.3f);
+  return make_float4(z[0], z[1], z[2], z[3]);
+}
+
+// Actor forward of one tile with register-resident layer-2 weights. X0 -> H1 -> H2 -> A.
+__device__ __forceinline__ void actor_forward_regs(const ActorRegs& R, const ActorLds& W, int na, const float4* X0,
+                                                   float4* H1, float4* H2, float4* red, float* A, const Lane& L) {
+  const float4 x = X0[L.lane];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ot = L.wave + 4 * i;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = mfma_block(W.a1[ot * 64 + L.lane], x, acc);
+    H1[ot * 64 + L.lane] = lrelu_bias(acc, W.b1, 16 * ot + 4 * L.g);
+  }
+  __syncthreads();
+  floatx4 acc2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc2[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float4 b = H1[k * 64 + L.lane];
+#pragma unroll
+    for (int i = 0; i < A2_REG_TILES; ++i) acc2[i] = mfma_block(R.a2[i][k], b, acc2[i]);
+    acc2[3] = mfma_block(W.a2[(L.wave * 16 + k) * 64 + L.lane], b, acc2[3]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ot = L.wave + 4 * i;
+    H2[ot * 64 + L.lane] = lrelu_bias(acc2[i], W.b2, 16 * ot + 4 * L.g);
+  }
+  __syncthreads();
+  floatx4 acc3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kt = L.wave + 4 * i;
+    acc3 = mfma_block(W.a3[kt * 64 + L.lane], H2[kt * 64 + L.lane], acc3);
+  }
+  red[L.wave * 64 + L.lane] = make_float4(acc3[0], acc3[1], acc3[2], acc3[3]);
+  __syncthreads();
+  if (L.wave == 0) {
+    float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < CACTO_NWAVES; ++w) {
+      const float4 p = red[w * 64 + L.lane];
+      sum[0] += p.x;
+      sum[1] += p.y;
+      sum[2] += p.z;
+      sum[3] += p.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 4 * L.g + r;
+      if (f < na) A[L.c * na + f] = fadd(sum[r], W.b3[f]);
+    }
+  }
+}
+
+// One workgroup = 16 episodes (lane c of a wave <-> episode c of the tile). Per step:
+//   actor tile (4 waves, MFMA, weights stationary)                         -> A (LDS)
+//   E1: wave 0 integrates the dynamics s -> s'; waves 1-3 evaluate the reward terms of (s, a)
+//       (ellipses / peak / control cost) from EE(s) kept in LDS
+//   E2: wave 0 combines the reward in the reference's order and writes S/A/R; wave 1 computes
+//       EE(s'); wave 2 normalises s' into the next actor input tile.
+template <int NJ>
+__global__ void __launch_bounds__(CACTO_THREADS, 1)
+    k_rollout(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
+              const int32_t* __restrict__ nsteps, int T, int use_actor, const double* __restrict__ Wext,
+              double* __restrict__ Straj, float* __restrict__ Atraj, double* __restrict__ Rtraj,
+              double* __restrict__ EEtraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
   __shared__ float4 X0[64];
-  __shared__ float4 H[2 * 16 * 64];
+  __shared__ float4 H1[16 * 64], H2[16 * 64];
   __shared__ float4 red[4 * 64];
   __shared__ float st[16 * 16];
-  __shared__ float A[16 * CACTO_MAX_ACTION];
+  __shared__ float A[16 * na];
+  __shared__ double sS[16 * ns], sEE[16 * 3], terms[16 * 6];
+  __shared__ int sb[16], sn_[16], salive[16];
   __shared__ int tmax;
+  __shared__ ActorLds WL;
   const SysDevice& sd = *sdp;
   const cacto_sys_params& p = sd.p;
   const Lane L;
-  const int ns = p.nb_state, na = p.nb_action, s0 = blockIdx.x * CACTO_TILE;
-  const bool owner = L.tid < 16 && s0 + L.tid < B;
-  const int b = owner ? (order ? order[s0 + L.tid] : s0 + L.tid) : 0;
-  double s[CACTO_MAX_STATE], w[8];
-  int my_n = 0;
-  bool alive = false;
+  const int s0 = blockIdx.x * CACTO_TILE;
+  const int c = L.c;                      // episode slot handled by this lane (lanes 0..15)
+  const bool ep_lane = L.lane < 16 && s0 + c < B;
+  double w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = k >= p.n_weights ? 0.0 : Wext ? Wext[k] : p.w_running[k];
+  const bool want_R = Rtraj != nullptr, want_EE = EEtraj != nullptr || want_R;
+  ActorRegs R;
+  if (use_actor) load_actor_regs(N, na, L, R, WL);
   if (L.tid == 0) tmax = 0;
   __syncthreads();
-  if (owner) {
-    for (int i = 0; i < ns; ++i) s[i] = S0[(size_t)b * ns + i];
-    for (int k = 0; k < p.n_weights; ++k) w[k] = Wext ? Wext[k] : p.w_running[k];
-    my_n = min(nsteps[b], T);
-    alive = my_n > 0;
-    atomicMax(&tmax, my_n);
-    if (Straj)
-      for (int i = 0; i < ns; ++i) Straj[(size_t)b * (T + 1) * ns + i] = s[i];
-    if (EEtraj) {
-      const V3 e = env_ee(sd, s);
-      EEtraj[(size_t)b * (T + 1) * 3 + 0] = e.x;
-      EEtraj[(size_t)b * (T + 1) * 3 + 1] = e.y;
-      EEtraj[(size_t)b * (T + 1) * 3 + 2] = e.z;
+  ConstDyn<NJ> cd;
+  if (L.wave == 0 && L.lane < 16) {
+    const bool valid = s0 + c < B;
+    const int b = valid ? (order ? order[s0 + c] : s0 + c) : 0;
+    const int n = valid ? min(nsteps[b], T) : 0;
+    sb[c] = b;
+    sn_[c] = n;
+    salive[c] = n > 0;
+    atomicMax(&tmax, n);
+    double s[ns];
+#pragma unroll
+    for (int i = 0; i < ns; ++i) {
+      s[i] = valid ? S0[(size_t)b * ns + i] : 0.0;
+      sS[c * ns + i] = s[i];
+      st[c * 16 + i] = (float)s[i];
+      if (valid && Straj) Straj[(size_t)b * (T + 1) * ns + i] = s[i];
+    }
+    for (int i = ns; i < 16; ++i) st[c * 16 + i] = 0.f;
+    if (NJ > 0 && p.const_dyn && valid) const_dyn_init<NJ>(sd, s, cd);
+    if (want_EE) {
+      const V3 e = env_ee<NJ>(sd, s);
+      sEE[c * 3 + 0] = e.x;
+      sEE[c * 3 + 1] = e.y;
+      sEE[c * 3 + 2] = e.z;
+      if (valid && EEtraj) {
+        EEtraj[(size_t)b * (T + 1) * 3 + 0] = e.x;
+        EEtraj[(size_t)b * (T + 1) * 3 + 1] = e.y;
+        EEtraj[(size_t)b * (T + 1) * 3 + 2] = e.z;
+      }
     }
   }
+  __syncthreads();
+  if (use_actor && L.wave == 0) fill_input_tile(p, st, X0, L);
   __syncthreads();
   const int steps = tmax;
   for (int t = 0; t < steps; ++t) {
     if (use_actor) {
-      if (L.tid < 16)
-        for (int f = 0; f < 16; ++f) st[L.tid * 16 + f] = (owner && f < ns) ? (float)s[f] : 0.f;
-      __syncthreads();
-      if (L.wave == 0) fill_input_tile(p, st, X0, L);
-      __syncthreads();
-      actor_forward_tile(N, na, X0, nullptr, H, red, A, L, [](int, int, float4, float4) {});
+      actor_forward_regs(R, WL, na, X0, H1, H2, red, A, L);
       __syncthreads();
     }
-    if (owner && alive && t < my_n) {
-      double a[CACTO_MAX_ACTION], sn[CACTO_MAX_STATE];
-      for (int i = 0; i < na; ++i) {
-        const float af = use_actor ? A[L.tid * na + i] : 0.f;
-        a[i] = (double)af;
-        if (Atraj) Atraj[((size_t)b * T + t) * na + i] = af;
+    const bool active = ep_lane && salive[c] && t < sn_[c];
+    double sn[ns];
+    // ---- E1
+    if (active) {
+      double a[na];
+#pragma unroll
+      for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)A[c * na + i] : 0.0;
+      if (L.wave == 0) {
+        double s[ns];
+#pragma unroll
+        for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
+        if (NJ > 0 && p.const_dyn)
+          env_simulate_const<NJ>(sd, cd, s, a, sn);
+        else
+          env_simulate<NJ>(sd, s, a, false, sn);
+      } else if (want_R) {
+        const double x = sEE[c * 3 + 0], y = sEE[c * 3 + 1];
+        const double* o = p.obs;
+        if (L.wave == 1) {
+          terms[c * 6 + 0] = ell_cost(p, x, y, o[0], o[1], o[6], o[7]);
+          terms[c * 6 + 1] = ell_cost(p, x, y, o[2], o[3], o[8], o[9]);
+        } else if (L.wave == 2) {
+          terms[c * 6 + 2] = ell_cost(p, x, y, o[4], o[5], o[10], o[11]);
+          terms[c * 6 + 3] = peak_cost(p, x, y);
+        } else {
+          terms[c * 6 + 4] = bound_control_cost<na>(p, a);
+          double vel = 0.0;
+          if (NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR && w[2] != 0.0) {
+#pragma unroll
+            for (int k = 0; k < (NJ > 0 ? NJ : 1); ++k) vel += sS[c * ns + NJ + k] * sS[c * ns + NJ + k];
+          }
+          terms[c * 6 + 5] = vel;
+        }
       }
-      env_simulate(sd, s, a, false, sn);
-      if (Rtraj) Rtraj[(size_t)b * T + t] = env_reward(sd, w, s, a, false);
-      bool bad = false;
+    }
+    __syncthreads();
+    // ---- E2
+    if (active) {
+      const int b = sb[c];
+      if (L.wave == 0) {
+        if (want_R) {
+          const bool has_vel = NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR;
+          Rtraj[(size_t)b * T + t] =
+              combine_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], terms[c * 6 + 3], terms[c * 6 + 5], has_vel,
+                             terms[c * 6 + 0], terms[c * 6 + 1], terms[c * 6 + 2], terms[c * 6 + 4]);
+        }
+        if (Atraj)
+#pragma unroll
+          for (int i = 0; i < na; ++i) Atraj[((size_t)b * T + t) * na + i] = use_actor ? A[c * na + i] : 0.f;
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < ns; ++i) {
+          bad |= isnan(sn[i]);
+          if (Straj) Straj[((size_t)b * (T + 1) + t + 1) * ns + i] = sn[i];
+        }
+        if (bad) salive[c] = 0;  // RL.py:229-231
+      }
+    }
+    __syncthreads();
+    if (active && L.wave == 0) {
+#pragma unroll
       for (int i = 0; i < ns; ++i) {
-        s[i] = sn[i];
-        bad |= isnan(sn[i]);
+        sS[c * ns + i] = sn[i];
+        st[c * 16 + i] = (float)sn[i];
       }
-      if (Straj)
-        for (int i = 0; i < ns; ++i) Straj[((size_t)b * (T + 1) + t + 1) * ns + i] = s[i];
+    }
+    __syncthreads();
+    if (active && L.wave == 1 && want_EE) {
+      double s[ns];
+#pragma unroll
+      for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
+      const V3 e = env_ee<NJ>(sd, s);
+      sEE[c * 3 + 0] = e.x;
+      sEE[c * 3 + 1] = e.y;
+      sEE[c * 3 + 2] = e.z;
       if (EEtraj) {
-        const V3 e = env_ee(sd, s);
+        const int b = sb[c];
         EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 0] = e.x;
         EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 1] = e.y;
         EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 2] = e.z;
       }
-      if (bad) alive = false;  // RL.py:229-231
     }
+    if (use_actor && L.wave == 2) fill_input_tile(p, st, X0, L);
     __syncthreads();
   }
-  if (owner && status) status[b] = alive || my_n == 0 ? 0 : 1;
+  if (L.wave == 0 && ep_lane && status) {
+    const int b = sb[c];
+    status[b] = (salive[c] || sn_[c] == 0) ? 0 : 1;
+  }
 }
 
 }  // namespace cacto
 
 using namespace cacto;
+
+namespace {
+template <int NJ>
+struct LaunchRollout {
+  static int run(const cacto_sys* sys, NetView v, const double* S0, const int32_t* n, int T, int use_actor,
+                 const double* W, double* S, float* A, double* R, double* EE, int32_t* status, const int32_t* order,
+                 int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_rollout<NJ>, dim3(ceil_div(B, CACTO_TILE)), dim3(CACTO_THREADS), 0, st, sys->dev, v, S0, n, T,
+                       use_actor, W, S, A, R, EE, status, order, B);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
+};
+}  // namespace
 
 NetView cacto_make_view(const cacto_sys* sys, int net, const float* netbuf) {
   NetView v;
@@ -247,8 +444,6 @@ extern "C" int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, 
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
   if (B == 0) return CACTO_OK;
   NetView v = cacto_make_view(sys, CACTO_NET_ACTOR, actor_netbuf_d);
-  hipLaunchKernelGGL(k_rollout, dim3(ceil_div(B, CACTO_TILE)), dim3(CACTO_THREADS), 0, as_stream(stream), sys->dev, v,
-                     S0_d, nsteps_d, T, use_actor, W_d, S_traj_d, A_traj_d, R_traj_d, EE_traj_d, status_d, order_d, B);
-  CACTO_CHECK_HIP(hipGetLastError());
-  return CACTO_OK;
+  return dispatch_nj<LaunchRollout>(sys->host.p, sys, v, S0_d, nsteps_d, T, use_actor, W_d, S_traj_d, A_traj_d,
+                                    R_traj_d, EE_traj_d, status_d, order_d, B, as_stream(stream));
 }

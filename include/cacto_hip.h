@@ -82,7 +82,8 @@ typedef struct {
   int32_t ee_parent; /* chain only: joint index of the 'EE' frame's parent */
   int32_t n_check;   /* car_park only */
   int32_t n_weights; /* length of cost_weights_* (7, car_park 8) */
-  int32_t pad0;
+  int32_t const_dyn; /* filled by cacto_sys_create: 1 if every joint is prismatic, so M and nle
+                      * do not depend on the state (DI) — input value ignored */
   double dt;
   double state_norm[CACTO_MAX_STATE];
   double u_max[CACTO_MAX_ACTION];
