@@ -42,6 +42,24 @@ def _compile(src):
     return obj
 
 
+def build_variant(name, defines):
+    """A diagnostic build (e.g. in-kernel timestamps) into cacto_amd/<name>.so."""
+    out = os.path.join(HERE, name + ".so")
+    objs = []
+    os.makedirs(OBJ, exist_ok=True)
+    for src in SOURCES:
+        obj = os.path.join(OBJ, name + "_" + src.replace(".hip", ".o"))
+        cmd = [hipcc()] + FLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr[-4000:])
+        objs.append(obj)
+    r = subprocess.run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-o", out] + objs, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr[-4000:])
+    return out
+
+
 def build(force=False, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():

@@ -38,6 +38,30 @@ int hip_fail(hipError_t e, const char* what);
 __device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
 __device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
 __device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+
+// sin and cos of x: Cody-Waite reduction by pi/2 (3-part constant, FMA) and minimax polynomials
+// on [-pi/4, pi/4] (max error ~1 ulp for |x| <= 8192, far beyond SIREN pre-activations);
+// larger |x| falls back to the library's Payne-Hanek path.
+__device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
+  const float j = rintf(x * 0.636619772367581343f);
+  float r = fmaf(-j, 1.5703125f, x);
+  r = fmaf(-j, 4.837512969970703125e-4f, r);
+  r = fmaf(-j, 7.54978995489188216e-8f, r);
+  const float r2 = r * r;
+  float ps = fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+  ps = fmaf(r2, ps, -1.6666654611e-1f);
+  const float sr = fmaf(r * r2, ps, r);
+  float pc = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = fmaf(r2, pc, 4.166664568298827e-2f);
+  const float cr = fmaf(r2 * r2, pc, fmaf(-0.5f, r2, 1.0f));
+  const int q = (int)j & 3;
+  const float a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;
+  float so = (q & 2) ? -a : a;
+  float co = ((q + 1) & 2) ? -b : b;
+  if (__builtin_expect(fabsf(x) > 8192.f, 0)) sincosf(x, &so, &co);
+  *s = so;
+  *c = co;
+}
 __device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
 __device__ __forceinline__ double dmul(double a, double b) { return __dmul_rn(a, b); }
 __device__ __forceinline__ double dadd(double a, double b) { return __dadd_rn(a, b); }

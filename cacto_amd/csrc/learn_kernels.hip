@@ -55,8 +55,8 @@ __global__ void __launch_bounds__(CACTO_THREADS)
                   int B, GradBufs gb, float* __restrict__ y_out, float* __restrict__ V_out, float* __restrict__ Vt_out,
                   int32_t* __restrict__ step) {
   __shared__ float4 X0[64], XT[64], G0[64];
-  __shared__ float4 Z[24 * 64];
-  __shared__ float4 H[16 * 64];
+  __shared__ float4 Cs[24 * 64];  // cos z_l
+  __shared__ float4 Hs[24 * 64];  // h_l = sin z_l
   __shared__ float4 G[16 * 64];
   __shared__ float4 ZB[24 * 64];
   __shared__ float4 GB[16 * 64];
@@ -94,24 +94,24 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   __syncthreads();
 
   // y = R + (1 - d) * V_tgt(s_next)   (NeuralNetwork.py:153-158)
-  if (!cs.MC) critic_forward_tile(Tg, XT, nullptr, H, red, Vn, L, [](int, int, float4, float4) {});
+  if (!cs.MC) critic_forward_tile(Tg, XT, nullptr, nullptr, Hs, red, Vn, L, [](int, int, float4) {});
   __syncthreads();
   if (L.tid < 16) y[L.tid] = cs.MC ? Rs[L.tid] : fadd(Rs[L.tid], fmul(fsub(1.f, ds[L.tid]), Vn[L.tid]));
   if (cs.want_vt) {  // the extra V_tgt(s) of NeuralNetwork.py:178
-    critic_forward_tile(Tg, X0, nullptr, H, red, Vt2, L, [](int, int, float4, float4) {});
+    critic_forward_tile(Tg, X0, nullptr, nullptr, Hs, red, Vt2, L, [](int, int, float4) {});
     __syncthreads();
   }
 
-  // forward at s, keeping z; h_l -> LT_l second half
+  // forward at s, keeping sin z and cos z; h_l -> LT_l second half
   if (L.wave == 0) store_panel(gb.LT[0], ld, Bp + s0 + L.c, 0, L.g, X0[L.lane]);
-  critic_forward_tile(C, X0, Z, H, red, V, L, [&](int l, int ot, float4, float4 h4) {
+  critic_forward_tile(C, X0, Cs, Hs, Hs, red, V, L, [&](int l, int ot, float4 h4) {
     store_panel(gb.LT[l + 1], ld, Bp + s0 + L.c, ot, L.g, h4);
   });
   __syncthreads();
 
   if (sob) {
     // first backward: D_l -> RT_l first half; G_l kept in LDS; G_0 = dV/dx0
-    critic_first_backward(C, Z, H, G, G0, red, L, [&](int l, int ot, int lane, float4 d4) {
+    critic_first_backward(C, Cs, GB, G, G0, red, L, [&](int l, int ot, int lane, float4 d4) {
       store_panel(gb.RT[l], ld, s0 + (lane & 15), ot, lane >> 4, d4);
     });
     __syncthreads();
@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     for (int l = 0; l < 4; ++l) {
       float4* nxt = GB + ((l + 1) & 1) * 8 * 64;
       layer(C.fwd(l), C.t.OT[l], C.t.KT[l], cur, red, L, [&](int ot, floatx4 acc) {
-        const float4 z = Z[(zoff[l] + ot) * 64 + L.lane];
+        const float4 sz = Hs[(zoff[l] + ot) * 64 + L.lane], cz = Cs[(zoff[l] + ot) * 64 + L.lane];
         float4 gu;
         if (l < 3) {
           gu = G[(goff[l + 1] + ot) * 64 + L.lane];
@@ -149,11 +149,12 @@ __global__ void __launch_bounds__(CACTO_THREADS)
           const int f = 16 * ot + 4 * L.g;
           gu = make_float4(C.w(4, f, 0), C.w(4, f + 1, 0), C.w(4, f + 2, 0), C.w(4, f + 3, 0));
         }
-        const float zz[4] = {z.x, z.y, z.z, z.w}, gg[4] = {gu.x, gu.y, gu.z, gu.w};
+        const float sv[4] = {sz.x, sz.y, sz.z, sz.w}, cv[4] = {cz.x, cz.y, cz.z, cz.w};
+        const float gg[4] = {gu.x, gu.y, gu.z, gu.w};
         float zb[4], gn[4];
         for (int r = 0; r < 4; ++r) {
-          zb[r] = fmul(-fmul(acc[r], gg[r]), sinf(zz[r]));  // CosGrad: -grad * sin(x)
-          gn[r] = fmul(acc[r], cosf(zz[r]));                 // MulGrad into the upstream grad
+          zb[r] = fmul(-fmul(acc[r], gg[r]), sv[r]);  // CosGrad: -grad * sin(x)
+          gn[r] = fmul(acc[r], cv[r]);                 // MulGrad into the upstream grad
         }
         ZB[(zoff[l] + ot) * 64 + L.lane] = make_float4(zb[0], zb[1], zb[2], zb[3]);
         const float4 g4 = make_float4(gn[0], gn[1], gn[2], gn[3]);
@@ -184,13 +185,13 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   __syncthreads();
   for (int k = L.tid; k < 8 * 64; k += CACTO_THREADS) {  // zbar_3 += (Vbar * W5) * cos(z3)
     const int ot = k >> 6, lane = k & 63, g = lane >> 4, c = lane & 15;
-    const float4 z = Z[(zoff[3] + ot) * 64 + lane];
+    const float4 z = Cs[(zoff[3] + ot) * 64 + lane];
     float4 zb = ZB[(zoff[3] + ot) * 64 + lane];
     const int f = 16 * ot + 4 * g;
-    zb.x = fadd(zb.x, fmul(fmul(Vb[c], C.w(4, f, 0)), cosf(z.x)));
-    zb.y = fadd(zb.y, fmul(fmul(Vb[c], C.w(4, f + 1, 0)), cosf(z.y)));
-    zb.z = fadd(zb.z, fmul(fmul(Vb[c], C.w(4, f + 2, 0)), cosf(z.z)));
-    zb.w = fadd(zb.w, fmul(fmul(Vb[c], C.w(4, f + 3, 0)), cosf(z.w)));
+    zb.x = fadd(zb.x, fmul(fmul(Vb[c], C.w(4, f, 0)), z.x));
+    zb.y = fadd(zb.y, fmul(fmul(Vb[c], C.w(4, f + 1, 0)), z.y));
+    zb.z = fadd(zb.z, fmul(fmul(Vb[c], C.w(4, f + 2, 0)), z.z));
+    zb.w = fadd(zb.w, fmul(fmul(Vb[c], C.w(4, f + 3, 0)), z.w));
     ZB[(zoff[3] + ot) * 64 + lane] = zb;
   }
   __syncthreads();
@@ -202,12 +203,12 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     }
     if (l == 0) break;
     layer(C.bwd(l), C.t.KT[l], C.t.OT[l], ZB + zoff[l] * 64, red, L, [&](int it, floatx4 acc) {
-      const float4 z = Z[(zoff[l - 1] + it) * 64 + L.lane];
+      const float4 z = Cs[(zoff[l - 1] + it) * 64 + L.lane];
       float4 zb = ZB[(zoff[l - 1] + it) * 64 + L.lane];
-      zb.x = fadd(zb.x, fmul(acc[0], cosf(z.x)));
-      zb.y = fadd(zb.y, fmul(acc[1], cosf(z.y)));
-      zb.z = fadd(zb.z, fmul(acc[2], cosf(z.z)));
-      zb.w = fadd(zb.w, fmul(acc[3], cosf(z.w)));
+      zb.x = fadd(zb.x, fmul(acc[0], z.x));
+      zb.y = fadd(zb.y, fmul(acc[1], z.y));
+      zb.z = fadd(zb.z, fmul(acc[2], z.z));
+      zb.w = fadd(zb.w, fmul(acc[3], z.w));
       ZB[(zoff[l - 1] + it) * 64 + L.lane] = zb;
     });
   }
@@ -222,7 +223,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   __shared__ float4 X0[64], XS[64], G0[64], ZB3[64];
   __shared__ float4 ZA[32 * 64];  // actor z1, z2
   __shared__ float4 H[32 * 64];   // actor h ping-pong; later critic H (16) + actor zbar2 (16)
-  __shared__ float4 ZC[24 * 64];  // critic z at s'
+  __shared__ float4 ZC[24 * 64];  // critic cos z at s'
   __shared__ float4 red[4 * 64];
   __shared__ float st[256], stn[256];
   __shared__ float A[16 * CACTO_MAX_ACTION];
@@ -286,7 +287,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   // critic (already updated) at s': V and dV/dx0 (NeuralNetwork.py:190-195)
   float4* HC = H;            // 16 tiles
   float4* ZB2 = H + 16 * 64;  // 16 tiles
-  critic_forward_tile(C, XS, ZC, HC, red, Vn, L, [](int, int, float4, float4) {});
+  critic_forward_tile(C, XS, ZC, nullptr, HC, red, Vn, L, [](int, int, float4) {});
   __syncthreads();
   critic_first_backward(C, ZC, HC, nullptr, G0, red, L, [](int, int, int, float4) {});
   __syncthreads();

@@ -91,16 +91,17 @@ __device__ __forceinline__ void mm_layer_t(const float4* __restrict__ A, int OT,
 #pragma unroll
       for (int k = 0; k < KT; ++k) an[k] = A[((size_t)nxt * KT + k) * 64 + lane];
     }
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    // the 4 k-steps of a fragment block go to 4 independent accumulators (issue-bound chain)
+    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
       const float4 b = X[k * 64 + lane];
-      if (k & 1)
-        acc1 = mfma_block(a[k], b, acc1);
-      else
-        acc0 = mfma_block(a[k], b, acc0);
+      c0 = mfma4(a[k].x, b.x, c0);
+      c1 = mfma4(a[k].y, b.y, c1);
+      c2 = mfma4(a[k].z, b.z, c2);
+      c3 = mfma4(a[k].w, b.w, c3);
     }
-    epi(ot, acc0 + acc1);
+    epi(ot, (c0 + c1) + (c2 + c3));
     if (nxt >= OT) break;
     ot = nxt;
 #pragma unroll

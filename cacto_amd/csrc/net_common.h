@@ -17,25 +17,32 @@ struct Lane {
   }
 };
 
+__device__ __forceinline__ float4 f4(const floatx4& a) { return make_float4(a[0], a[1], a[2], a[3]); }
+
 // Layers whose output is a single 16-row tile (OT == 1): split the K loop over the 4 waves,
 // reduce the partial accumulators through LDS `red` (4 x 64 float4) in fixed order, and let
 // wave 0 run the epilogue. Contains __syncthreads(): all threads must call it.
 template <typename Epi>
 __device__ __forceinline__ void mm_single_tile(const float4* __restrict__ A, int KT, const float4* X, float4* red,
                                                const Lane& L, Epi&& epi) {
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  float4 a[4];
+  float4 a[4], b[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int kt = L.wave + 4 * i;
-    a[i] = kt < KT ? A[kt * 64 + L.lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int kt = min(L.wave + 4 * i, KT - 1);
+    a[i] = A[kt * 64 + L.lane];
+    b[i] = X[kt * 64 + L.lane];
   }
+  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int kt = L.wave + 4 * i;
-    if (kt < KT) acc = mfma_block(a[i], X[kt * 64 + L.lane], acc);
+    if (L.wave + 4 * i < KT) {
+      c0 = mfma4(a[i].x, b[i].x, c0);
+      c1 = mfma4(a[i].y, b[i].y, c1);
+      c2 = mfma4(a[i].z, b[i].z, c2);
+      c3 = mfma4(a[i].w, b[i].w, c3);
+    }
   }
-  red[L.wave * 64 + L.lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  red[L.wave * 64 + L.lane] = f4((c0 + c1) + (c2 + c3));
   __syncthreads();
   if (L.wave == 0) {
     floatx4 s = {0.f, 0.f, 0.f, 0.f};
@@ -62,29 +69,26 @@ __device__ __forceinline__ void layer(const float4* __restrict__ A, int OT, int 
   __syncthreads();
 }
 
-__device__ __forceinline__ float4 f4(const floatx4& a) { return make_float4(a[0], a[1], a[2], a[3]); }
+constexpr int ZOFF[4] = {0, 4, 8, 16};  // critic hidden-layer tile offsets (64, 64, 128, 128 features)
 
-// Critic forward over the input tile X0. Hidden pre-activations go to Z (24 tiles at offsets
-// 0,4,8,16) when Z != nullptr; h tiles alternate in H (2 x 8 tiles). hook(l, ot, z4, h4) runs for
+// Critic forward over the input tile X0. With Hs != nullptr every h_l = sin(z_l) is kept (24 tiles,
+// offsets ZOFF); otherwise h tiles alternate in H (2 x 8 tiles). With Cs != nullptr cos(z_l) is
+// kept too (24 tiles), so no later pass re-evaluates a transcendental. hook(l, ot, h4) runs for
 // every hidden out tile (l = 0..3). V[c] (LDS, 16 floats) receives the output for sample c.
 template <typename Hook>
-__device__ void critic_forward_tile(const NetView& N, const float4* X0, float4* Z, float4* H, float4* red, float* V,
-                                    const Lane& L, Hook&& hook) {
-  const int zoff[4] = {0, 4, 8, 16};
+__device__ void critic_forward_tile(const NetView& N, const float4* X0, float4* Cs, float4* Hs, float4* H, float4* red,
+                                    float* V, const Lane& L, Hook&& hook) {
   const float4* in = X0;
   for (int l = 0; l < 4; ++l) {
-    float4* out = H + (l & 1) * 8 * 64;
+    float4* out = Hs ? Hs + ZOFF[l] * 64 : H + (l & 1) * 8 * 64;
     layer(N.fwd(l), N.t.OT[l], N.t.KT[l], in, red, L, [&](int ot, floatx4 acc) {
-      float z[4], h[4];
-      for (int r = 0; r < 4; ++r) {
-        z[r] = fadd(acc[r], N.bias(l, 16 * ot + 4 * L.g + r));
-        h[r] = sinf(z[r]);
-      }
-      const float4 z4 = make_float4(z[0], z[1], z[2], z[3]);
+      float h[4], c[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) fast_sincos(fadd(acc[r], N.bias(l, 16 * ot + 4 * L.g + r)), &h[r], &c[r]);
       const float4 h4 = make_float4(h[0], h[1], h[2], h[3]);
-      if (Z) Z[(zoff[l] + ot) * 64 + L.lane] = z4;
+      if (Cs) Cs[(ZOFF[l] + ot) * 64 + L.lane] = make_float4(c[0], c[1], c[2], c[3]);
       out[ot * 64 + L.lane] = h4;
-      hook(l, ot, z4, h4);
+      hook(l, ot, h4);
     });
     in = out;
   }
@@ -134,23 +138,21 @@ __device__ __forceinline__ void fill_input_tile(const cacto_sys_params& p, const
   X[L.lane] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// Critic input gradient given D[l] construction from stored Z tiles: runs the first backward
-// pass G[4] = W5, D[l] = G[l+1] cos z_l, G[l] = D[l] W_l^T. Results: G tiles (G1 at 0, G2 at 4,
-// G3 at 8; 16 tiles) when Gs != nullptr, D via hookD(l, ot, d4), and dV/dx0 in G0 (1 tile).
+// Critic input gradient (first backward pass) from the cos tiles Cs: G[4] = W5,
+// D[l] = G[l+1] cos z_l, G[l] = D[l] W_l^T. Results: G tiles (G1 at 0, G2 at 4, G3 at 8; 16 tiles)
+// when Gs != nullptr, D via hookD(l, ot, lane, d4), and dV/dx0 in G0 (1 tile).
 template <typename HookD>
-__device__ void critic_first_backward(const NetView& N, const float4* Z, float4* P /* 2 x 8 tiles */, float4* Gs,
+__device__ void critic_first_backward(const NetView& N, const float4* Cs, float4* P /* 2 x 8 tiles */, float4* Gs,
                                       float4* G0, float4* red, const Lane& L, HookD&& hookD) {
-  const int zoff[4] = {0, 4, 8, 16};
   const int goff[4] = {0, 0, 4, 8};  // G[l] tile offsets for l = 1..3
   // D3 = W5[:,0] * cos(z3)
   float4* D = P;
   for (int idx = L.tid; idx < N.t.OT[3] * 64; idx += CACTO_THREADS) {
     const int ot = idx >> 6, lane = idx & 63, g = lane >> 4;
-    const float4 z = Z[(zoff[3] + ot) * 64 + lane];
-    float d[4];
-    const float zz[4] = {z.x, z.y, z.z, z.w};
-    for (int r = 0; r < 4; ++r) d[r] = fmul(N.w(4, 16 * ot + 4 * g + r, 0), cosf(zz[r]));
-    const float4 d4 = make_float4(d[0], d[1], d[2], d[3]);
+    const float4 c = Cs[(ZOFF[3] + ot) * 64 + lane];
+    const int f = 16 * ot + 4 * g;
+    const float4 d4 = make_float4(fmul(N.w(4, f, 0), c.x), fmul(N.w(4, f + 1, 0), c.y), fmul(N.w(4, f + 2, 0), c.z),
+                                  fmul(N.w(4, f + 3, 0), c.w));
     D[idx] = d4;
     hookD(3, ot, lane, d4);
   }
@@ -161,9 +163,8 @@ __device__ void critic_first_backward(const NetView& N, const float4* Z, float4*
     layer(N.bwd(l), N.t.KT[l], N.t.OT[l], D, red, L, [&](int it, floatx4 acc) {
       const float4 gl = f4(acc);
       if (Gs) Gs[(goff[l] + it) * 64 + L.lane] = gl;
-      const float4 z = Z[(zoff[l - 1] + it) * 64 + L.lane];
-      const float4 d4 = make_float4(fmul(gl.x, cosf(z.x)), fmul(gl.y, cosf(z.y)), fmul(gl.z, cosf(z.z)),
-                                    fmul(gl.w, cosf(z.w)));
+      const float4 c = Cs[(ZOFF[l - 1] + it) * 64 + L.lane];
+      const float4 d4 = make_float4(fmul(gl.x, c.x), fmul(gl.y, c.y), fmul(gl.z, c.z), fmul(gl.w, c.w));
       Dn[it * 64 + L.lane] = d4;
       hookD(l - 1, it, L.lane, d4);
     });

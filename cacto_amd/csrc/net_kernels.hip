@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(CACTO_THREADS) k_critic_forward(const SysDevic
   __syncthreads();
   if (L.wave == 0) fill_input_tile(p, st, X0, L);
   __syncthreads();
-  critic_forward_tile(N, X0, dVdS ? Z : nullptr, H, red, V, L, [](int, int, float4, float4) {});
+  critic_forward_tile(N, X0, dVdS ? Z : nullptr, nullptr, H, red, V, L, [](int, int, float4) {});  // Z: cos tiles
   __syncthreads();
   if (L.tid < 16 && s0 + L.tid < B && Vout) Vout[s0 + L.tid] = V[L.tid];
   if (!dVdS) return;
