@@ -143,13 +143,31 @@ __device__ __forceinline__ float4 lrelu_bias(const floatx4& acc, const float* bi
 // Actor forward of one tile with register-resident layer-2 weights. X0 -> H1 -> H2 -> A.
 __device__ __forceinline__ void actor_forward_regs(const ActorRegs& R, const ActorLds& W, int na, const float4* X0,
                                                    float4* H1, float4* H2, float4* red, float* A, const Lane& L) {
+  // MFMA order: within a k-block, the 4 k-steps (j) outer and the 4 out tiles (i) inner, so
+  // consecutive MFMAs hit different accumulators (issue-bound); each accumulator still sums its
+  // k-steps in order.
   const float4 x = X0[L.lane];
+  {
+    float4 a1[4];
+    floatx4 acc1[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ot = L.wave + 4 * i;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    acc = mfma_block(W.a1[ot * 64 + L.lane], x, acc);
-    H1[ot * 64 + L.lane] = lrelu_bias(acc, W.b1, 16 * ot + 4 * L.g);
+    for (int i = 0; i < 4; ++i) {
+      a1[i] = W.a1[(L.wave + 4 * i) * 64 + L.lane];
+      acc1[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc1[i] = mfma4(a1[i].x, x.x, acc1[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc1[i] = mfma4(a1[i].y, x.y, acc1[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc1[i] = mfma4(a1[i].z, x.z, acc1[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc1[i] = mfma4(a1[i].w, x.w, acc1[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ot = L.wave + 4 * i;
+      H1[ot * 64 + L.lane] = lrelu_bias(acc1[i], W.b1, 16 * ot + 4 * L.g);
+    }
   }
   __syncthreads();
   floatx4 acc2[4];
@@ -158,9 +176,19 @@ __device__ __forceinline__ void actor_forward_regs(const ActorRegs& R, const Act
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const float4 b = H1[k * 64 + L.lane];
+    const float4 a3 = W.a2[(L.wave * 16 + k) * 64 + L.lane];
 #pragma unroll
-    for (int i = 0; i < A2_REG_TILES; ++i) acc2[i] = mfma_block(R.a2[i][k], b, acc2[i]);
-    acc2[3] = mfma_block(W.a2[(L.wave * 16 + k) * 64 + L.lane], b, acc2[3]);
+    for (int i = 0; i < A2_REG_TILES; ++i) acc2[i] = mfma4(R.a2[i][k].x, b.x, acc2[i]);
+    acc2[3] = mfma4(a3.x, b.x, acc2[3]);
+#pragma unroll
+    for (int i = 0; i < A2_REG_TILES; ++i) acc2[i] = mfma4(R.a2[i][k].y, b.y, acc2[i]);
+    acc2[3] = mfma4(a3.y, b.y, acc2[3]);
+#pragma unroll
+    for (int i = 0; i < A2_REG_TILES; ++i) acc2[i] = mfma4(R.a2[i][k].z, b.z, acc2[i]);
+    acc2[3] = mfma4(a3.z, b.z, acc2[3]);
+#pragma unroll
+    for (int i = 0; i < A2_REG_TILES; ++i) acc2[i] = mfma4(R.a2[i][k].w, b.w, acc2[i]);
+    acc2[3] = mfma4(a3.w, b.w, acc2[3]);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -168,12 +196,17 @@ __device__ __forceinline__ void actor_forward_regs(const ActorRegs& R, const Act
     H2[ot * 64 + L.lane] = lrelu_bias(acc2[i], W.b2, 16 * ot + 4 * L.g);
   }
   __syncthreads();
-  floatx4 acc3 = {0.f, 0.f, 0.f, 0.f};
+  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int kt = L.wave + 4 * i;
-    acc3 = mfma_block(W.a3[kt * 64 + L.lane], H2[kt * 64 + L.lane], acc3);
+    const float4 a = W.a3[kt * 64 + L.lane], b = H2[kt * 64 + L.lane];
+    c0 = mfma4(a.x, b.x, c0);
+    c1 = mfma4(a.y, b.y, c1);
+    c2 = mfma4(a.z, b.z, c2);
+    c3 = mfma4(a.w, b.w, c3);
   }
+  const floatx4 acc3 = (c0 + c1) + (c2 + c3);
   red[L.wave * 64 + L.lane] = make_float4(acc3[0], acc3[1], acc3[2], acc3[3]);
   __syncthreads();
   if (L.wave == 0) {
