@@ -53,7 +53,34 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--extra-systems", default="manipulator")
+    p.add_argument("--no-diagnostics", action="store_true",
+                   help="skip the rollout variants (profiling runs: every k_rollout dispatch is a full rollout)")
     return p.parse_args()
+
+
+def pmc_traffic(kernel="k_rollout<2>"):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summaries
+    (profiles/rNN_pmc_{fetch,write}.csv, made by tools/prof_summary.py from separate --pmc
+    FETCH_SIZE / WRITE_SIZE passes). gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE
+    counts half of the bytes of 16-B-per-lane reads -> x2; WRITE_SIZE is exact. Values are KiB."""
+    import csv
+    import glob
+    prof = os.path.join(ROOT, "profiles")
+    fetch = sorted(glob.glob(os.path.join(prof, "r*_pmc_fetch.csv")))
+    write = sorted(glob.glob(os.path.join(prof, "r*_pmc_write.csv")))
+    if not fetch or not write:
+        return None, None
+
+    def mean(path, counter):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["kernel"] == kernel and row["counter"] == counter:
+                    return float(row["mean"])
+        return None
+    fk, wk = mean(fetch[-1], "FETCH_SIZE"), mean(write[-1], "WRITE_SIZE")
+    if fk is None or wk is None:
+        return None, None
+    return (2.0 * fk + wk) * 1024.0, os.path.basename(fetch[-1]) + " + " + os.path.basename(write[-1])
 
 
 def init_dist():
@@ -277,7 +304,7 @@ def main():
     roll = rollout_phase(rl, conf, env, args.rollouts, args.steps, args.warmup, world, rank)
     value = roll["total_steps"] / roll["wall"]
     achieved = roll["steps_per_call"] * fa_flops(ns, na) / (roll["kernel_ms"] * 1e-3)
-    diag = rollout_diagnostics(rl, conf, roll)
+    diag = None if args.no_diagnostics else rollout_diagnostics(rl, conf, roll)
     buf = fill_buffer(rl, conf, roll, seed=rank)
     updates = {}
     for B in [int(b) for b in args.batches.split(",") if b]:
@@ -305,6 +332,7 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline_rollout(conf, rl, roll, args.cpu_seconds)
         cpu["update"] = cpu_baseline_update(conf, rl, buf, 128, args.cpu_seconds / 2)
+    traffic, traffic_src = pmc_traffic()
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -327,8 +355,9 @@ def main():
                        "parallelism": "dp%d" % world},
             "roofline": {"kernel": "k_rollout", "bound": "mfma", "achieved": achieved / 1e12,
                          "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK,
-                         "traffic": None, "kernel_ms": roll["kernel_ms"],
-                         "flop_per_env_step": fa_flops(ns, na)},
+                         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                         "kernel_ms": roll["kernel_ms"], "flop_per_env_step": fa_flops(ns, na),
+                         "env_steps_per_launch": roll["steps_per_call"]},
             "critic_updates": updates,
             "rollout_diagnostics": diag,
             "cpu_baseline": cpu,
