@@ -17,6 +17,22 @@ from .neural_network import ACTOR, CRITIC, Net
 from .system import DEVICE, dptr, stream
 
 
+def dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update):
+    """One data-parallel RL_AC.update (RL.py:101-111) + update_target (RL.py:113-118).
+
+    Every rank holds replicated weights and a local minibatch; the gradient callables return flat
+    gradients whose losses are already normalised by the GLOBAL batch, so the exchange is a plain
+    sum. Order (the reference's): critic gradient -> all-reduce -> critic Adam (+ soft target
+    update) -> actor gradient against the UPDATED critic -> all-reduce -> actor Adam.
+    """
+    gc = critic_grad()
+    all_reduce(gc)
+    apply("critic", gc, soft_update)
+    ga = actor_grad()
+    all_reduce(ga)
+    apply("actor", ga, False)
+
+
 class RL_AC:
     def __init__(self, env, NN, conf, N_try=0, w_S=None):
         self.env = env
@@ -165,12 +181,12 @@ class RL_AC:
 
     def _update_rows_dp(self, storage, idx, is_w=None, y=None, V=None, Vt=None):
         import torch.distributed as dist
-        gc = self.critic_grad_flat(storage, idx, is_w, y, V, Vt)
-        dist.all_reduce(gc, group=self.dp_group)                 # sum of (1/B_global)-scaled shards
-        self.apply_gradients(CRITIC, gc, soft_update=not self.conf.MC)
-        ga = self.actor_grad_flat(storage, idx)
-        dist.all_reduce(ga, group=self.dp_group)
-        self.apply_gradients(ACTOR, ga)
+        dp_update_step(lambda: self.critic_grad_flat(storage, idx, is_w, y, V, Vt),
+                       lambda: self.actor_grad_flat(storage, idx),
+                       lambda which, g, soft: self.apply_gradients(CRITIC if which == "critic" else ACTOR, g,
+                                                                   soft_update=soft),
+                       lambda t: dist.all_reduce(t, group=self.dp_group),
+                       soft_update=not self.conf.MC)
 
     def update(self, state_batch, state_next_rollout_batch, partial_reward_to_go_batch, dVdx_batch, d_batch,
                term_batch, weights_batch, batch_size=None):

@@ -1,0 +1,123 @@
+"""Data-parallel update logic on CPU (gloo, world size 2).
+
+cacto_amd.rl.dp_update_step is the exchange/ordering logic RL_AC uses with RCCL on the GPUs. Here it
+drives oracle gradients over two gloo ranks, each holding half of a global minibatch with losses
+normalised by the GLOBAL batch. The result must equal one single-process update on the whole
+batch (RL.py:101-118), and the two ranks must end with identical weights.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import env as oenv
+from oracle import nn as onn
+from tests.conftest import load_weights
+
+B_GLOBAL = 16
+
+
+def _rows(conf, rng):
+    ns = conf.nb_state
+    lo = np.asarray(conf.x_init_min, dtype=np.float64)
+    hi = np.asarray(conf.x_init_max, dtype=np.float64)
+    S = lo + (hi - lo) * rng.uniform(size=(B_GLOBAL, ns))
+    Sn = lo + (hi - lo) * rng.uniform(size=(B_GLOBAL, ns))
+    R = rng.normal(size=(B_GLOBAL, 1)) * 0.5
+    dVdx = rng.normal(size=(B_GLOBAL, ns)) * 0.3
+    d = (rng.uniform(size=(B_GLOBAL, 1)) < 0.3).astype(float)
+    term = (rng.uniform(size=(B_GLOBAL, 1)) < 0.2).astype(float)
+    return np.concatenate([S, R, Sn, dVdx, d, term], axis=1)
+
+
+def _flat(ps):
+    return torch.from_numpy(np.concatenate([np.asarray(p, dtype=np.float64).ravel() for p in ps]))
+
+
+def _unflat(t, like):
+    out, off = [], 0
+    for p in like:
+        n = int(np.prod(np.shape(p)))
+        out.append(t[off:off + n].numpy().reshape(np.shape(p)))
+        off += n
+    return out
+
+
+def _run_update(rows, world, all_reduce, n_steps=2):
+    """n_steps data-parallel updates on `rows` (this rank's shard), returning final weights."""
+    from cacto_amd.confs import load_conf
+    from cacto_amd.rl import dp_update_step
+    conf = load_conf("double_integrator")
+    oe = oenv.make_env(conf)
+    w = load_weights("di_seed0_0")
+    st = {"actor": [np.asarray(p, np.float64) for p in w["actor"]],
+          "critic": [np.asarray(p, np.float64) for p in w["critic"]],
+          "target": [np.asarray(p, np.float64) for p in w["target"]]}
+    adam = {"critic": onn.KerasAdam(conf.CRITIC_LEARNING_RATE), "actor": onn.KerasAdam(conf.ACTOR_LEARNING_RATE)}
+    norm = conf.state_norm_arr.astype(np.float64)
+    ns = conf.nb_state
+    S, R, Sn = rows[:, :ns], rows[:, ns:ns + 1], rows[:, ns + 1:2 * ns + 1]
+    dVdx, d, term = rows[:, 2 * ns + 1:3 * ns + 1], rows[:, 3 * ns + 1:3 * ns + 2], rows[:, 3 * ns + 2:]
+    scale = rows.shape[0] / float(B_GLOBAL)  # local-mean gradient -> share of the global mean
+
+    def critic_grad():
+        g = onn.compute_critic_grad(st["critic"], st["target"], S, Sn, R, dVdx, d, np.ones((S.shape[0], 1)), 1e-2,
+                                    norm)[0]
+        return _flat(g) * scale
+
+    def actor_grad():
+        g = onn.compute_actor_grad(oe, st["actor"], st["critic"], S.astype(np.float32), term, norm)
+        return _flat(g) * scale
+
+    def apply(which, g, soft):
+        st[which] = adam[which].apply(st[which], _unflat(g, st[which]))
+        if soft:
+            st["target"] = onn.soft_update(st["target"], st["critic"], conf.UPDATE_RATE)
+
+    for _ in range(n_steps):
+        dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update=True)
+    return {k: _flat(v).numpy() for k, v in st.items()}
+
+
+def _worker(rank, world, port, rows, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = rows.shape[0] // world
+        out = _run_update(rows[rank * n:(rank + 1) * n], world, lambda t: dist.all_reduce(t))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_dp_update_equals_single_process():
+    from cacto_amd.confs import load_conf
+    rows = _rows(load_conf("double_integrator"), np.random.default_rng(7))
+    ref = _run_update(rows, 1, lambda t: None)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, rows, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in ("actor", "critic", "target"):
+        assert np.array_equal(res[0][k], res[1][k]), k          # replicas stay identical
+        np.testing.assert_allclose(res[0][k], ref[k], rtol=1e-9, atol=1e-12, err_msg=k)
+    # and the update did move the weights
+    w0 = load_weights("di_seed0_0")
+    assert not np.allclose(ref["critic"], _flat(w0["critic"]).numpy())
