@@ -2,7 +2,7 @@
 
 Run with the interpreter that has h5py (this container: /opt/conda/bin/python3.9):
 
-    /opt/conda/bin/python3.9 tests/golden/make_h5_fixtures.py
+    /opt/conda/bin/python3.9 -B tests/golden/make_h5_fixtures.py
 
 Only the tensors are read (h5py datasets; nothing is executed from the files). The layer order
 is the Keras `trainable_variables` order the reference's optimizers iterate over
@@ -12,6 +12,8 @@ Sources: `Results Double Integrator/Results set test/NNs/N_try_{0,6}` (seed 0, w
 """
 import os
 import sys
+
+sys.dont_write_bytecode = True  # never write __pycache__ into the read-only reference tree
 
 import h5py
 import numpy as np

@@ -3,7 +3,7 @@
 Run in THIS container (the reference is not on the GPU box) with the numpy-1.x interpreter, so the
 reference's numpy-1.24 scalar-promotion semantics hold:
 
-    /opt/conda/bin/python3.9 tests/golden/make_ref_vectors.py
+    /opt/conda/bin/python3.9 -B tests/golden/make_ref_vectors.py
 
 TensorFlow, Pinocchio and CasADi are absent, so small stub modules (written below, into a temp dir)
 stand in for the few names the imported modules touch at import time:
@@ -18,6 +18,8 @@ import json
 import os
 import random
 import sys
+
+sys.dont_write_bytecode = True  # never write __pycache__ into the read-only reference tree
 import tempfile
 import types
 
