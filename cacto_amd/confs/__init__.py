@@ -5,7 +5,10 @@ SYSTEM_MAP = {
     # system_id: (conf module, Environment class name) — main.py:100-107
     'single_integrator': ('conf_single_integrator', 'SingleIntegrator'),
     'double_integrator': ('conf_double_integrator', 'DoubleIntegrator'),
+    'car': ('conf_car', 'Car'),
+    'car_park': ('conf_car_park', 'CarPark'),
     'manipulator': ('conf_manipulator', 'Manipulator'),
+    'ur5': ('conf_ur5', 'UR5'),
 }
 
 

@@ -31,10 +31,21 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
     CACTO_REQUIRE(p.nb_state >= 2 && p.nb_state <= CACTO_MAX_STATE, "cacto_sys_create: nb_state out of range");
     CACTO_REQUIRE(p.nb_action >= 1 && p.nb_action <= CACTO_MAX_ACTION, "cacto_sys_create: nb_action out of range");
     CACTO_REQUIRE(p.nb_state <= 16 && p.nb_action <= 16, "cacto_sys_create: MLP tiles assume ns, na <= 16");
-    CACTO_REQUIRE(p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR || p.dyn_kind == CACTO_DYN_CHAIN,
-                  "cacto_sys_create: dynamics kind not implemented in this build (car / car_park)");
-    CACTO_REQUIRE(p.reward_kind == CACTO_REW_PLANAR || p.reward_kind == CACTO_REW_MANIPULATOR,
-                  "cacto_sys_create: reward kind not implemented in this build (ur5 / car_park)");
+    CACTO_REQUIRE(p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR || p.dyn_kind == CACTO_DYN_CHAIN ||
+                      p.dyn_kind == CACTO_DYN_CAR || p.dyn_kind == CACTO_DYN_CAR_PARK,
+                  "cacto_sys_create: unknown dynamics kind");
+    CACTO_REQUIRE(p.reward_kind == CACTO_REW_PLANAR || p.reward_kind == CACTO_REW_MANIPULATOR ||
+                      p.reward_kind == CACTO_REW_UR5 || p.reward_kind == CACTO_REW_CAR_PARK,
+                  "cacto_sys_create: unknown reward kind");
+    if (p.dyn_kind == CACTO_DYN_CAR || p.dyn_kind == CACTO_DYN_CAR_PARK)
+      CACTO_REQUIRE(p.nb_state == 6 && p.nb_action == 2, "car / car_park need ns = 6, na = 2");
+    if (p.dyn_kind == CACTO_DYN_CAR_PARK)
+      CACTO_REQUIRE(p.L_delta > 0.0 && p.tau_delta > 0.0, "car_park needs L_delta > 0 and tau_delta > 0");
+    if (p.reward_kind == CACTO_REW_CAR_PARK)
+      CACTO_REQUIRE(p.dyn_kind == CACTO_DYN_CAR_PARK && p.n_check >= 1 && p.n_check <= 10,
+                    "car_park reward needs car_park dynamics and 1..10 check points");
+    if (p.reward_kind == CACTO_REW_UR5)
+      CACTO_REQUIRE(p.dyn_kind == CACTO_DYN_CHAIN, "ur5 reward needs chain dynamics");
     if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) {
       CACTO_REQUIRE(p.nb_state == 3 && p.nb_action == 2, "single integrator needs ns = 3, na = 2");
     }

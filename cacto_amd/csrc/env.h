@@ -343,6 +343,7 @@ __device__ inline V3 chain_ee(const SysDevice& sd, const double* q) {
 // which makes `v*dt` a float32 product and `self.v += dv*dt` round to float32 (numpy in-place on a
 // float32 view, robot_utils.py:403-405); otherwise all float64 (rollouts). environment.py:80-91.
 // NJ = 0: single integrator (environment.py:235-243); NJ > 0: Pinocchio chain with NJ joints.
+// NJ = -1: Car (environment.py:437-448), NJ = -2: CarPark (environment.py:584-595).
 template <int NJ>
 __device__ inline bool env_simulate(const SysDevice& sd, const double* s, const double* a, bool f32in, double* out) {
   const double dt = sd.p.dt;
@@ -350,6 +351,39 @@ __device__ inline bool env_simulate(const SysDevice& sd, const double* s, const 
     out[0] = s[0] + dt * a[0];
     out[1] = s[1] + dt * a[1];
     out[2] = s[2] + dt;
+    return true;
+  } else if constexpr (NJ == -1) {
+    // x' = x + dt*v*tf.cos(th) + dt**2*a*tf.cos(th)/2 (and y with sin). With float32 inputs
+    // (simulate_batch in compute_actor_grad) numpy-1.x makes dt*v a float64 scalar, TF casts it to
+    // float32 against the float32 tf.cos result, so x', y' are float32 arithmetic; the other
+    // components stay float64 scalars.
+    const double dt2 = dt * dt;
+    if (f32in) {
+      const float th = (float)s[2];
+      const float c = cosf(th), sn = sinf(th);
+      const float x1 = __fadd_rn((float)s[0], __fmul_rn((float)(dt * s[3]), c));
+      out[0] = (double)__fadd_rn(x1, __fdiv_rn(__fmul_rn((float)(dt2 * s[4]), c), 2.0f));
+      const float y1 = __fadd_rn((float)s[1], __fmul_rn((float)(dt * s[3]), sn));
+      out[1] = (double)__fadd_rn(y1, __fdiv_rn(__fmul_rn((float)(dt2 * s[4]), sn), 2.0f));
+    } else {
+      const double c = cos(s[2]), sn = sin(s[2]);
+      out[0] = (s[0] + dt * s[3] * c) + dt2 * s[4] * c / 2.0;
+      out[1] = (s[1] + dt * s[3] * sn) + dt2 * s[4] * sn / 2.0;
+    }
+    out[2] = s[2] + dt * a[0];
+    out[3] = s[3] + dt * s[4];
+    out[4] = s[4] + dt * a[1];
+    out[5] = s[5] + dt;
+    return true;
+  } else if constexpr (NJ == -2) {
+    // math.cos/sin/tan: float64 for any input dtype.
+    const double L = sd.p.L_delta, tau = sd.p.tau_delta;
+    out[0] = s[0] + dt * s[3] * cos(s[2]);
+    out[1] = s[1] + dt * s[3] * sin(s[2]);
+    out[2] = s[2] + dt * s[3] * tan(s[4]) / L;
+    out[3] = s[3] + dt * a[0];
+    out[4] = s[4] + dt * a[1] / tau;
+    out[5] = s[5] + dt;
     return true;
   } else {
     double M[NJ * NJ], h[NJ], dv[NJ];
@@ -410,16 +444,23 @@ __device__ inline void env_simulate_const(const SysDevice& sd, const ConstDyn<NJ
 
 // Env.derivative (environment.py:93-109 / SI :209-219): Fu[ns, na] row-major, rows scaled by
 // 1/state_norm when NORMALIZE_INPUTS.
+// Car :408-418 (Fu[2,0] = Fu[4,1] = dt), CarPark :555-565 (Fu[3,0] = dt, Fu[4,1] = dt/tau_delta).
 template <int NJ>
 __device__ inline void env_derivative(const SysDevice& sd, const double* s, double* Fu) {
   const cacto_sys_params& p = sd.p;
-  constexpr int NS = NJ == 0 ? 3 : 2 * NJ + 1;
-  constexpr int NA = NJ == 0 ? 2 : NJ;
+  constexpr int NS = NJ == 0 ? 3 : NJ < 0 ? 6 : 2 * NJ + 1;
+  constexpr int NA = NJ > 0 ? NJ : 2;
 #pragma unroll
   for (int k = 0; k < NS * NA; ++k) Fu[k] = 0.0;
   if constexpr (NJ == 0) {
     Fu[0 * NA + 0] = p.dt;
     Fu[1 * NA + 1] = p.dt;
+  } else if constexpr (NJ == -1) {
+    Fu[2 * NA + 0] = p.dt;
+    Fu[4 * NA + 1] = p.dt;
+  } else if constexpr (NJ == -2) {
+    Fu[3 * NA + 0] = p.dt;
+    Fu[4 * NA + 1] = p.dt / p.tau_delta;
   } else {
     double M[NJ * NJ], h[NJ], zero[NJ];
 #pragma unroll
@@ -448,8 +489,12 @@ __device__ inline void env_derivative(const SysDevice& sd, const double* s, doub
 
 template <int NJ>
 __device__ inline V3 env_ee(const SysDevice& sd, const double* s) {
-  if constexpr (NJ == 0) {
-    return v3(s[0], s[1], 0.0);  // SI / car: environment.py:245-250
+  if constexpr (NJ == 0 || NJ == -1) {
+    return v3(s[0], s[1], 0.0);  // SI / car: environment.py:245-250, :450-455
+  } else if constexpr (NJ == -2) {
+    // CarPark :597-602: p = s[:2] + [[c, -s], [s, c]] . [L/2, 0]
+    const double c = cos(s[2]), sn = sin(s[2]), h = sd.p.L_delta / 2.0;
+    return v3(s[0] + (c * h + -sn * 0.0), s[1] + (sn * h + c * 0.0), 0.0);
   } else {
     return chain_ee<NJ>(sd, s);
   }
@@ -497,11 +542,114 @@ __device__ __forceinline__ double combine_reward(const cacto_sys_params& p, cons
   return p.scale * r;
 }
 
+// CarPark obs_cost_fun (environment.py:604-613) for one check point, in the Python expression's
+// left-to-right order (fv = 1, k = k_db).
+__device__ inline double box_cost(double x, double y, double xs, double ys, double Wx, double Wy, double k) {
+  const double k2 = k * k;
+  const double ay = (y - ys) + Wy / 2, by = (y - ys) - Wy / 2;
+  const double ax = (x - xs) + Wx / 2, bx = (x - xs) - Wx / 2;
+  const double t1 = 4.0 + 4.0 * (ay * ay) * k2, t2 = 4.0 + 4.0 * (by * by) * k2;
+  const double t3 = 4.0 + 4.0 * (ax * ax) * k2, t4 = 4.0 + 4.0 * (bx * bx) * k2;
+  double r = pow(t1, -0.5);
+  r = r * (-sqrt(t2) / 2.0 + by * k);
+  r = r * pow(t3, -0.5);
+  r = r * pow(t2, -0.5);
+  r = r * (sqrt(t1) / 2.0 + ay * k);
+  r = r * pow(t4, -0.5);
+  r = r * (sqrt(t3) / 2.0 + ax * k);
+  r = r * (-sqrt(t4) / 2.0 + bx * k);
+  return r;
+}
+
+// numpy's pairwise float64 sum of n <= 15 contiguous values (8 partial sums, then the tail).
+__device__ inline double np_sum_small(const double* v, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += v[i];
+    return r;
+  }
+  double r = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  for (int i = 8; i < n; ++i) r += v[i];
+  return r;
+}
+
+// CarPark.reward (environment.py:615-641): 10 body check points x 3 smooth boxes.
+// `f32state`: theta came from a float32 tensor, so np.cos/np.sin run in float32.
+__device__ inline double carpark_obs_cost(const cacto_sys_params& p, double x, double y, double th, bool f32state) {
+  const double c = f32state ? (double)cosf((float)th) : cos(th);
+  const double sn = f32state ? (double)sinf((float)th) : sin(th);
+  double tot = 0.0;
+  const double* o = p.obs;
+  for (int ob = 0; ob < 3; ++ob) {
+    double v[10];
+    for (int k = 0; k < p.n_check; ++k) {
+      const double bx = p.check_points[2 * k], by = p.check_points[2 * k + 1];
+      const double wx = (c * bx + -sn * by) + x, wy = (sn * bx + c * by) + y;
+      v[k] = box_cost(wx, wy, o[2 * ob], o[2 * ob + 1], o[6 + 2 * ob], o[7 + 2 * ob], p.k_db);
+    }
+    tot = tot + np_sum_small(v, p.n_check);
+  }
+  return tot;
+}
+
+__device__ __forceinline__ double soft_term(double alpha, double e) { return log(exp(alpha * -(e - 1.0)) + 1.0) / alpha; }
+
+// UR5.reward (environment.py:780-805): 3-D ellipsoids, peak over x, y, z, joint-velocity cost and
+// u_cost = a.a (the bound term only enters reward_batch's float32 part).
+template <int NJ>
+__device__ inline double ur5_reward(const SysDevice& sd, const double* w, const double* s, const double* a,
+                                    bool f32state) {
+  const cacto_sys_params& p = sd.p;
+  const V3 e = env_ee<NJ>(sd, s);
+  const double* o = p.obs;
+  double ell[3];
+  for (int k = 0; k < 3; ++k) {
+    const double dx = e.x - o[3 * k], dy = e.y - o[3 * k + 1], dz = e.z - o[3 * k + 2];
+    const double A = o[9 + 3 * k] / 2, B = o[10 + 3 * k] / 2, Cc = o[11 + 3 * k] / 2;
+    ell[k] = soft_term(p.alpha, (dx * dx) / (A * A) + (dy * dy) / (B * B) + (dz * dz) / (Cc * Cc));
+  }
+  const double dx = e.x - p.target[0], dy = e.y - p.target[1], dz = e.z - p.target[2];
+  const double s01 = sqrt(0.1);
+  double pk = sqrt(dx * dx + 0.1);
+  pk = pk - s01;
+  pk = pk - 0.1;
+  pk = pk + sqrt(dy * dy + 0.1);
+  pk = pk - s01;
+  pk = pk - 0.1;
+  pk = pk + sqrt(dz * dz + 0.1);
+  pk = pk - s01;
+  pk = pk - 0.1;
+  const double peak = log(exp(p.alpha2 * -pk) + 1.0) / p.alpha2;
+  double u_cost = 0.0;
+  if (a) {
+    constexpr int NA = NJ > 0 ? NJ : 2;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) u_cost += a[i] * a[i];
+  }
+  double vel = 0.0;
+  if constexpr (NJ > 0) {
+    if (f32state) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) acc = __fadd_rn(acc, __fmul_rn((float)s[NJ + k], (float)s[NJ + k]));
+      vel = acc;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) vel += s[NJ + k] * s[NJ + k];
+    }
+  }
+  const double dist = (dx * dx + dy * dy) + dz * dz;
+  double r = -w[0] * dist + w[1] * peak;
+  r = r - w[2] * vel - w[3] * ell[0] - w[4] * ell[1] - w[5] * ell[2] - w[6] * u_cost + p.offset;
+  return p.scale * r;
+}
+
 template <int NJ>
 __device__ inline double env_reward(const SysDevice& sd, const double* w, const double* s, const double* a,
                                     bool f32state) {
-  constexpr int NA = NJ == 0 ? 2 : NJ;
+  constexpr int NA = NJ > 0 ? NJ : 2;
   const cacto_sys_params& p = sd.p;
+  if (p.reward_kind == CACTO_REW_UR5) return ur5_reward<NJ>(sd, w, s, a, f32state);
   const V3 e = env_ee<NJ>(sd, s);
   const double x = e.x, y = e.y;
   const double* o = p.obs;
@@ -520,6 +668,13 @@ __device__ inline double env_reward(const SysDevice& sd, const double* w, const 
   const double u_cost = a ? bound_control_cost<NA>(p, a) : 0.0;
   const double dist = dx * dx + dy * dy;
   double r = -w[0] * dist + w[1] * peak;
+  if (NJ == -2 && p.reward_kind == CACTO_REW_CAR_PARK) {
+    // - w2*v^2 - w3*obs_cost (CarPark.reward :638)
+    const double v2 = f32state ? (double)__fmul_rn((float)s[3], (float)s[3]) : s[3] * s[3];
+    const double obs = carpark_obs_cost(p, x, y, s[2], f32state);
+    r = r - w[2] * v2 - w[3] * obs - w[6] * u_cost + p.offset;
+    return p.scale * r;
+  }
   if (NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR) {
     double vel = 0.0;
     if (w[2] != 0.0) {
@@ -563,16 +718,19 @@ __device__ inline float reward_batch_f32(const cacto_sys_params& p, double w6, c
   return __fadd_rn(__fmul_rn(scale, __fmul_rn(nw6, u)), (float)partial);
 }
 
+// NJ: 0 single integrator, -1 car, -2 car_park (kinematic, 6 states, 2 controls), > 0 chain joints.
 template <int NJ>
 struct Dims {
-  static constexpr int NS = NJ == 0 ? 3 : 2 * NJ + 1;
-  static constexpr int NA = NJ == 0 ? 2 : NJ;
+  static constexpr int NS = NJ == 0 ? 3 : NJ < 0 ? 6 : 2 * NJ + 1;
+  static constexpr int NA = NJ > 0 ? NJ : 2;
 };
 
 // Dispatch a templated launcher on the system's dynamics: F<NJ>::run(args...).
 template <template <int> class F, typename... Args>
 inline int dispatch_nj(const cacto_sys_params& p, Args&&... args) {
   if (p.dyn_kind == CACTO_DYN_SINGLE_INTEGRATOR) return F<0>::run(args...);
+  if (p.dyn_kind == CACTO_DYN_CAR) return F<-1>::run(args...);
+  if (p.dyn_kind == CACTO_DYN_CAR_PARK) return F<-2>::run(args...);
   switch (p.n_joints) {
     case 2: return F<2>::run(args...);
     case 3: return F<3>::run(args...);

@@ -259,6 +259,8 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
 #pragma unroll
   for (int k = 0; k < 8; ++k) w[k] = k >= p.n_weights ? 0.0 : Wext ? Wext[k] : p.w_running[k];
   const bool want_R = Rtraj != nullptr, want_EE = EEtraj != nullptr || want_R;
+  // planar / manipulator rewards are split over waves 1-3 (terms of EE(s)); others whole on wave 1
+  const bool split_R = p.reward_kind == CACTO_REW_PLANAR || p.reward_kind == CACTO_REW_MANIPULATOR;
   ActorRegs R;
   if (use_actor) load_actor_regs(N, na, L, R, WL);
   if (L.tid == 0) tmax = 0;
@@ -318,6 +320,14 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
           env_simulate_const<NJ>(sd, cd, s, a, sn);
         else
           env_simulate<NJ>(sd, s, a, false, sn);
+      } else if (want_R && !split_R) {
+        // car_park / UR5: the whole Env.step reward of (s, a) on wave 1 (environment.py:615-641, :780-805)
+        if (L.wave == 1) {
+          double s[ns];
+#pragma unroll
+          for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
+          terms[c * 6 + 0] = env_reward<NJ>(sd, w, s, a, false);
+        }
       } else if (want_R) {
         const double x = sEE[c * 3 + 0], y = sEE[c * 3 + 1];
         const double* o = p.obs;
@@ -346,8 +356,9 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (want_R) {
           const bool has_vel = NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR;
           Rtraj[(size_t)b * T + t] =
-              combine_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], terms[c * 6 + 3], terms[c * 6 + 5], has_vel,
-                             terms[c * 6 + 0], terms[c * 6 + 1], terms[c * 6 + 2], terms[c * 6 + 4]);
+              split_R ? combine_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], terms[c * 6 + 3], terms[c * 6 + 5],
+                                       has_vel, terms[c * 6 + 0], terms[c * 6 + 1], terms[c * 6 + 2], terms[c * 6 + 4])
+                      : terms[c * 6 + 0];
         }
         if (Atraj)
 #pragma unroll

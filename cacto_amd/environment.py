@@ -131,14 +131,29 @@ class DoubleIntegrator(Env):
     """environment.py:288-362."""
 
 
+class Car(Env):
+    """environment.py:364-491 (kinematic car: x, y, theta, v, a)."""
+
+
+class CarPark(Car):
+    """environment.py:493-652 (kinematic bicycle, smooth-box obstacles over body check points)."""
+
+
 class Manipulator(Env):
     """environment.py:654-734."""
+
+
+class UR5(Env):
+    """environment.py:736-816 (6-DoF arm, 3-D ellipsoids)."""
 
 
 ENV_CLASSES = {
     "single_integrator": SingleIntegrator,
     "double_integrator": DoubleIntegrator,
+    "car": Car,
+    "car_park": CarPark,
     "manipulator": Manipulator,
+    "ur5": UR5,
 }
 
 

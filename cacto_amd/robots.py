@@ -109,9 +109,37 @@ def _planar_manipulator_3dof() -> RobotModel:
     return RobotModel("planar_manipulator_3dof", joints, 2, eye.copy(), np.array([10.0, 0.0, 0.0]))
 
 
+def _ur5() -> RobotModel:
+    # urdf/ur5_robot.urdf (example-robot-data UR5): six revolute joints in a serial chain, every link
+    # inertia diagonal about its COM; EE fixed to wrist_3_link at xyz (0, 0.0823, 0), rpy (0, 0, 1.57079632679).
+    # Literal URDF numbers (the pitch 1.57079632679 is not exactly pi/2; kept as written).
+    hp = 1.57079632679
+    spec = [  # name, axis, rpy, xyz, mass, com, (ixx, iyy, izz)
+        ("shoulder_pan_joint", (0, 0, 1), (0, 0, 0), (0.0, 0.0, 0.089159), 3.7, (0, 0, 0),
+         (0.010267495893, 0.010267495893, 0.00666)),
+        ("shoulder_lift_joint", (0, 1, 0), (0, hp, 0), (0.0, 0.13585, 0.0), 8.393, (0, 0, 0.28),
+         (0.22689067591, 0.22689067591, 0.0151074)),
+        ("elbow_joint", (0, 1, 0), (0, 0, 0), (0.0, -0.1197, 0.425), 2.275, (0, 0, 0.25),
+         (0.049443313556, 0.049443313556, 0.004095)),
+        ("wrist_1_joint", (0, 1, 0), (0, hp, 0), (0.0, 0.0, 0.39225), 1.219, (0, 0, 0),
+         (0.111172755531, 0.111172755531, 0.21942)),
+        ("wrist_2_joint", (0, 0, 1), (0, 0, 0), (0.0, 0.093, 0.0), 1.219, (0, 0, 0),
+         (0.111172755531, 0.111172755531, 0.21942)),
+        ("wrist_3_joint", (0, 1, 0), (0, 0, 0), (0.0, 0.0, 0.09465), 0.1879, (0, 0, 0),
+         (0.0171364731454, 0.0171364731454, 0.033822)),
+    ]
+    joints = []
+    for k, (name, axis, rpy, xyz, m, com, I) in enumerate(spec):
+        joints.append(Joint(name, k - 1, REVOLUTE, np.array(axis, dtype=np.float64), rpy_to_matrix(*rpy),
+                            np.array(xyz, dtype=np.float64), mass=m, com=np.array(com, dtype=np.float64),
+                            inertia=np.diag(np.array(I, dtype=np.float64))))
+    return RobotModel("ur5", joints, 5, rpy_to_matrix(0.0, 0.0, hp), np.array([0.0, 0.0823, 0.0]))
+
+
 _BUILTIN = {
     "double_integrator": _double_integrator,
     "planar_manipulator_3dof": _planar_manipulator_3dof,
+    "ur5": _ur5,
 }
 
 

@@ -51,11 +51,19 @@ class System:
         robot = getattr(conf, "robot", None)
         if sid == "single_integrator":
             p.dyn_kind, p.reward_kind = L.CACTO_DYN_SINGLE_INTEGRATOR, L.CACTO_REW_PLANAR
-        elif robot is not None and sid in ("double_integrator", "manipulator"):
+        elif sid == "car":
+            p.dyn_kind, p.reward_kind = L.CACTO_DYN_CAR, L.CACTO_REW_PLANAR
+        elif sid == "car_park":
+            p.dyn_kind, p.reward_kind = L.CACTO_DYN_CAR_PARK, L.CACTO_REW_CAR_PARK
+            p.L_delta, p.tau_delta, p.k_db = float(conf.L_delta), float(conf.tau_delta), float(conf.k_db)
+            cp = np.asarray(conf.check_points_BF, dtype=np.float64)
+            p.n_check = cp.shape[0]
+            _fill(p.check_points, cp.reshape(-1))
+        elif robot is not None and sid in ("double_integrator", "manipulator", "ur5"):
             p.dyn_kind = L.CACTO_DYN_CHAIN
-            p.reward_kind = L.CACTO_REW_MANIPULATOR if sid == "manipulator" else L.CACTO_REW_PLANAR
+            p.reward_kind = {"manipulator": L.CACTO_REW_MANIPULATOR, "ur5": L.CACTO_REW_UR5}.get(sid, L.CACTO_REW_PLANAR)
         else:
-            raise NotImplementedError("system %r is not in this build's hot path yet" % sid)
+            raise NotImplementedError("system %r is not in this build's hot path" % sid)
         p.nb_state, p.nb_action = conf.nb_state, conf.nb_action
         p.nq = conf.nq or 0
         p.nv = conf.nv or 0

@@ -208,10 +208,145 @@ class Manipulator(Env):
         return self._planar_reward(weights, state, action, vel)
 
 
+class Car(Env):
+    """environment.py:364-491. Car.simulate (:437-448) uses tf.cos/tf.sin: with float32 inputs the
+    numpy-1.x scalar dt*v is float64, TF casts it to float32 against the float32 tf.cos, so x' and y'
+    are float32 arithmetic; with float64 inputs everything is float64."""
+
+    def simulate(self, state, action):
+        dt = self.conf.dt
+        s = np.asarray(state)
+        out = np.zeros(self.nx + 1)
+        if s.dtype == F32:
+            c, sn = F32(math.cos(F64(s[2]))), F32(math.sin(F64(s[2])))   # tf.cos(float32 scalar)
+            x1 = F32(s[0]) + F32(F64(dt) * F64(s[3])) * c
+            out[0] = F64(x1 + F32(F32(F64(dt) ** 2 * F64(s[4])) * c) / F32(2))
+            y1 = F32(s[1]) + F32(F64(dt) * F64(s[3])) * sn
+            out[1] = F64(y1 + F32(F32(F64(dt) ** 2 * F64(s[4])) * sn) / F32(2))
+        else:
+            c, sn = math.cos(F64(s[2])), math.sin(F64(s[2]))
+            out[0] = F64(s[0]) + dt * F64(s[3]) * c + dt ** 2 * F64(s[4]) * c / 2
+            out[1] = F64(s[1]) + dt * F64(s[3]) * sn + dt ** 2 * F64(s[4]) * sn / 2
+        out[2] = F64(s[2]) + dt * F64(action[0])
+        out[3] = F64(s[3]) + dt * F64(s[4])
+        out[4] = F64(s[4]) + dt * F64(action[1])
+        out[5] = F64(s[5]) + dt
+        return out
+
+    def derivative(self, state, action):
+        c = self.conf
+        Fu = np.zeros((self.nx + 1, self.nu))
+        Fu[2, 0] = c.dt
+        Fu[4, 1] = c.dt
+        if c.NORMALIZE_INPUTS:
+            Fu[:-1] *= (1 / c.state_norm_arr[:-1, None])
+        return Fu
+
+    def get_end_effector_position(self, state):
+        p = np.zeros(3)
+        p[:2] = np.asarray(state[:2]).astype(F64)
+        return p
+
+
+class CarPark(Car):
+    """environment.py:493-652 (math.cos/sin/tan: float64 dynamics for any input dtype)."""
+
+    def simulate(self, state, action):
+        c = self.conf
+        dt = c.dt
+        s = [F64(v) for v in state]
+        out = np.zeros(self.nx + 1)
+        out[0] = s[0] + dt * s[3] * math.cos(s[2])
+        out[1] = s[1] + dt * s[3] * math.sin(s[2])
+        out[2] = s[2] + dt * s[3] * math.tan(s[4]) / c.L_delta
+        out[3] = s[3] + dt * F64(action[0])
+        out[4] = s[4] + dt * F64(action[1]) / c.tau_delta
+        out[5] = s[5] + dt
+        return out
+
+    def derivative(self, state, action):
+        c = self.conf
+        Fu = np.zeros((self.nx + 1, self.nu))
+        Fu[3, 0] = c.dt
+        Fu[4, 1] = c.dt / c.tau_delta
+        if c.NORMALIZE_INPUTS:
+            Fu[:-1] *= (1 / c.state_norm_arr[:-1, None])
+        return Fu
+
+    def get_end_effector_position(self, state):
+        th = F64(state[2])
+        R = np.array([[math.cos(th), -math.sin(th)], [math.sin(th), math.cos(th)]])
+        p = np.zeros(3)
+        p[:2] = np.asarray(state[:2]).astype(F64) + R.dot(np.array([self.conf.L_delta / 2, 0]))
+        return p
+
+    def obs_cost_fun(self, x, y, x_step, y_step, Wx, Wy, fv=1):
+        k = self.conf.k_db
+        term1 = 4 + 4 * (y - y_step + Wy / 2) ** 2 * k ** 2
+        term2 = 4 + 4 * (y - y_step - Wy / 2) ** 2 * k ** 2
+        term3 = 4 + 4 * (x - x_step + Wx / 2) ** 2 * k ** 2
+        term4 = 4 + 4 * (x - x_step - Wx / 2) ** 2 * k ** 2
+        return ((term1) ** (-1 / 2) * fv * (-np.sqrt(term2) / 2 + (y - y_step - Wy / 2) * k) * (term3) ** (-1 / 2)
+                * (term2) ** (-1 / 2) * (np.sqrt(term1) / 2 + (y - y_step + Wy / 2) * k) * (term4) ** (-1 / 2)
+                * (np.sqrt(term3) / 2 + (x - x_step + Wx / 2) * k) * (-np.sqrt(term4) / 2 + (x - x_step - Wx / 2) * k))
+
+    def reward(self, weights, state, action=None):
+        c = self.conf
+        p = self.get_end_effector_position(state)
+        x, y = F64(p[0]), F64(p[1])
+        th = state[2]   # float32 state -> np.cos/np.sin in float32
+        R = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+        wf = np.dot(R, c.check_points_BF.T).T + np.array([x, y])
+        o = self.obs
+        obs_cost = 0
+        for k in range(3):
+            obs_cost += np.sum(self.obs_cost_fun(wf[:, 0], wf[:, 1], o[2 * k], o[2 * k + 1], o[6 + 2 * k], o[7 + 2 * k]))
+        peak = self._peak(x - self.target[0], y - self.target[1])
+        u_cost = self.bound_control_cost(action) if action is not None else 0
+        dist = (x - self.target[0]) ** 2 + (y - self.target[1]) ** 2
+        w = [F64(v) for v in weights]
+        v2 = state[3] ** 2   # float32 scalar square for a float32 state
+        r = - w[0] * dist + w[1] * peak - w[2] * F64(v2) - w[3] * obs_cost - w[6] * u_cost + self.offset
+        return self.scale * r
+
+
+class UR5(Env):
+    """environment.py:736-816."""
+
+    def reward(self, weights, state, action=None):
+        e = self.get_end_effector_position(state)
+        x, y, z = F64(e[0]), F64(e[1]), F64(e[2])
+        o = self.obs
+        ells = []
+        for k in range(3):
+            xc, yc, zc = o[3 * k], o[3 * k + 1], o[3 * k + 2]
+            A, B, C = o[9 + 3 * k], o[10 + 3 * k], o[11 + 3 * k]
+            ex = ((x - xc) ** 2) / ((A / 2) ** 2) + ((y - yc) ** 2) / ((B / 2) ** 2) + ((z - zc) ** 2) / ((C / 2) ** 2)
+            ells.append(math.log(math.exp(self.alpha * -(ex - 1.0)) + 1) / self.alpha)
+        peak = self._peak(x - self.target[0], y - self.target[1], z - self.target[2])
+        u_cost = F64(np.asarray(action, dtype=F64).dot(np.asarray(action, dtype=F64))) if action is not None else 0
+        v = np.asarray(state[self.nq:self.nx])
+        if v.dtype == F32:
+            acc = F32(0)
+            for k in range(len(v)):
+                acc = F32(acc + v[k] * v[k])
+            vel = F64(acc)
+        else:
+            vel = F64(v.dot(v))
+        dist = (x - self.target[0]) ** 2 + (y - self.target[1]) ** 2 + (z - self.target[2]) ** 2
+        w = [F64(v_) for v_ in weights]
+        r = (- w[0] * dist + w[1] * peak - w[2] * vel - w[3] * ells[0] - w[4] * ells[1] - w[5] * ells[2]
+             - w[6] * u_cost + self.offset)
+        return self.scale * r
+
+
 ENV_CLASSES = {
     'single_integrator': SingleIntegrator,
     'double_integrator': DoubleIntegrator,
+    'car': Car,
+    'car_park': CarPark,
     'manipulator': Manipulator,
+    'ur5': UR5,
 }
 
 

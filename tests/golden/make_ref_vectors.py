@@ -43,6 +43,32 @@ def install_stubs():
     keras.regularizers = types.SimpleNamespace()
     tf.keras = keras
     tf.function = lambda f: f
+
+    class TFScalar:
+        """Eager TF scalar: the other operand is converted to THIS tensor's dtype (no numpy
+        promotion), as tf.convert_to_tensor(x, dtype=y.dtype) does in TF binary ops."""
+
+        def __init__(self, v, dt):
+            self.dt = dt
+            self.v = dt(v)
+
+        def _o(self, x):
+            return self.dt(x.v if isinstance(x, TFScalar) else x)
+
+        def __mul__(self, x): return TFScalar(self.v * self._o(x), self.dt)
+        __rmul__ = __mul__
+        def __add__(self, x): return TFScalar(self.v + self._o(x), self.dt)
+        def __radd__(self, x): return TFScalar(self._o(x) + self.v, self.dt)
+        def __truediv__(self, x): return TFScalar(self.v / self._o(x), self.dt)
+        def __float__(self): return float(self.v)
+
+    def _trig(fn):
+        def f(x):
+            dt = np.float32 if isinstance(x, np.float32) else np.float64
+            return TFScalar(fn(float(x)), dt)   # libm cos/sin, rounded to the tensor dtype
+        return f
+    import math as _m
+    tf.cos, tf.sin = _trig(_m.cos), _trig(_m.sin)
     sys.modules["tensorflow"] = tf
     sys.modules["tensorflow.keras"] = keras
 
@@ -100,6 +126,8 @@ def main():
     import conf_single_integrator as csi
     import conf_double_integrator as cdi
     import RL
+    import conf_car as ccar
+    import conf_car_park as ccp
     os.chdir(cwd)
 
     out = {}
@@ -208,6 +236,27 @@ def main():
     out["di_S"], out["di_A"] = SD, AD
     out["di_reward"] = np.asarray([di.reward(w, s, a) for w, s, a in zip(W, SD, AD)])
     out["di_reward32"] = np.asarray([di.reward(w, s) for w, s in zip(W, SD.astype(np.float32))])
+
+    # ---- car / car_park (environment.py:364-652) ----
+    car, cpk = environment.Car(ccar), environment.CarPark(ccp)
+    n = 200
+    for tag, env, c in (("car", car, ccar), ("cp", cpk, ccp)):
+        lo, hi = np.asarray(c.x_init_min, float), np.asarray(c.x_init_max, float)
+        S = lo + (hi - lo) * rng.uniform(size=(n, 6))
+        S[:, 3] = rng.uniform(-5, 5, size=n)
+        S[:, 4] = rng.uniform(-0.5, 0.5, size=n)
+        if tag == "cp":
+            S[:, 1] = rng.uniform(-1.0, 7.5, size=n)   # reach the boxes' edges
+        A = rng.uniform(-1, 1, size=(n, 2)) * c.u_max
+        Wc = np.where(rng.uniform(size=(n, 1)) < .5, c.cost_weights_running, c.cost_weights_terminal)
+        S32, A32 = S.astype(np.float32), A.astype(np.float32)
+        out[tag + "_S"], out[tag + "_A"], out[tag + "_W"] = S, A, Wc
+        out[tag + "_sim"] = np.asarray([env.simulate(s, a) for s, a in zip(S, A)])
+        out[tag + "_sim32"] = np.asarray([env.simulate(s, a) for s, a in zip(S32, A32)])
+        out[tag + "_der"] = np.asarray([env.derivative(s, a) for s, a in zip(S, A)])
+        out[tag + "_ee"] = np.asarray([env.get_end_effector_position(s) for s in S])
+        out[tag + "_reward"] = np.asarray([env.reward(w, s, a) for w, s, a in zip(Wc, S, A)])
+        out[tag + "_reward32"] = np.asarray([env.reward(w, s) for w, s in zip(Wc, S32)])
 
     # ---- RL_Solve n-step targets (RL.py:145-189) ----
     rl = RL.RL_AC(si, None, csi, 0)

@@ -46,7 +46,8 @@ def test_workspace_query_without_gpu_needs_a_handle():
 
 @pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference checkout not present")
 @pytest.mark.parametrize("urdf,name", [("double_integrator.urdf", "double_integrator"),
-                                       ("planar_manipulator_3dof.urdf", "planar_manipulator_3dof")])
+                                       ("planar_manipulator_3dof.urdf", "planar_manipulator_3dof"),
+                                       ("ur5_robot.urdf", "ur5")])
 def test_builtin_models_match_reference_urdf(urdf, name):
     m = parse_urdf(os.path.join(REFERENCE, "urdf", urdf))
     b = builtin_model(name)
@@ -78,7 +79,7 @@ def _ref_constants(fname):
 
 
 @pytest.mark.skipif(not os.path.isdir(REFERENCE), reason="reference checkout not present")
-@pytest.mark.parametrize("system", ["single_integrator", "double_integrator", "manipulator"])
+@pytest.mark.parametrize("system", ["single_integrator", "double_integrator", "manipulator", "car", "car_park", "ur5"])
 def test_conf_constants_match_reference(system):
     ref = _ref_constants("conf_%s.py" % system)
     conf = load_conf(system)

@@ -174,3 +174,91 @@ def test_di_final_policy_known_answer():
     assert abs(ends[(10.0, 10.0)][0] + 19.3) < 0.2
     near = [np.hypot(e[0] + 8, e[1] + 0.9) < 1.5 for e in ends.values()]
     assert sum(near) >= 5
+
+
+def _fk_links(model, q):
+    """Independent forward kinematics (4x4 homogeneous transforms + Rodrigues), per link:
+    world rotation R_i and COM position c_i (robots.py model conventions: joint frame placed in
+    the parent joint frame by (R, p), then rotated about `axis` by q_i)."""
+    def rod(axis, th):
+        a = np.asarray(axis, float) / np.linalg.norm(axis)
+        K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+        return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+    Ts, out = [], []
+    for i, j in enumerate(model.joints):
+        T = np.eye(4)
+        T[:3, :3], T[:3, 3] = j.R, j.p
+        J = np.eye(4)
+        J[:3, :3] = rod(j.axis, q[i])
+        Tw = (Ts[j.parent] if j.parent >= 0 else np.eye(4)) @ T @ J
+        Ts.append(Tw)
+        out.append((Tw[:3, :3], Tw[:3, :3] @ j.com + Tw[:3, 3]))
+    return out
+
+
+def _lagrangian_terms(model, q, v, eps=1e-6):
+    """M(q) from link Jacobians (finite differences of the independent FK) and
+    h(q, v) = Mdot v - 1/2 d(v'Mv)/dq + dV/dq (Lagrange's equations), by central differences."""
+    n = len(q)
+    g = np.asarray(model.gravity, float)
+
+    def mass(qq):
+        links = _fk_links(model, qq)
+        M = np.zeros((n, n))
+        for i, j in enumerate(model.joints):
+            Jv, Jw = np.zeros((3, n)), np.zeros((3, n))
+            for k in range(n):
+                dq = np.zeros(n)
+                dq[k] = eps
+                Rp, cp = _fk_links(model, qq + dq)[i]
+                Rm, cm = _fk_links(model, qq - dq)[i]
+                Jv[:, k] = (cp - cm) / (2 * eps)
+                W = (Rp - Rm) / (2 * eps) @ links[i][0].T   # skew(omega_k)
+                Jw[:, k] = [W[2, 1], W[0, 2], W[1, 0]]
+            R = links[i][0]
+            M += j.mass * Jv.T @ Jv + Jw.T @ (R @ j.inertia @ R.T) @ Jw
+        return M
+
+    def potential(qq):
+        return -sum(j.mass * g @ c for j, (_, c) in zip(model.joints, _fk_links(model, qq)))
+
+    M = mass(q)
+    h = np.zeros(n)
+    e2 = 1e-4
+    Mdot = (mass(q + e2 * v) - mass(q - e2 * v)) / (2 * e2)
+    h += Mdot @ v
+    for k in range(n):
+        dq = np.zeros(n)
+        dq[k] = e2
+        h[k] -= 0.5 * (v @ mass(q + dq) @ v - v @ mass(q - dq) @ v) / (2 * e2)
+        h[k] += (potential(q + dq) - potential(q - dq)) / (2 * e2)
+    return M, h
+
+
+def test_ur5_chain_matches_lagrangian():
+    """UR5 (6-DoF, 3-D, gravity) oracle CRBA/RNEA vs an independent Lagrangian evaluation. Pinocchio
+    (the reference's dynamics, pin 2.9.2) is absent: UR5 parity is pinned by this internal
+    consistency only."""
+    from cacto_amd.robots import builtin_model
+    from oracle.dynamics import Chain
+    model = builtin_model("ur5")
+    chain = Chain.from_model(model)
+    rng = np.random.default_rng(5)
+    for _ in range(3):
+        q = rng.uniform(-np.pi, np.pi, 6)
+        v = rng.uniform(-1, 1, 6)
+        M_ref, h_ref = _lagrangian_terms(model, q, v)
+        np.testing.assert_allclose(chain.mass_matrix(q), M_ref, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(chain.nle(q, v), h_ref, rtol=1e-5, atol=1e-5)
+        # EE frame: wrist_3 placement composed with the fixed EE offset
+        ee = chain.frame_position(q)
+        Tw = np.eye(4)
+        for i, j in enumerate(model.joints):
+            A = np.eye(4)
+            A[:3, :3], A[:3, 3] = j.R, j.p
+            Jr = np.eye(4)
+            a = j.axis / np.linalg.norm(j.axis)
+            K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+            Jr[:3, :3] = np.eye(3) + np.sin(q[i]) * K + (1 - np.cos(q[i])) * K @ K
+            Tw = Tw @ A @ Jr
+        np.testing.assert_allclose(ee, Tw[:3, :3] @ model.ee_p + Tw[:3, 3], atol=1e-12)
