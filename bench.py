@@ -52,7 +52,7 @@ def parse():
     p.add_argument("--batches", default="128,4096")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--extra-systems", default="manipulator")
+    p.add_argument("--extra-systems", default="manipulator,car_park,ur5")
     p.add_argument("--no-diagnostics", action="store_true",
                    help="skip the rollout variants (profiling runs: every k_rollout dispatch is a full rollout)")
     return p.parse_args()
@@ -198,7 +198,7 @@ def rollout_diagnostics(rl, conf, roll, K=5):
     return res
 
 
-def fill_buffer(rl, conf, roll, seed):
+def fill_buffer(rl, conf, roll, seed, per=False):
     """Replay rows from the rollouts (RL_Solve n-step targets, RL.py:145-189, vectorised over
     episodes; rewards = the rollout rewards, dVdx synthetic N(0,1))."""
     from cacto_amd.replay_buffer import ReplayBuffer
@@ -226,7 +226,11 @@ def fill_buffer(rl, conf, roll, seed):
         if sum(len(x) for x in rows) >= conf.REPLAY_SIZE + 8192:
             break
     rows = np.concatenate(rows)
-    buf = ReplayBuffer(conf, rl.sys)
+    if per:
+        from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+        buf = PrioritizedReplayBuffer(conf, rl.sys)
+    else:
+        buf = ReplayBuffer(conf, rl.sys)
     for k in range(0, len(rows), 8192):     # per-batch adds, so the ring wraps and `full` latches
         buf.add_rows(rows[k:k + 8192])
     return buf
@@ -247,6 +251,66 @@ def update_phase(rl, buf, B, K, W, world, seed):
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
     return wall
+
+
+# BASELINE.json configs[2..4] (per GPU): rollouts, minibatches, Sobolev weight, PER.
+EXTRA = {
+    "manipulator": dict(R=8192, batches=(64, 8192), w_S=0.0, per=False,
+                        config="configs[2]: manipulator (3-DoF planar), batch 8192"),
+    "car_park": dict(R=4096, batches=(64, 4096), w_S=0.0, per=True,
+                     config="configs[3]: car_park, PER (alpha 0.6, beta 0.6), 4096 rollouts and B=4096 per GPU"),
+    "ur5": dict(R=2048, batches=(64, 2048), w_S=1e-2, per=False,
+                config="configs[4]: ur5 (6-DoF), Sobolev w-S=1e-2, 16384 rollouts / global batch over 8 GPUs "
+                       "(2048 per GPU)"),
+}
+
+
+def per_update_phase(rl, buf, B, K, W, world, seed):
+    """learn_and_update with PER (RL.py:122-137): sample (stratified, IS weights) -> update ->
+    priority update, with the per-step uniforms pre-drawn on the device."""
+    gen = np.random.Generator(np.random.PCG64(seed))
+    U = torch.as_tensor(gen.random((K + W, B)), device="cuda")
+    y = torch.empty(B, dtype=torch.float32, device="cuda")
+    V = torch.empty_like(y)
+
+    def step(i):
+        idx, w = buf.sample_device(U[i])
+        rl.update_rows(buf.storage, idx, w, y, V)
+        buf.update_priorities_device(idx, y, V)
+    for i in range(W):
+        step(i)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        step(W + i)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    return max_over_ranks(t1 - t0, world)
+
+
+def extra_system(name, args, world, rank):
+    cfg = EXTRA[name]
+    conf, env, rl = make_learner(name, w_S=cfg["w_S"])
+    if world > 1:
+        rl.set_data_parallel(world)
+    if cfg["per"]:
+        conf.prioritized_replay_alpha = 0.6
+    r = rollout_phase(rl, conf, env, cfg["R"], args.steps, args.warmup, world, rank)
+    buf = fill_buffer(rl, conf, r, seed=rank, per=cfg["per"])
+    ups = {}
+    for B in cfg["batches"]:
+        if cfg["per"]:
+            conf.BATCH_SIZE = B
+            wall = per_update_phase(rl, buf, B, args.update_steps, 3, world, seed=300 + rank)
+        else:
+            wall = update_phase(rl, buf, B, args.update_steps, 3, world, seed=200 + rank)
+        ups["B=%d" % B] = dict(value=args.update_steps / wall, unit="critic-updates/s", global_batch=B * world,
+                               ms_per_update=1e3 * wall / args.update_steps)
+    return dict(config=cfg["config"], env_steps_per_s=r["total_steps"] / r["wall"], rollouts_per_gpu=cfg["R"],
+                rollout_kernel_ms=r["kernel_ms"], env_steps_per_launch=r["steps_per_call"],
+                w_S=cfg["w_S"], per=cfg["per"], critic_updates=ups)
 
 
 def cpu_baseline_rollout(conf, rl, roll, seconds):
@@ -316,18 +380,7 @@ def main():
                                    mfma_frac=flop * K / wall / (FP32_MFMA_PEAK * world))
     extra = {}
     for sysname in [s for s in args.extra_systems.split(",") if s and s != args.system]:
-        c2, e2, rl2 = make_learner(sysname, w_S=0.0)
-        if world > 1:
-            rl2.set_data_parallel(world)
-        R2 = 8192 if sysname == "manipulator" else args.rollouts
-        r2 = rollout_phase(rl2, c2, e2, R2, args.steps, args.warmup, world, rank)
-        b2 = fill_buffer(rl2, c2, r2, seed=rank)
-        u2 = {}
-        for B in (64, 8192):
-            wall = update_phase(rl2, b2, B, args.update_steps, 3, world, seed=200 + rank)
-            u2["B=%d" % B] = dict(value=args.update_steps / wall, unit="critic-updates/s", global_batch=B * world)
-        extra[sysname] = dict(env_steps_per_s=r2["total_steps"] / r2["wall"], rollouts_per_gpu=R2,
-                              rollout_kernel_ms=r2["kernel_ms"], critic_updates=u2)
+        extra[sysname] = extra_system(sysname, args, world, rank)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline_rollout(conf, rl, roll, args.cpu_seconds)

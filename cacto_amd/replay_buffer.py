@@ -114,10 +114,14 @@ class PrioritizedReplayBuffer(ReplayBuffer):
 
     def sample_device(self, uniforms=None):
         """_sample_proportional + IS weights + exp_counter (replay_buffer.py:139-188)."""
-        B = self.conf.BATCH_SIZE
-        if uniforms is None:
-            uniforms = [self.random.random() for _ in range(B)]
-        u = torch.as_tensor(np.asarray(uniforms, dtype=np.float64), device=DEVICE)
+        if isinstance(uniforms, torch.Tensor):      # device uniforms (e.g. pre-drawn for many steps)
+            u = uniforms.to(device=DEVICE, dtype=torch.float64).contiguous()
+            B = u.shape[0]
+        else:
+            B = self.conf.BATCH_SIZE
+            if uniforms is None:
+                uniforms = [self.random.random() for _ in range(B)]
+            u = torch.as_tensor(np.asarray(uniforms, dtype=np.float64), device=DEVICE)
         idx = torch.empty(B, dtype=torch.int32, device=DEVICE)
         w = torch.empty(B, dtype=torch.float32, device=DEVICE)
         L.lib().call("cacto_per_sample", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.max_idx(),
