@@ -550,14 +550,16 @@ __device__ inline double box_cost(double x, double y, double xs, double ys, doub
   const double ax = (x - xs) + Wx / 2, bx = (x - xs) - Wx / 2;
   const double t1 = 4.0 + 4.0 * (ay * ay) * k2, t2 = 4.0 + 4.0 * (by * by) * k2;
   const double t3 = 4.0 + 4.0 * (ax * ax) * k2, t4 = 4.0 + 4.0 * (bx * bx) * k2;
-  double r = pow(t1, -0.5);
-  r = r * (-sqrt(t2) / 2.0 + by * k);
-  r = r * pow(t3, -0.5);
-  r = r * pow(t2, -0.5);
-  r = r * (sqrt(t1) / 2.0 + ay * k);
-  r = r * pow(t4, -0.5);
-  r = r * (sqrt(t3) / 2.0 + ax * k);
-  r = r * (-sqrt(t4) / 2.0 + bx * k);
+  // term**(-1/2) as 1/sqrt(term) (<= 1 ulp; numpy's own SIMD pow is not correctly rounded either)
+  const double q1 = sqrt(t1), q2 = sqrt(t2), q3 = sqrt(t3), q4 = sqrt(t4);
+  double r = 1.0 / q1;
+  r = r * (-q2 / 2.0 + by * k);
+  r = r * (1.0 / q3);
+  r = r * (1.0 / q2);
+  r = r * (q1 / 2.0 + ay * k);
+  r = r * (1.0 / q4);
+  r = r * (q3 / 2.0 + ax * k);
+  r = r * (-q4 / 2.0 + bx * k);
   return r;
 }
 
@@ -574,22 +576,27 @@ __device__ inline double np_sum_small(const double* v, int n) {
 }
 
 // CarPark.reward (environment.py:615-641): 10 body check points x 3 smooth boxes.
+// Pair pr = ob * n_check + k: check point k (rotated by theta, shifted to the EE) against box ob.
+__device__ inline double carpark_pair_cost(const cacto_sys_params& p, double x, double y, double c, double sn, int pr) {
+  const int ob = pr / p.n_check, k = pr - ob * p.n_check;
+  const double bx = p.check_points[2 * k], by = p.check_points[2 * k + 1];
+  const double wx = (c * bx + -sn * by) + x, wy = (sn * bx + c * by) + y;
+  const double* o = p.obs;
+  return box_cost(wx, wy, o[2 * ob], o[2 * ob + 1], o[6 + 2 * ob], o[7 + 2 * ob], p.k_db);
+}
+// obs_cost = 0; obs_cost += np.sum(box_1); += np.sum(box_2); += np.sum(box_3)
+__device__ inline double carpark_sum(const cacto_sys_params& p, const double* v) {
+  double tot = 0.0;
+  for (int ob = 0; ob < 3; ++ob) tot = tot + np_sum_small(v + ob * p.n_check, p.n_check);
+  return tot;
+}
 // `f32state`: theta came from a float32 tensor, so np.cos/np.sin run in float32.
 __device__ inline double carpark_obs_cost(const cacto_sys_params& p, double x, double y, double th, bool f32state) {
   const double c = f32state ? (double)cosf((float)th) : cos(th);
   const double sn = f32state ? (double)sinf((float)th) : sin(th);
-  double tot = 0.0;
-  const double* o = p.obs;
-  for (int ob = 0; ob < 3; ++ob) {
-    double v[10];
-    for (int k = 0; k < p.n_check; ++k) {
-      const double bx = p.check_points[2 * k], by = p.check_points[2 * k + 1];
-      const double wx = (c * bx + -sn * by) + x, wy = (sn * bx + c * by) + y;
-      v[k] = box_cost(wx, wy, o[2 * ob], o[2 * ob + 1], o[6 + 2 * ob], o[7 + 2 * ob], p.k_db);
-    }
-    tot = tot + np_sum_small(v, p.n_check);
-  }
-  return tot;
+  double v[30];
+  for (int pr = 0; pr < 3 * p.n_check; ++pr) v[pr] = carpark_pair_cost(p, x, y, c, sn, pr);
+  return carpark_sum(p, v);
 }
 
 __device__ __forceinline__ double soft_term(double alpha, double e) { return log(exp(alpha * -(e - 1.0)) + 1.0) / alpha; }
@@ -641,6 +648,18 @@ __device__ inline double ur5_reward(const SysDevice& sd, const double* w, const 
   const double dist = (dx * dx + dy * dy) + dz * dz;
   double r = -w[0] * dist + w[1] * peak;
   r = r - w[2] * vel - w[3] * ell[0] - w[4] * ell[1] - w[5] * ell[2] - w[6] * u_cost + p.offset;
+  return p.scale * r;
+}
+
+// CarPark.reward with the obstacle cost already summed (rollout path; float64 state).
+__device__ inline double carpark_reward(const cacto_sys_params& p, const double* w, double x, double y,
+                                        const double* s, const double* a, double obs) {
+  const double dx = x - p.target[0], dy = y - p.target[1];
+  const double peak = peak_cost(p, x, y);
+  const double u_cost = a ? bound_control_cost<2>(p, a) : 0.0;
+  const double dist = dx * dx + dy * dy;
+  double r = -w[0] * dist + w[1] * peak;
+  r = r - w[2] * (s[3] * s[3]) - w[3] * obs - w[6] * u_cost + p.offset;
   return p.scale * r;
 }
 

@@ -246,6 +246,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   __shared__ float st[16 * 16];
   __shared__ float A[16 * na];
   __shared__ double sS[16 * ns], sEE[16 * 3], terms[16 * 6];
+  __shared__ double cpv[NJ == -2 ? 16 * 30 : 1];  // car_park obstacle pair costs
   __shared__ int sb[16], sn_[16], salive[16];
   __shared__ int tmax;
   __shared__ ActorLds WL;
@@ -321,8 +322,9 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         else
           env_simulate<NJ>(sd, s, a, false, sn);
       } else if (want_R && !split_R) {
-        // car_park / UR5: the whole Env.step reward of (s, a) on wave 1 (environment.py:615-641, :780-805)
-        if (L.wave == 1) {
+        // UR5: the whole Env.step reward of (s, a) on wave 1 (environment.py:780-805); car_park's
+        // obstacle pairs are spread over waves 1-3 below
+        if (NJ != -2 && L.wave == 1) {
           double s[ns];
 #pragma unroll
           for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
@@ -348,6 +350,19 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         }
       }
     }
+    if constexpr (NJ == -2) {
+      // CarPark obstacle cost (environment.py:619-624): 3 x n_check smooth-box terms of EE(s), theta,
+      // over 12 lane groups (waves 1-3 x 4 groups of the 16 episode lanes)
+      if (want_R && L.wave >= 1) {
+        const bool act_c = s0 + c < B && salive[c] && t < sn_[c];
+        if (act_c) {
+          const int grp = (L.wave - 1) * 4 + (L.lane >> 4);
+          const double th = sS[c * ns + 2], ct = cos(th), stt = sin(th);
+          for (int pr = grp; pr < 3 * p.n_check; pr += 12)
+            cpv[c * 30 + pr] = carpark_pair_cost(p, sEE[c * 3 + 0], sEE[c * 3 + 1], ct, stt, pr);
+        }
+      }
+    }
     __syncthreads();
     // ---- E2
     if (active) {
@@ -355,10 +370,21 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
       if (L.wave == 0) {
         if (want_R) {
           const bool has_vel = NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR;
-          Rtraj[(size_t)b * T + t] =
-              split_R ? combine_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], terms[c * 6 + 3], terms[c * 6 + 5],
-                                       has_vel, terms[c * 6 + 0], terms[c * 6 + 1], terms[c * 6 + 2], terms[c * 6 + 4])
-                      : terms[c * 6 + 0];
+          double r;
+          if constexpr (NJ == -2) {
+            double a[na], s[ns];
+#pragma unroll
+            for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)A[c * na + i] : 0.0;
+#pragma unroll
+            for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
+            r = carpark_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], s, a, carpark_sum(p, cpv + c * 30));
+          } else {
+            r = split_R ? combine_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], terms[c * 6 + 3], terms[c * 6 + 5],
+                                         has_vel, terms[c * 6 + 0], terms[c * 6 + 1], terms[c * 6 + 2],
+                                         terms[c * 6 + 4])
+                        : terms[c * 6 + 0];
+          }
+          Rtraj[(size_t)b * T + t] = r;
         }
         if (Atraj)
 #pragma unroll

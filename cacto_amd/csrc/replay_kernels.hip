@@ -120,8 +120,13 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, doubl
   __shared__ int32_t id_s[PER_MAX_B];
   __shared__ double maxp_s[PER_THREADS];
   double my_max = -__builtin_inf();
+  bool unsorted = false;
   for (int i = threadIdx.x; i < n; i += blockDim.x) id_s[i] = idx[i];
   __syncthreads();
+  // Stratified samples come out non-decreasing in i (monotone prefix-sum search), so duplicates are
+  // adjacent and "last occurrence" is a neighbour test; arbitrary index lists take the O(n^2) scan.
+  for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) unsorted |= id_s[i + 1] < id_s[i];
+  const bool sorted = !__syncthreads_or(unsorted);
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     double leaf;
     if (vals) {
@@ -135,24 +140,28 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, doubl
       leaf = pow((double)p, alpha);
     }
     bool last = true;
-    for (int j = i + 1; j < n; ++j)
-      if (id_s[j] == id_s[i]) {
-        last = false;
-        break;
-      }
+    if (sorted) {
+      last = i + 1 == n || id_s[i + 1] != id_s[i];
+    } else {
+      for (int j = i + 1; j < n; ++j)
+        if (id_s[j] == id_s[i]) {
+          last = false;
+          break;
+        }
+    }
     if (last) {
       sum_tree[cap + id_s[i]] = leaf;
       min_tree[cap + id_s[i]] = leaf;
     }
   }
-  if (max_priority) {
+  if (max_priority) {  // max is order-independent: tree reduction
     maxp_s[threadIdx.x] = my_max;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      double m = max_priority[0];
-      for (int t = 0; t < (int)blockDim.x; ++t) m = fmax(m, maxp_s[t]);
-      max_priority[0] = m;
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) maxp_s[threadIdx.x] = fmax(maxp_s[threadIdx.x], maxp_s[threadIdx.x + w]);
+      __syncthreads();
     }
+    if (threadIdx.x == 0) max_priority[0] = fmax(max_priority[0], maxp_s[0]);
   }
   __syncthreads();
   __threadfence_block();
