@@ -276,6 +276,76 @@ __device__ inline void chain_terms(const SysDevice& sd, const double* q, const d
 }
 
 // In-place Cholesky of SPD M (NJ x NJ); returns false if not positive definite.
+// The two halves of chain_terms with fewer live values (the rollout runs them on different waves):
+// nle(q, v) by RNEA, M(q) by CRBA. Same operation order as chain_terms, so results are identical.
+template <int NJ>
+__device__ inline void chain_nle(const SysDevice& sd, const double* q, const double* v, double* h) {
+  SE3 X[NJ];
+  SV f[NJ];
+  const SV gacc{v3(-sd.p.gravity[0], -sd.p.gravity[1], -sd.p.gravity[2]), v3(0, 0, 0)};
+  SV vp{v3(0, 0, 0), v3(0, 0, 0)}, ap = gacc;
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    X[i] = joint_placement(j, q[i]);
+    const SV S = joint_S(j);
+    SV vi = act_motion_inv(X[i], vp);
+    const SV Sq{v[i] * S.l, v[i] * S.a};
+    vi.l = vi.l + Sq.l;
+    vi.a = vi.a + Sq.a;
+    SV ai = act_motion_inv(X[i], ap);
+    const SV c = cross_motion(vi, Sq);
+    ai.l = ai.l + c.l;
+    ai.a = ai.a + c.a;
+    const Inertia I = j.inertia();
+    const SV Iv = inertia_mul(I, vi);
+    const SV Ia = inertia_mul(I, ai);
+    const SV vf = cross_force(vi, Iv);
+    f[i].l = Ia.l + vf.l;
+    f[i].a = Ia.a + vf.a;
+    vp = vi;
+    ap = ai;
+  }
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    h[i] = sdot(joint_S(j), f[i]);
+    if (i > 0) {
+      const SV fp = act_force(X[i], f[i]);
+      f[i - 1].l = f[i - 1].l + fp.l;
+      f[i - 1].a = f[i - 1].a + fp.a;
+    }
+  }
+}
+
+template <int NJ>
+__device__ inline void chain_mass(const SysDevice& sd, const double* q, double* M) {
+  SE3 X[NJ];
+  Inertia Ic[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    X[i] = joint_placement(j, q[i]);
+    Ic[i] = j.inertia();
+  }
+#pragma unroll
+  for (int i = NJ - 1; i > 0; --i) add_inertia(Ic[i - 1], act_inertia(X[i], Ic[i]));
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    SV F = inertia_mul(Ic[i], joint_S(j));
+    M[i * NJ + i] = sdot(joint_S(j), F);
+#pragma unroll
+    for (int k = i; k > 0; --k) {
+      F = act_force(X[k], F);
+      JointView jp{sd.joints + (k - 1) * CACTO_JOINT_COLS};
+      const double mij = sdot(joint_S(jp), F);
+      M[i * NJ + (k - 1)] = mij;
+      M[(k - 1) * NJ + i] = mij;
+    }
+  }
+}
+
 template <int NJ>
 __device__ inline bool cholesky(double* L) {
   bool ok = true;
@@ -316,6 +386,26 @@ __device__ inline void chol_solve(const double* L, double* x) {
 }
 
 // EE frame translation (forward kinematics to the EE parent joint, then the fixed placement).
+// s' from (s, a) given M (Cholesky-factored in place) and h: explicit Euler, float64 path.
+template <int NJ>
+__device__ inline bool chain_step(const SysDevice& sd, const double* s, const double* a, double* M, const double* h,
+                                  double* out) {
+  const double dt = sd.p.dt;
+  double dv[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) dv[i] = a[i] - h[i];
+  const bool ok = cholesky<NJ>(M);
+  chol_solve<NJ>(M, dv);
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    const double v = s[NJ + i];
+    out[i] = s[i] + v * dt;
+    out[NJ + i] = v + dv[i] * dt;
+  }
+  out[2 * NJ] = s[2 * NJ] + dt;
+  return ok;
+}
+
 template <int NJ>
 __device__ inline V3 chain_ee(const SysDevice& sd, const double* q) {
   M3 oR;
@@ -506,12 +596,18 @@ __device__ __forceinline__ double ell_cost(const cacto_sys_params& p, double x, 
   return log(exp(p.alpha * -(e - 1.0)) + 1.0) / p.alpha;
 }
 
-// bound_control_cost (environment.py:158-163), float64
+// One term of bound_control_cost: a^2 + w_b*(a/u_max)^10; x^10 by squaring (within a few ulp of pow).
+__device__ __forceinline__ double bound_term(const cacto_sys_params& p, double a, int i) {
+  const double x = a / p.u_max[i];
+  const double x2 = x * x, x4 = x2 * x2, x8 = x4 * x4;
+  return a * a + p.w_b * (x8 * x2);
+}
+// bound_control_cost (environment.py:158-163), float64: u = 0; u += term_i in action order
 template <int NA>
 __device__ inline double bound_control_cost(const cacto_sys_params& p, const double* a) {
   double u = 0.0;
 #pragma unroll
-  for (int i = 0; i < NA; ++i) u += a[i] * a[i] + p.w_b * pow(a[i] / p.u_max[i], 10.0);
+  for (int i = 0; i < NA; ++i) u += bound_term(p, a[i], i);
   return u;
 }
 

@@ -2,6 +2,18 @@
 // persistent rollout kernel (K18: actor MFMA tile + float64 dynamics per step, T steps in-kernel).
 #include "net_common.h"
 
+#ifdef CACTO_STAMPS
+__device__ unsigned long long g_rstamps[8];
+#define RSTAMP(k)                                                                   \
+  do {                                                                              \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && t == 20) g_rstamps[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define RSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 namespace cacto {
 
 // ---------------------------------------------------------------- packing
@@ -245,8 +257,9 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   __shared__ float4 red[4 * 64];
   __shared__ float st[16 * 16];
   __shared__ float A[16 * na];
-  __shared__ double sS[16 * ns], sEE[16 * 3], terms[16 * 6];
+  __shared__ double sS[2 * 16 * ns], sEE[2 * 16 * 3], terms[16 * 6], uterm[16 * 8];
   __shared__ double cpv[NJ == -2 ? 16 * 30 : 1];  // car_park obstacle pair costs
+  __shared__ double MS[NJ > 0 ? 16 * NJ * NJ : 1], hS[NJ > 0 ? 16 * NJ : 1];  // chain M(q), nle(q, v)
   __shared__ int sb[16], sn_[16], salive[16];
   __shared__ int tmax;
   __shared__ ActorLds WL;
@@ -262,6 +275,8 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   const bool want_R = Rtraj != nullptr, want_EE = EEtraj != nullptr || want_R;
   // planar / manipulator rewards are split over waves 1-3 (terms of EE(s)); others whole on wave 1
   const bool split_R = p.reward_kind == CACTO_REW_PLANAR || p.reward_kind == CACTO_REW_MANIPULATOR;
+  // chains with configuration-dependent M: RNEA (wave 0) and CRBA (wave 3) run concurrently
+  const bool split_dyn = NJ > 0 && !p.const_dyn;
   ActorRegs R;
   if (use_actor) load_actor_regs(N, na, L, R, WL);
   if (L.tid == 0) tmax = 0;
@@ -302,86 +317,141 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   __syncthreads();
   const int steps = tmax;
   for (int t = 0; t < steps; ++t) {
+    RSTAMP(0);
     if (use_actor) {
       actor_forward_regs(R, WL, na, X0, H1, H2, red, A, L);
       __syncthreads();
     }
-    const bool active = ep_lane && salive[c] && t < sn_[c];
+    RSTAMP(1);
+    // state and EE are double-buffered: step t reads buffer t&1 and writes the other one
+    const int cur = t & 1;
+    const double* Sc = sS + cur * 16 * ns;
+    double* Sn = sS + (cur ^ 1) * 16 * ns;
+    const double* Ec = sEE + cur * 48;
+    double* En = sEE + (cur ^ 1) * 48;
+    const bool act_c = s0 + c < B && salive[c] && t < sn_[c];  // episode c = lane & 15 of any lane group
+    const bool active = act_c && L.lane < 16;
     double sn[ns];
-    // ---- E1
-    if (active) {
-      double a[na];
+    // ---- E1: wave 0 integrates s_t -> s_{t+1}; waves 1-3 evaluate the reward terms of (s_t, a_t)
+    if (L.wave == 0) {
+      if (active) {
+        double s[ns], a[na];
 #pragma unroll
-      for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)A[c * na + i] : 0.0;
-      if (L.wave == 0) {
-        double s[ns];
+        for (int i = 0; i < ns; ++i) s[i] = Sc[c * ns + i];
 #pragma unroll
-        for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
-        if (NJ > 0 && p.const_dyn)
-          env_simulate_const<NJ>(sd, cd, s, a, sn);
-        else
-          env_simulate<NJ>(sd, s, a, false, sn);
-      } else if (want_R && !split_R) {
-        // UR5: the whole Env.step reward of (s, a) on wave 1 (environment.py:780-805); car_park's
-        // obstacle pairs are spread over waves 1-3 below
-        if (NJ != -2 && L.wave == 1) {
-          double s[ns];
+        for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)A[c * na + i] : 0.0;
+        if (split_dyn) {
+          // chains: nle(q, v) here by RNEA, M(q) on wave 3 by CRBA, Cholesky step after the barrier
+          if constexpr (NJ > 0) {
+            double h[NJ];
+            chain_nle<NJ>(sd, s, s + NJ, h);
 #pragma unroll
-          for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
-          terms[c * 6 + 0] = env_reward<NJ>(sd, w, s, a, false);
-        }
-      } else if (want_R) {
-        const double x = sEE[c * 3 + 0], y = sEE[c * 3 + 1];
-        const double* o = p.obs;
-        if (L.wave == 1) {
-          terms[c * 6 + 0] = ell_cost(p, x, y, o[0], o[1], o[6], o[7]);
-          terms[c * 6 + 1] = ell_cost(p, x, y, o[2], o[3], o[8], o[9]);
-        } else if (L.wave == 2) {
-          terms[c * 6 + 2] = ell_cost(p, x, y, o[4], o[5], o[10], o[11]);
-          terms[c * 6 + 3] = peak_cost(p, x, y);
-        } else {
-          terms[c * 6 + 4] = bound_control_cost<na>(p, a);
-          double vel = 0.0;
-          if (NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR && w[2] != 0.0) {
-#pragma unroll
-            for (int k = 0; k < (NJ > 0 ? NJ : 1); ++k) vel += sS[c * ns + NJ + k] * sS[c * ns + NJ + k];
+            for (int i = 0; i < NJ; ++i) hS[c * NJ + i] = h[i];
           }
-          terms[c * 6 + 5] = vel;
+        } else {
+          if (NJ > 0 && p.const_dyn)
+            env_simulate_const<NJ>(sd, cd, s, a, sn);
+          else
+            env_simulate<NJ>(sd, s, a, false, sn);
+#pragma unroll
+          for (int i = 0; i < ns; ++i) {
+            Sn[c * ns + i] = sn[i];
+            st[c * 16 + i] = (float)sn[i];
+          }
         }
       }
+    } else if (split_dyn && L.wave == 3 && active) {
+      if constexpr (NJ > 0) {
+        double M[NJ * NJ];
+        chain_mass<NJ>(sd, Sc + c * ns, M);
+#pragma unroll
+        for (int k = 0; k < NJ * NJ; ++k) MS[c * NJ * NJ + k] = M[k];
+      }
     }
-    if constexpr (NJ == -2) {
-      // CarPark obstacle cost (environment.py:619-624): 3 x n_check smooth-box terms of EE(s), theta,
-      // over 12 lane groups (waves 1-3 x 4 groups of the 16 episode lanes)
-      if (want_R && L.wave >= 1) {
-        const bool act_c = s0 + c < B && salive[c] && t < sn_[c];
-        if (act_c) {
-          const int grp = (L.wave - 1) * 4 + (L.lane >> 4);
-          const double th = sS[c * ns + 2], ct = cos(th), stt = sin(th);
-          for (int pr = grp; pr < 3 * p.n_check; pr += 12)
-            cpv[c * 30 + pr] = carpark_pair_cost(p, sEE[c * 3 + 0], sEE[c * 3 + 1], ct, stt, pr);
+    if (L.wave != 0 && want_R && act_c) {
+      const int grp = L.lane >> 4;
+      const double x = Ec[c * 3 + 0], y = Ec[c * 3 + 1];
+      const double* o = p.obs;
+      if (split_R) {
+        // the three ellipses share one code path: one lane group each (environment.py:337-339)
+        if (L.wave == 1) {
+          if (grp < 3) terms[c * 6 + grp] = ell_cost(p, x, y, o[2 * grp], o[2 * grp + 1], o[6 + 2 * grp], o[7 + 2 * grp]);
+        } else if (L.wave == 2) {
+          if (grp == 0) terms[c * 6 + 3] = peak_cost(p, x, y);
+        } else {
+          // wave 3: one control-bound term per lane group (summed in action order in E2), velocity cost
+          for (int i = grp; i < na; i += 4) uterm[c * 8 + i] = bound_term(p, use_actor ? (double)A[c * na + i] : 0.0, i);
+          if (grp == 0) {
+            double vel = 0.0;
+            if (NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR && w[2] != 0.0) {
+#pragma unroll
+              for (int k = 0; k < (NJ > 0 ? NJ : 1); ++k) vel += Sc[c * ns + NJ + k] * Sc[c * ns + NJ + k];
+            }
+            terms[c * 6 + 5] = vel;
+          }
         }
+      } else if constexpr (NJ == -2) {
+        // CarPark obstacle cost (environment.py:619-624): 3 x n_check smooth-box terms of EE(s),
+        // theta, over 12 lane groups (waves 1-3 x 4 groups of the 16 episode lanes)
+        const int g12 = (L.wave - 1) * 4 + grp;
+        const double th = Sc[c * ns + 2], ct = cos(th), stt = sin(th);
+        for (int pr = g12; pr < 3 * p.n_check; pr += 12) cpv[c * 30 + pr] = carpark_pair_cost(p, x, y, ct, stt, pr);
+      } else if (L.wave == 1 && grp == 0) {
+        // UR5: the whole Env.step reward of (s, a) (environment.py:780-805)
+        double s[ns], a[na];
+#pragma unroll
+        for (int i = 0; i < ns; ++i) s[i] = Sc[c * ns + i];
+#pragma unroll
+        for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)A[c * na + i] : 0.0;
+        terms[c * 6 + 0] = env_reward<NJ>(sd, w, s, a, false);
       }
     }
     __syncthreads();
-    // ---- E2
-    if (active) {
-      const int b = sb[c];
-      if (L.wave == 0) {
+    if (split_dyn) {
+      if constexpr (NJ > 0) {
+        if (L.wave == 0 && active) {
+          double s[ns], a[na], M[NJ * NJ], h[NJ];
+#pragma unroll
+          for (int i = 0; i < ns; ++i) s[i] = Sc[c * ns + i];
+#pragma unroll
+          for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)A[c * na + i] : 0.0;
+#pragma unroll
+          for (int k = 0; k < NJ * NJ; ++k) M[k] = MS[c * NJ * NJ + k];
+#pragma unroll
+          for (int i = 0; i < NJ; ++i) h[i] = hS[c * NJ + i];
+          chain_step<NJ>(sd, s, a, M, h, sn);
+#pragma unroll
+          for (int i = 0; i < ns; ++i) {
+            Sn[c * ns + i] = sn[i];
+            st[c * 16 + i] = (float)sn[i];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    RSTAMP(2);
+    // ---- E2: wave 0 combines the reward (reference order) and writes S/A/R; wave 1 computes
+    //          EE(s_{t+1}); wave 2 normalises s_{t+1} into the next actor input tile.
+    if (L.wave == 0) {
+      if (active) {
+        const int b = sb[c];
         if (want_R) {
-          const bool has_vel = NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR;
           double r;
           if constexpr (NJ == -2) {
             double a[na], s[ns];
 #pragma unroll
             for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)A[c * na + i] : 0.0;
 #pragma unroll
-            for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
-            r = carpark_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], s, a, carpark_sum(p, cpv + c * 30));
+            for (int i = 0; i < ns; ++i) s[i] = Sc[c * ns + i];
+            r = carpark_reward(p, w, Ec[c * 3 + 0], Ec[c * 3 + 1], s, a, carpark_sum(p, cpv + c * 30));
           } else {
-            r = split_R ? combine_reward(p, w, sEE[c * 3 + 0], sEE[c * 3 + 1], terms[c * 6 + 3], terms[c * 6 + 5],
-                                         has_vel, terms[c * 6 + 0], terms[c * 6 + 1], terms[c * 6 + 2],
-                                         terms[c * 6 + 4])
+            const bool has_vel = NJ > 0 && p.reward_kind == CACTO_REW_MANIPULATOR;
+            double u_cost = 0.0;
+            if (split_R)
+#pragma unroll
+              for (int i = 0; i < na; ++i) u_cost += uterm[c * 8 + i];
+            r = split_R ? combine_reward(p, w, Ec[c * 3 + 0], Ec[c * 3 + 1], terms[c * 6 + 3], terms[c * 6 + 5],
+                                         has_vel, terms[c * 6 + 0], terms[c * 6 + 1], terms[c * 6 + 2], u_cost)
                         : terms[c * 6 + 0];
           }
           Rtraj[(size_t)b * T + t] = r;
@@ -397,33 +467,27 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         }
         if (bad) salive[c] = 0;  // RL.py:229-231
       }
-    }
-    __syncthreads();
-    if (active && L.wave == 0) {
+    } else if (L.wave == 1) {
+      if (active && want_EE) {
+        double s[ns];
 #pragma unroll
-      for (int i = 0; i < ns; ++i) {
-        sS[c * ns + i] = sn[i];
-        st[c * 16 + i] = (float)sn[i];
+        for (int i = 0; i < ns; ++i) s[i] = Sn[c * ns + i];
+        const V3 e = env_ee<NJ>(sd, s);
+        En[c * 3 + 0] = e.x;
+        En[c * 3 + 1] = e.y;
+        En[c * 3 + 2] = e.z;
+        if (EEtraj) {
+          const int b = sb[c];
+          EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 0] = e.x;
+          EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 1] = e.y;
+          EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 2] = e.z;
+        }
       }
+    } else if (L.wave == 2 && use_actor) {
+      fill_input_tile(p, st, X0, L);
     }
     __syncthreads();
-    if (active && L.wave == 1 && want_EE) {
-      double s[ns];
-#pragma unroll
-      for (int i = 0; i < ns; ++i) s[i] = sS[c * ns + i];
-      const V3 e = env_ee<NJ>(sd, s);
-      sEE[c * 3 + 0] = e.x;
-      sEE[c * 3 + 1] = e.y;
-      sEE[c * 3 + 2] = e.z;
-      if (EEtraj) {
-        const int b = sb[c];
-        EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 0] = e.x;
-        EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 1] = e.y;
-        EEtraj[((size_t)b * (T + 1) + t + 1) * 3 + 2] = e.z;
-      }
-    }
-    if (use_actor && L.wave == 2) fill_input_tile(p, st, X0, L);
-    __syncthreads();
+    RSTAMP(3);
   }
   if (L.wave == 0 && ep_lane && status) {
     const int b = sb[c];
@@ -448,6 +512,14 @@ struct LaunchRollout {
   }
 };
 }  // namespace
+
+#ifdef CACTO_STAMPS
+extern "C" int cacto_debug_rollout_stamps(unsigned long long* out_h) {
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 8));
+  return CACTO_OK;
+}
+#endif
 
 NetView cacto_make_view(const cacto_sys* sys, int net, const float* netbuf) {
   NetView v;

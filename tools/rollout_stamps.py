@@ -1,0 +1,39 @@
+"""Diagnostic: per-phase cycle counts of one k_rollout step (workgroup 0, step 20) from the
+CACTO_STAMPS build. Not part of the product path.
+
+    python -c "from cacto_amd.build import build_variant; build_variant('libcacto_hip_stamps', ['CACTO_STAMPS'])"
+    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/rollout_stamps.py [system]
+"""
+import ctypes
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.argv += [] if len(sys.argv) > 1 else ["double_integrator"]
+
+from cacto_amd import _lib as L  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    system = sys.argv[1]
+    conf, env, rl = bench.make_learner(system)
+    S0, n = bench.initial_states(env, conf, 4096, seed=0)
+    T = int(n.max())
+    inputs = rl.rollout_inputs(S0, n)
+    for _ in range(3):
+        out = rl.rollout_batch(None, None, T, inputs=inputs)
+    torch.cuda.synchronize()
+    st = (ctypes.c_ulonglong * 8)()
+    L.lib().dll.cacto_debug_rollout_stamps(st)
+    t = np.array(st[:4], dtype=np.float64)
+    names = ["actor", "E1 (dynamics | reward terms)", "E2 (reward combine + stores | EE(s') | next input tile)"]
+    print(system, "step cycles %.0f: " % (t[3] - t[0]) + ", ".join("%s %.0f" % (nm, d) for nm, d in zip(names, np.diff(t))))
+
+
+if __name__ == "__main__":
+    main()
