@@ -22,6 +22,7 @@ import os
 import random
 import sys
 import time
+import types
 
 import numpy as np
 import torch
@@ -198,42 +199,73 @@ def rollout_diagnostics(rl, conf, roll, K=5):
     return res
 
 
-def fill_buffer(rl, conf, roll, seed, per=False):
-    """Replay rows from the rollouts (RL_Solve n-step targets, RL.py:145-189, vectorised over
-    episodes; rewards = the rollout rewards, dVdx synthetic N(0,1))."""
-    from cacto_amd.replay_buffer import ReplayBuffer
-    S = roll["out"]["S"].cpu().numpy()
-    Rw = roll["out"]["R"].cpu().numpy()
-    nsteps = roll["nsteps"]
-    ns, nTD = conf.nb_state, conf.nsteps_TD_N
-    gen = np.random.Generator(np.random.PCG64(seed))
-    rows = []
-    for e in range(len(nsteps)):
-        T = int(nsteps[e])
-        r = np.concatenate([Rw[e, :T], [0.0]])
-        c = np.concatenate([[0.0], np.cumsum(r)])
-        i = np.arange(T + 1)
-        fin = np.minimum(i + nTD, T)
-        partial = (c[fin + 1] - c[i]).astype(np.float32).astype(np.float64)
-        done = (fin == T).astype(np.float64)
-        snext = np.zeros((T + 1, ns))
-        m = fin < T
-        snext[m] = S[e, fin[m] + 1]
-        term = np.zeros(T + 1)
-        term[-1] = 1
-        rows.append(np.concatenate([S[e, :T + 1], partial[:, None], snext, gen.standard_normal((T + 1, ns)),
-                                    done[:, None], term[:, None]], axis=1))
-        if sum(len(x) for x in rows) >= conf.REPLAY_SIZE + 8192:
-            break
-    rows = np.concatenate(rows)
-    if per:
-        from cacto_amd.replay_buffer import PrioritizedReplayBuffer
-        buf = PrioritizedReplayBuffer(conf, rl.sys)
-    else:
-        buf = ReplayBuffer(conf, rl.sys)
-    for k in range(0, len(rows), 8192):     # per-batch adds, so the ring wraps and `full` latches
-        buf.add_rows(rows[k:k + 8192])
+def terminal_rewards(env, conf, roll):
+    """rwrd_arr[-1] = env.reward(cost_weights_terminal, s_T) per episode (RL.py:165), on the device."""
+    S, n = roll["out"]["S"], torch.as_tensor(roll["nsteps"].astype(np.int64), device="cuda")
+    s_T = S[torch.arange(S.shape[0], device="cuda"), n]
+    return env.step_batch(s_T, torch.zeros(S.shape[0], conf.nb_action, dtype=torch.float64, device="cuda"),
+                          conf.cost_weights_terminal)[1]
+
+
+def episode_groups(nsteps, max_rows):
+    """Consecutive episode ranges of at most max_rows replay rows each."""
+    groups, lo, rows = [], 0, 0
+    for e, T in enumerate(nsteps):
+        if rows + T + 1 > max_rows:
+            groups.append((lo, e))
+            lo, rows = e, 0
+        rows += int(T) + 1
+    groups.append((lo, len(nsteps)))
+    return groups
+
+
+def fill_buffer(rl, conf, roll, env, seed, per=False):
+    """Replay rows from the rollouts on the device: RL_Solve n-step targets fused with the ring add
+    (cacto_rl_solve_add), rewards = the rollout rewards + terminal reward, dVdx synthetic N(0,1).
+    Episodes go in groups of <= 8192 rows until the ring has wrapped once, so `full` latches."""
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer, ReplayBuffer
+    buf = PrioritizedReplayBuffer(conf, rl.sys) if per else ReplayBuffer(conf, rl.sys)
+    S, R, nsteps = roll["out"]["S"], roll["out"]["R"], roll["nsteps"]
+    R_term = terminal_rewards(env, conf, roll)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(seed)
+    added = 0
+    while added < conf.REPLAY_SIZE + 8192:
+        for lo, hi in episode_groups(nsteps, 8192):
+            dV = torch.randn(hi - lo, S.shape[1], S.shape[2], dtype=torch.float64, device="cuda", generator=gen)
+            buf.add_episodes(S[lo:hi], R[lo:hi], nsteps[lo:hi], R_term=R_term[lo:hi], dVdx=dV)
+            added += int((nsteps[lo:hi] + 1).sum())
+            if added >= conf.REPLAY_SIZE + 8192:
+                break
     return buf
+
+
+def episode_to_buffer_phase(rl, conf, roll, env, K):
+    """The whole rollout batch through cacto_rl_solve_add into one ring that holds it (RL_Solve +
+    buffer.add for every episode of a create_TO_init batch). Returns rows/s and the kernel's
+    algorithmic bandwidth: per row it reads s and dVdx (8*ns each) and r (8), writes 8*(3ns+3)."""
+    from cacto_amd.replay_buffer import ReplayBuffer
+    nsteps = roll["nsteps"]
+    rows = int((nsteps + 1).sum())
+    c = types.SimpleNamespace(**{k: getattr(conf, k) for k in dir(conf) if not k.startswith("__")})
+    c.REPLAY_SIZE = rows
+    buf = ReplayBuffer(c, rl.sys)
+    S, R = roll["out"]["S"], roll["out"]["R"]
+    R_term = terminal_rewards(env, conf, roll)
+    dV = torch.randn(S.shape, dtype=torch.float64, device="cuda")
+    buf.add_episodes(S, R, nsteps, R_term=R_term, dVdx=dV)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(K):
+        buf.add_episodes(S, R, nsteps, R_term=R_term, dVdx=dV)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / K
+    ns = conf.nb_state
+    row_bytes = 8 * (2 * ns + 1) + 8 * (3 * ns + 3)
+    return dict(rows_per_s=rows / (ms * 1e-3), rows_per_call=rows, ms_per_call=ms, episodes=len(nsteps),
+                algorithmic_bytes_per_row=row_bytes, achieved_GBps=rows * row_bytes / (ms * 1e-3) / 1e9)
 
 
 def update_phase(rl, buf, B, K, W, world, seed):
@@ -298,7 +330,7 @@ def extra_system(name, args, world, rank):
     if cfg["per"]:
         conf.prioritized_replay_alpha = 0.6
     r = rollout_phase(rl, conf, env, cfg["R"], args.steps, args.warmup, world, rank)
-    buf = fill_buffer(rl, conf, r, seed=rank, per=cfg["per"])
+    buf = fill_buffer(rl, conf, r, env, seed=rank, per=cfg["per"])
     ups = {}
     for B in cfg["batches"]:
         if cfg["per"]:
@@ -369,7 +401,8 @@ def main():
     value = roll["total_steps"] / roll["wall"]
     achieved = roll["steps_per_call"] * fa_flops(ns, na) / (roll["kernel_ms"] * 1e-3)
     diag = None if args.no_diagnostics else rollout_diagnostics(rl, conf, roll)
-    buf = fill_buffer(rl, conf, roll, seed=rank)
+    buf = fill_buffer(rl, conf, roll, env, seed=rank)
+    e2b = episode_to_buffer_phase(rl, conf, roll, env, 5)
     updates = {}
     for B in [int(b) for b in args.batches.split(",") if b]:
         K = args.update_steps
@@ -412,6 +445,7 @@ def main():
                          "kernel_ms": roll["kernel_ms"], "flop_per_env_step": fa_flops(ns, na),
                          "env_steps_per_launch": roll["steps_per_call"]},
             "critic_updates": updates,
+            "episode_to_buffer": e2b,
             "rollout_diagnostics": diag,
             "cpu_baseline": cpu,
             "extra_systems": extra,

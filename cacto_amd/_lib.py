@@ -75,6 +75,8 @@ _SIGS = {
                                vp, sz, vp]),
     "cacto_rollout": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
     "cacto_buffer_add": (C.c_int, [vp, vp, i64, i64, vp, i64, vp]),
+    "cacto_rl_solve_add": (C.c_int, [vp, vp, i64, vp, i64, vp, vp, vp, C.c_int, C.c_int, i64, C.c_int, C.c_int, vp,
+                                     i64, i64, vp, vp]),
     "cacto_buffer_gather": (C.c_int, [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp]),
     "cacto_per_init": (C.c_int, [vp, vp, i64, vp]),
     "cacto_per_set_range": (C.c_int, [vp, vp, i64, i64, i64, i64, dbl, vp]),

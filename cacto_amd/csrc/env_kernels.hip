@@ -107,6 +107,56 @@ __global__ void k_buffer_add(double* __restrict__ storage, int64_t capacity, int
   }
 }
 
+// RL_AC.RL_Solve (RL.py:145-189) for a batch of episodes, fused with the ring write of
+// ReplayBuffer.add (replay_buffer.py:25-36) that main.py:240 applies to its output. One workgroup
+// per episode. Python's sum() over a float64 slice adds left to right starting from integer 0, so
+// acc = 0.0 followed by the same additions reproduces it bit for bit (0 + -0.0 == +0.0 in both);
+// the total reward-to-go continues the partial sum's additions before either is rounded to f32.
+__global__ void k_rl_solve_add(const double* __restrict__ S, int64_t ldS, const double* __restrict__ R, int64_t ldR,
+                               const double* __restrict__ R_term, const double* __restrict__ dVdx,
+                               const int64_t* __restrict__ row_off, int ns, int max_T, int nTD, int mc,
+                               double* __restrict__ storage, int64_t capacity, int64_t next_idx,
+                               double* __restrict__ total_out) {
+  extern __shared__ double sm[];
+  double* r = sm;                  // rwrd_arr of this episode, [Te+1]
+  double* part = sm + max_T + 1;   // partial_reward_to_go_arr, [Te+1]
+  const int e = blockIdx.x;
+  const int64_t off = row_off[e];
+  const int Te = (int)(row_off[e + 1] - off) - 1;  // NSTEPS_SH of this episode
+  if (Te < 0 || Te > max_T) return;                // violates the documented precondition: write nothing
+  for (int t = threadIdx.x; t <= Te; t += blockDim.x)
+    r[t] = (t == Te && R_term) ? R_term[e] : R[e * ldR + t];
+  __syncthreads();
+  for (int i = threadIdx.x; i <= Te; i += blockDim.x) {
+    const int fin = mc ? Te : min(i + nTD, Te);
+    double acc = 0.0;
+    for (int t = i; t <= fin; ++t) acc += r[t];
+    part[i] = (double)(float)acc;
+    if (total_out) {
+      for (int t = fin + 1; t <= Te; ++t) acc += r[t];
+      total_out[e * ldS + i] = (double)(float)acc;
+    }
+  }
+  __syncthreads();
+  const double* Se = S + e * ldS * ns;
+  const double* De = dVdx ? dVdx + e * ldS * ns : nullptr;
+  const int cols = 3 * ns + 3;
+  const int64_t n = (int64_t)(Te + 1) * cols;
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const int i = (int)(k / cols), c = (int)(k - (int64_t)i * cols);
+    const int fin = mc ? Te : min(i + nTD, Te);
+    const bool done = mc || fin == Te;
+    double v;
+    if (c < ns) v = Se[i * ns + c];
+    else if (c == ns) v = part[i];
+    else if (c <= 2 * ns) v = done ? 0.0 : Se[(fin + 1) * ns + (c - ns - 1)];
+    else if (c <= 3 * ns) v = De ? De[i * ns + (c - 2 * ns - 1)] : 0.0;
+    else if (c == 3 * ns + 1) v = done ? 1.0 : 0.0;
+    else v = i == Te ? 1.0 : 0.0;
+    storage[((next_idx + off + i) % capacity) * cols + c] = v;
+  }
+}
+
 __global__ void k_buffer_gather(const double* __restrict__ storage, int ns, const int32_t* __restrict__ idx, int B,
                                 float* __restrict__ S, float* __restrict__ R, float* __restrict__ Sn,
                                 float* __restrict__ dVdx, float* __restrict__ d, double* __restrict__ term) {
@@ -197,6 +247,26 @@ extern "C" int cacto_buffer_add(const cacto_sys* sys, double* storage_d, int64_t
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(k_buffer_add, dim3(grid), dim3(256), 0, as_stream(stream), storage_d, capacity, next_idx, cols,
                      rows_d, n);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_rl_solve_add(const cacto_sys* sys, const double* S_traj_d, int64_t ldS, const double* R_d,
+                                  int64_t ldR, const double* R_term_d, const double* dVdx_d, const int64_t* row_off_d,
+                                  int n_ep, int max_T, int64_t total_rows, int nsteps_td, int mc, double* storage_d,
+                                  int64_t capacity, int64_t next_idx, double* total_d, void* stream) {
+  CACTO_REQUIRE(sys && S_traj_d && R_d && row_off_d && storage_d && n_ep >= 0 && max_T >= 0 && nsteps_td >= 0 &&
+                    capacity > 0 && next_idx >= 0 && next_idx < capacity && total_rows >= 0,
+                "cacto_rl_solve_add: bad arguments");
+  CACTO_REQUIRE(ldS >= max_T + 1 && ldR >= (R_term_d ? max_T : max_T + 1),
+                "cacto_rl_solve_add: trajectory strides shorter than max_T");
+  CACTO_REQUIRE(max_T + 1 <= 4096, "cacto_rl_solve_add: episodes longer than 4095 steps");
+  CACTO_REQUIRE(total_rows <= capacity, "cacto_rl_solve_add: more rows than capacity");
+  if (n_ep == 0 || total_rows == 0) return CACTO_OK;
+  const size_t smem = 2 * (size_t)(max_T + 1) * sizeof(double);
+  hipLaunchKernelGGL(k_rl_solve_add, dim3(n_ep), dim3(256), smem, as_stream(stream), S_traj_d, ldS, R_d, ldR,
+                     R_term_d, dVdx_d, row_off_d, sys->host.p.nb_state, max_T, nsteps_td, mc, storage_d, capacity,
+                     next_idx, total_d);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }

@@ -44,9 +44,58 @@ class ReplayBuffer:
             raise ValueError("cannot add more rows than REPLAY_SIZE at once")
         L.lib().call("cacto_buffer_add", self.sys.handle, dptr(self.storage), self.N, self.next_idx, dptr(rows), n,
                      stream())
+        self._advance(n)
+
+    def _advance(self, n):
+        start = self.next_idx
         if n + self.next_idx > self.N:
             self.full = 1
         self.next_idx = (self.next_idx + n) % self.N
+        self._rows_added(start, n)
+
+    def _rows_added(self, start, n):
+        pass
+
+    def _row_offsets(self, nsteps):
+        """Exclusive prefix sum of the episode row counts on the device; the last batch's copy is
+        reused when the lengths repeat (one create_TO_init batch is added many times in a bench)."""
+        key = nsteps.tobytes()
+        if getattr(self, "_off_key", None) != key:
+            off = np.zeros(len(nsteps) + 1, dtype=np.int64)
+            np.cumsum(nsteps + 1, out=off[1:])
+            self._off_key, self._off = key, (torch.as_tensor(off, device=DEVICE), int(off[-1]))
+        return self._off
+
+    def add_episodes(self, S_traj, rewards, nsteps, R_term=None, dVdx=None, want_total=False):
+        """RL_AC.RL_Solve (RL.py:145-189) for a batch of episodes, with the rows of each episode
+        added in order as main.py:240 adds them, all on the device (cacto_rl_solve_add).
+
+        S_traj [E, ldS, ns] f64 device (s_0..s_T per episode, e.g. cacto_rollout's S_traj);
+        rewards [E, ldR] f64 device: r_0..r_T, or r_0..r_{T-1} with R_term [E] giving r_T;
+        nsteps: host ints (NSTEPS_SH per episode); dVdx [E, ldS, ns] f64 device or None (zeros).
+        Returns total_reward_to_go [E, ldS] (device) when want_total, else None."""
+        nsteps = np.asarray(nsteps, dtype=np.int64)
+        E = len(nsteps)
+        if E == 0:
+            return None
+        off_d, n = self._row_offsets(nsteps)
+        if n > self.N:
+            raise ValueError("cannot add more rows than REPLAY_SIZE at once")
+        f64 = lambda t: t.to(device=DEVICE, dtype=torch.float64).contiguous()
+        S_traj, rewards = f64(S_traj), f64(rewards)
+        if S_traj.dim() != 3 or S_traj.shape[0] != E or S_traj.shape[2] != self.ns or rewards.shape[0] != E:
+            raise ValueError("add_episodes: S_traj must be [E, T+1, ns] and rewards [E, *]")
+        R_term = None if R_term is None else f64(R_term)
+        dVdx = None if dVdx is None else f64(dVdx)
+        if dVdx is not None and dVdx.shape != S_traj.shape:
+            raise ValueError("add_episodes: dVdx must have the shape of S_traj")
+        total = torch.empty(E, S_traj.shape[1], dtype=torch.float64, device=DEVICE) if want_total else None
+        L.lib().call("cacto_rl_solve_add", self.sys.handle, dptr(S_traj), S_traj.shape[1], dptr(rewards),
+                     rewards.shape[1], dptr(R_term), dptr(dVdx), dptr(off_d), E, int(nsteps.max()), n,
+                     int(getattr(self.conf, "nsteps_TD_N", 0)), int(bool(self.conf.MC)), dptr(self.storage), self.N,
+                     self.next_idx, dptr(total), stream())
+        self._advance(n)
+        return total
 
     def add(self, obses_t, rewards, obses_t1, dVdxs, dones, terms):
         """replay_buffer.py:25-36."""
@@ -103,10 +152,7 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         self.fresh = float(conf.fresh_factor)
         self.random = py_random or random  # replay_buffer.py:150 uses the global `random`
 
-    def add_rows(self, rows):
-        start = self.next_idx
-        n = len(rows)
-        super().add_rows(rows)
+    def _rows_added(self, start, n):
         # leaves = max_priority ** alpha (replay_buffer.py:133-135); max_priority read on the host
         leaf = float(self.max_priority.item()) ** self.alpha
         L.lib().call("cacto_per_set_range", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.N, start, n,

@@ -21,6 +21,8 @@
  *   cacto_update           RL_AC.update + update_target (one learn_and_update iteration, RL.py:122-137)
  *   cacto_buffer_gather    ReplayBuffer.sample row gather replay_buffer.py:47-61
  *   cacto_buffer_add       ReplayBuffer.add ring write replay_buffer.py:25-36
+ *   cacto_rl_solve_add     RL_AC.RL_Solve n-step targets RL.py:145-189 fused with the
+ *                          buffer.add of its output (main.py:240)
  *   cacto_per_*            PrioritizedReplayBuffer + segment trees replay_buffer.py:87-218,
  *                          segment_tree.py:4-145
  *
@@ -231,6 +233,23 @@ int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const doubl
 /* rows_d [n, 3ns+3] f64 written at ring position next_idx (wraps modulo capacity). */
 int cacto_buffer_add(const cacto_sys* sys, double* storage_d, int64_t capacity, int64_t next_idx,
                      const double* rows_d, int64_t n, void* stream);
+
+/* RL_Solve (RL.py:145-189) for n_ep episodes, rows written straight into the ring as
+ * buffer.add(state_arr, partial_reward_to_go_arr, state_next_rollout_arr, dVdx, done_arr, term_arr)
+ * does after it (main.py:240). Episode e has Te = row_off_d[e+1] - row_off_d[e] - 1 steps
+ * (NSTEPS_SH), 0 <= Te <= max_T, and its Te+1 rows go to ring slots
+ * (next_idx + row_off_d[e] + i) % capacity; total_rows = row_off_d[n_ep] <= capacity.
+ *   S_traj_d [n_ep, ldS, ns] f64: s_0..s_Te (ldS >= max_T+1; the cacto_rollout layout with T = max_T)
+ *   R_d [n_ep, ldR] f64: rwrd_arr r_0..r_Te, or r_0..r_{Te-1} when R_term_d [n_ep] (f64) gives r_Te
+ *     (env_RL: RL.py:160-165); pass -TO_step_cost for env_RL = 0 (RL.py:167)
+ *   dVdx_d [n_ep, ldS, ns] f64 or NULL (zeros)
+ *   nsteps_td = conf.nsteps_TD_N, mc = conf.MC
+ *   total_d [n_ep, ldS] f64 or NULL: total_reward_to_go_arr.
+ * Partial/total reward-to-go are Python's left-to-right sums rounded to float32, bit-exact. */
+int cacto_rl_solve_add(const cacto_sys* sys, const double* S_traj_d, int64_t ldS, const double* R_d,
+                       int64_t ldR, const double* R_term_d, const double* dVdx_d, const int64_t* row_off_d,
+                       int n_ep, int max_T, int64_t total_rows, int nsteps_td, int mc, double* storage_d,
+                       int64_t capacity, int64_t next_idx, double* total_d, void* stream);
 
 /* replay_buffer.py:47-61: S, R, S_next, dVdx, d as float32, term float64; any may be NULL. */
 int cacto_buffer_gather(const cacto_sys* sys, const double* storage_d, const int32_t* idx_d, int B,

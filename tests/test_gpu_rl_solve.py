@@ -1,0 +1,125 @@
+"""GPU parity of the fused RL_Solve + ring add (cacto_rl_solve_add, RL.py:145-189 + main.py:240).
+
+Bit-exact: the partial / total reward-to-go are Python's left-to-right float64 sums rounded to
+float32, and every other column is a copy. Checked against the reference's own RL_Solve outputs
+(tests/golden rls_*) and, for ragged batches with ring wrap-around, MC and a separate terminal
+reward, against oracle.buffer.rl_solve episode by episode.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import buffer as obuf
+from cacto_amd.confs import load_conf
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _buffer(system, N, nTD, MC=0):
+    from cacto_amd.replay_buffer import ReplayBuffer
+    from cacto_amd.system import System
+    conf = load_conf(system)
+
+    class C:
+        pass
+    c = C()
+    c.__dict__.update({k: getattr(conf, k) for k in dir(conf) if not k.startswith("__")})
+    c.REPLAY_SIZE, c.nsteps_TD_N, c.MC = N, nTD, MC
+    return ReplayBuffer(c, System(conf)), conf
+
+
+def _expected_rows(states, rwrd, dVdx, nTD, MC):
+    p, t, sn, d, term = obuf.rl_solve(states, -rwrd, nTD, MC=bool(MC))
+    rows = np.concatenate([states, p[:, None], sn, dVdx, d[:, None], term[:, None]], axis=1)
+    return rows, t
+
+
+def test_rl_solve_add_reference_vectors(ref_vectors):
+    S = ref_vectors["rls_states"]
+    cost = ref_vectors["rls_cost"]
+    T = len(cost) - 1
+    rb, _ = _buffer("single_integrator", 64, 25)
+    assert S.shape[1] == rb.ns
+    dev = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+    total = rb.add_episodes(dev(S[None]), dev(-cost[None]), [T], want_total=True)
+    got = rb.storage.cpu().numpy()[:T + 1]
+    ns = rb.ns
+    np.testing.assert_array_equal(got[:, :ns], S)
+    np.testing.assert_array_equal(got[:, ns], ref_vectors["rls_partial"])
+    np.testing.assert_array_equal(got[:, ns + 1:2 * ns + 1], ref_vectors["rls_snext"])
+    np.testing.assert_array_equal(got[:, 2 * ns + 1:3 * ns + 1], 0.0)
+    np.testing.assert_array_equal(got[:, 3 * ns + 1], ref_vectors["rls_done"])
+    np.testing.assert_array_equal(got[:, 3 * ns + 2], ref_vectors["rls_term"])
+    np.testing.assert_array_equal(total.cpu().numpy()[0], ref_vectors["rls_total"])
+    assert (rb.next_idx, rb.full) == (T + 1, 0)
+
+
+@pytest.mark.parametrize("system,nTD,MC,split_term", [("double_integrator", 7, 0, False),
+                                                      ("car_park", 3, 0, True),
+                                                      ("manipulator", 40, 0, False),
+                                                      ("single_integrator", 5, 1, True)])
+def test_rl_solve_add_batch_matches_oracle(system, nTD, MC, split_term):
+    rng = np.random.default_rng(11)
+    E, Tmax, N = 37, 50, 4096
+    rb, conf = _buffer(system, N, nTD, MC)
+    ns = rb.ns
+    nsteps = rng.integers(0, Tmax + 1, size=E)
+    nsteps[:3] = [0, Tmax, 1]
+    S = rng.normal(size=(E, Tmax + 1, ns))
+    # rewards over many binades so the summation order shows in the float32 rounding
+    r = rng.normal(size=(E, Tmax + 1)) * 10.0 ** rng.integers(-6, 4, size=(E, Tmax + 1))
+    r[0, 0] = -0.0
+    dV = rng.normal(size=(E, Tmax + 1, ns))
+    start = N - 300                                   # the batch wraps past the end of the ring
+    rb.next_idx = start
+    dev = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+    if split_term:
+        R_term = np.array([r[e, nsteps[e]] for e in range(E)])
+        R_in = r[:, :Tmax].copy()
+        for e in range(E):                            # garbage at r_T in the strided array must be ignored
+            if nsteps[e] < Tmax:
+                R_in[e, nsteps[e]] = np.nan
+        total = rb.add_episodes(dev(S), dev(R_in), nsteps, R_term=dev(R_term), dVdx=dev(dV), want_total=True)
+    else:
+        total = rb.add_episodes(dev(S), dev(r), nsteps, dVdx=dev(dV), want_total=True)
+    store = rb.storage.cpu().numpy()
+    tot = total.cpu().numpy()
+    pos = start
+    for e in range(E):
+        T = int(nsteps[e])
+        rows, t = _expected_rows(S[e, :T + 1], r[e, :T + 1], dV[e, :T + 1], nTD, MC)
+        slots = (pos + np.arange(T + 1)) % N
+        np.testing.assert_array_equal(store[slots], rows, err_msg="episode %d" % e)
+        np.testing.assert_array_equal(tot[e, :T + 1], t, err_msg="episode %d" % e)
+        pos += T + 1
+    n = int((nsteps + 1).sum())
+    assert rb.next_idx == (start + n) % N
+    assert rb.full == int(start + n > N)
+
+
+def test_rl_solve_add_per_leaves_get_max_priority():
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    from cacto_amd.system import System
+    conf = load_conf("double_integrator")
+
+    class C:
+        pass
+    c = C()
+    c.__dict__.update({k: getattr(conf, k) for k in dir(conf) if not k.startswith("__")})
+    c.REPLAY_SIZE, c.prioritized_replay_alpha = 1024, 0.6
+    per = PrioritizedReplayBuffer(c, System(conf))
+    rng = np.random.default_rng(3)
+    nsteps = [9, 0, 20]
+    S = torch.as_tensor(rng.normal(size=(3, 21, per.ns)), device="cuda")
+    R = torch.as_tensor(rng.normal(size=(3, 21)), device="cuda")
+    per.add_episodes(S, R, nsteps)
+    leaves = per.sum_tree[per.cap:per.cap + 40].cpu().numpy()
+    m = float(per.max_priority.item()) ** 0.6
+    np.testing.assert_array_equal(leaves[:32], m)
+    np.testing.assert_array_equal(leaves[32:], 0.0)
