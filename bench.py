@@ -331,6 +331,8 @@ def extra_system(name, args, world, rank):
         conf.prioritized_replay_alpha = 0.6
     r = rollout_phase(rl, conf, env, cfg["R"], args.steps, args.warmup, world, rank)
     buf = fill_buffer(rl, conf, r, env, seed=rank, per=cfg["per"])
+    if cfg["per"] and world > 1:
+        buf.set_data_parallel(world)        # IS weights over the union of the ranks' shards
     ups = {}
     for B in cfg["batches"]:
         if cfg["per"]:

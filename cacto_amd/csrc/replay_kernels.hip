@@ -69,18 +69,34 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
                                                            int64_t max_idx, double beta,
                                                            const double* __restrict__ uniforms, int B,
                                                            int32_t* __restrict__ idx_out, float* __restrict__ w_out,
-                                                           double* __restrict__ exp_counter) {
-  __shared__ double seg_s, total_s, maxw_s;
+                                                           double* __restrict__ exp_counter,
+                                                           const double* __restrict__ shards, int n_shards) {
+  __shared__ double seg_s, total_s, maxw_s, scale_s;
   __shared__ int32_t idx_s[PER_MAX_B];
   if (threadIdx.x == 0) {
     const double p_total = prefix_reduce(sum_tree, cap, max_idx - 2);  // sum(0, max_idx - 1)
     seg_s = p_total / B;
     total_s = sum_tree[1];
-    const double p_min = min_tree[1] / total_s;
-    maxw_s = pow(p_min * (double)max_idx, -beta);
+    if (shards) {
+      // Data parallel: every shard draws B stratified samples from its own tree, so sample i of
+      // shard g has probability p_i / (G * total_g) in the union of N = sum N_g rows. The IS
+      // weight (N * P(i))^-beta is normalised by its maximum over all shards. For one shard this
+      // is exactly the single-buffer formula below.
+      double n_all = 0.0, ratio_min = __builtin_inf();
+      for (int g = 0; g < n_shards; ++g) {
+        n_all += shards[3 * g + 2];
+        ratio_min = tree_min(ratio_min, shards[3 * g + 1] / shards[3 * g + 0]);
+      }
+      scale_s = n_all / n_shards;
+      maxw_s = pow(ratio_min * scale_s, -beta);
+    } else {
+      const double p_min = min_tree[1] / total_s;
+      scale_s = (double)max_idx;
+      maxw_s = pow(p_min * scale_s, -beta);
+    }
   }
   __syncthreads();
-  const double seg = seg_s, total = total_s, maxw = maxw_s;
+  const double seg = seg_s, total = total_s, maxw = maxw_s, scale = scale_s;
   for (int i = threadIdx.x; i < B; i += blockDim.x) {
     double p = uniforms[i] * seg + i * seg;
     int64_t node = 1;
@@ -96,7 +112,7 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
     idx_s[i] = id;
     idx_out[i] = id;
     const double pr = sum_tree[node] / total;
-    w_out[i] = (float)(pow(pr * (double)max_idx, -beta) / maxw);
+    w_out[i] = (float)(pow(pr * scale, -beta) / maxw);
   }
   __syncthreads();
   // exp_counter[idxes] += 1: numpy fancy-index increment counts each distinct index once.
@@ -108,6 +124,16 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
   for (int i = threadIdx.x; i < B; i += blockDim.x) {
     if (exp_counter) exp_counter[idx_s[i]] = old[k] + 1.0;
     ++k;
+  }
+}
+
+// This shard's (sum, min, row count) for the data-parallel exchange of cacto_per_sample_global.
+__global__ void k_per_shard_stats(const double* __restrict__ sum_tree, const double* __restrict__ min_tree,
+                                  int64_t max_idx, double* __restrict__ stats) {
+  if (threadIdx.x == 0) {
+    stats[0] = sum_tree[1];
+    stats[1] = min_tree[1];
+    stats[2] = (double)max_idx;
   }
 }
 
@@ -235,7 +261,31 @@ extern "C" int cacto_per_sample(const double* sum_tree_d, const double* min_tree
   // max_idx <= 1 makes the reference's sum(0, max_idx - 1) recurse past the leaves (segment_tree.py:36-49)
   CACTO_REQUIRE(max_idx >= 2 && max_idx <= capacity, "cacto_per_sample: need 2 <= max_idx <= capacity");
   hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
-                     max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d);
+                     max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d, nullptr, 0);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_per_shard_stats(const double* sum_tree_d, const double* min_tree_d, int64_t max_idx,
+                                     double* stats_d, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && stats_d && max_idx >= 0, "cacto_per_shard_stats: bad arguments");
+  hipLaunchKernelGGL(k_per_shard_stats, dim3(1), dim3(64), 0, as_stream(stream), sum_tree_d, min_tree_d, max_idx,
+                     stats_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+extern "C" int cacto_per_sample_global(const double* sum_tree_d, const double* min_tree_d, int64_t capacity,
+                                       int64_t max_idx, double beta, const double* uniforms_d, int B,
+                                       const double* shard_stats_d, int n_shards, int32_t* idx_d, float* is_w_d,
+                                       double* exp_counter_d, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && uniforms_d && idx_d && is_w_d && shard_stats_d && n_shards > 0 &&
+                    pow2(capacity),
+                "cacto_per_sample_global: bad arguments");
+  CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_sample_global: 0 < B <= 8192");
+  CACTO_REQUIRE(max_idx >= 2 && max_idx <= capacity, "cacto_per_sample_global: need 2 <= max_idx <= capacity");
+  hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
+                     max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d, shard_stats_d, n_shards);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }

@@ -131,6 +131,14 @@ class ReplayBuffer:
         return s, r, sn, dv, d, term, w, None
 
 
+def exchange_shard_stats(local, world, all_gather):
+    """Gather every rank's 3-vector (sum, min, max_idx) into one contiguous [world, 3] tensor in
+    rank order; `all_gather(list_out, tensor)` is torch.distributed.all_gather (RCCL or gloo)."""
+    parts = [torch.empty_like(local) for _ in range(world)]
+    all_gather(parts, local)
+    return torch.stack(parts).contiguous()
+
+
 class PrioritizedReplayBuffer(ReplayBuffer):
     """replay_buffer.py:87-218 (with the three shipped crash bugs fixed — DESIGN.md §PER)."""
     prioritized = True
@@ -170,9 +178,31 @@ class PrioritizedReplayBuffer(ReplayBuffer):
             u = torch.as_tensor(np.asarray(uniforms, dtype=np.float64), device=DEVICE)
         idx = torch.empty(B, dtype=torch.int32, device=DEVICE)
         w = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        if self.dp_world > 1:
+            stats = self.shard_stats()
+            L.lib().call("cacto_per_sample_global", dptr(self.sum_tree), dptr(self.min_tree), self.cap,
+                         self.max_idx(), self.beta, dptr(u), B, dptr(stats), self.dp_world, dptr(idx), dptr(w),
+                         dptr(self.exp_counter), stream())
+            return idx, w
         L.lib().call("cacto_per_sample", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.max_idx(),
                      self.beta, dptr(u), B, dptr(idx), dptr(w), dptr(self.exp_counter), stream())
         return idx, w
+
+    # ---- data parallel: one replay shard per rank, IS weights over the union ----
+    dp_world = 1
+    dp_group = None
+
+    def set_data_parallel(self, world_size, group=None):
+        self.dp_world = int(world_size)
+        self.dp_group = group
+
+    def shard_stats(self):
+        """All ranks' (sum, min, max_idx), [G, 3] f64 on the device, via one all-gather (RCCL)."""
+        import torch.distributed as dist
+        local = torch.empty(3, dtype=torch.float64, device=DEVICE)
+        L.lib().call("cacto_per_shard_stats", dptr(self.sum_tree), dptr(self.min_tree), self.max_idx(), dptr(local),
+                     stream())
+        return exchange_shard_stats(local, self.dp_world, lambda out, t: dist.all_gather(out, t, group=self.dp_group))
 
     def sample(self, uniforms=None):
         idx, w = self.sample_device(uniforms)

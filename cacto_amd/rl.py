@@ -212,6 +212,8 @@ class RL_AC:
         B = self.conf.BATCH_SIZE
         per = getattr(buffer, "prioritized", False)
         if per:
+            if self.dp_world > 1 and buffer.dp_world != self.dp_world:
+                buffer.set_data_parallel(self.dp_world, self.dp_group)
             for _ in range(n):
                 idx, w = buffer.sample_device()
                 y = torch.empty(B, dtype=torch.float32, device=DEVICE)
@@ -272,13 +274,15 @@ class RL_AC:
         return (torch.as_tensor(np.asarray(S0, dtype=np.float64), device=DEVICE).contiguous(),
                 torch.as_tensor(nsteps, device=DEVICE).contiguous(), torch.as_tensor(order, device=DEVICE))
 
-    def rollout_batch(self, S0, nsteps, T, ep=1, weights=None, want=("S", "A", "R", "EE"), inputs=None, out=None):
-        """Roll out len(S0) episodes in one persistent kernel (K18), episodes packed by length."""
+    def rollout_batch(self, S0, nsteps, T, ep=1, weights=None, want=("S", "A", "R", "EE"), inputs=None, out=None,
+                      actor=None):
+        """Roll out len(S0) episodes in one persistent kernel (K18), episodes packed by length.
+        `actor` (an NN-held network, default self.actor_model) gives the policy."""
         S0, n, order = inputs if inputs is not None else self.rollout_inputs(S0, nsteps)
         R = S0.shape[0]
         ns, na = self.conf.nb_state, self.conf.nb_action
         if out is not None:
-            return self._launch_rollout(S0, n, order, T, ep, weights, out)
+            return self._launch_rollout(S0, n, order, T, ep, weights, out, actor)
         f64 = dict(dtype=torch.float64, device=DEVICE)
         out = {}
         if "S" in want:
@@ -290,11 +294,12 @@ class RL_AC:
         if "EE" in want:
             out["EE"] = torch.empty(R, T + 1, 3, **f64)
         out["status"] = torch.empty(R, dtype=torch.int32, device=DEVICE)
-        return self._launch_rollout(S0, n, order, T, ep, weights, out)
+        return self._launch_rollout(S0, n, order, T, ep, weights, out, actor)
 
-    def _launch_rollout(self, S0, n, order, T, ep, weights, out):
+    def _launch_rollout(self, S0, n, order, T, ep, weights, out, actor=None):
         W = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float64), device=DEVICE)
-        L.lib().call("cacto_rollout", self.sys.handle, dptr(self.actor_model.buf), dptr(S0), dptr(n), T,
+        actor = self.actor_model if actor is None else actor
+        L.lib().call("cacto_rollout", self.sys.handle, dptr(actor.buf), dptr(S0), dptr(n), T,
                      int(ep != 0), dptr(W), dptr(out.get("S")), dptr(out.get("A")), dptr(out.get("R")),
                      dptr(out.get("EE")), dptr(out.get("status")), dptr(order), S0.shape[0], stream())
         return out

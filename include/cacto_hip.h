@@ -268,6 +268,17 @@ int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity
 int cacto_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
                      double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
                      double* exp_counter_d, void* stream);
+/* Data-parallel PER: stats_d [3] = (total sum, min leaf, max_idx) of this shard,
+ * for an all-gather into shard_stats_d [n_shards, 3]. cacto_per_sample_global then samples B
+ * stratified indices from the local tree exactly as cacto_per_sample, with IS weights taken
+ * against the union of the shards: w = (N p_i / (G T_g))^-beta / (N min_h(m_h/T_h) / G)^-beta,
+ * N = sum of the shards' max_idx, T_g / m_g this shard's sum / min. With one shard the weights
+ * equal cacto_per_sample's bit for bit. */
+int cacto_per_shard_stats(const double* sum_tree_d, const double* min_tree_d, int64_t max_idx, double* stats_d,
+                          void* stream);
+int cacto_per_sample_global(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
+                            double beta, const double* uniforms_d, int B, const double* shard_stats_d,
+                            int n_shards, int32_t* idx_d, float* is_w_d, double* exp_counter_d, void* stream);
 /* update_priorities 'PER' (replay_buffer.py:190-218): p = fresh^count*|y-V| + eps; leaves p^alpha,
  * duplicates last-write-wins; max_priority_d[0] = max(max_priority, p). */
 int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,

@@ -158,6 +158,27 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         pr = np.array([self.it_sum[int(i)] for i in idxes]) / total
         return (pr * max_idx) ** (-self.beta) / max_weight
 
+    def shard_stats(self):
+        """(sum, min, max_idx) of this shard, the 3-vector the data-parallel ranks all-gather."""
+        return np.array([self.it_sum.sum(), self.it_min.min(), float(self.max_idx())])
+
+    def sample_weights_global(self, idxes, shard_stats):
+        """IS weights when G shards each draw the same number of stratified samples (a
+        build extension; the reference is single-process): P(i) = p_i / (G * T_g) over N = sum N_h
+        rows, w = (N P(i))^-beta / max over the union. G = 1 reduces to sample_weights."""
+        st = np.asarray(shard_stats, dtype=np.float64).reshape(-1, 3)
+        G = st.shape[0]
+        n_all = 0.0
+        ratio_min = float("inf")
+        for T, m, n in st:
+            n_all += n
+            ratio_min = min(ratio_min, m / T)
+        scale = n_all / G
+        max_weight = (ratio_min * scale) ** (-self.beta)
+        self.exp_counter[idxes] += 1
+        pr = np.array([self.it_sum[int(i)] for i in idxes]) / self.it_sum.sum()
+        return (pr * scale) ** (-self.beta) / max_weight
+
     def update_priorities(self, idxes, y, V):
         """replay_buffer.py:190-218 ('PER' branch): p = fresh^count * |y - V| + eps.
         The reference multiplies a float64 numpy array by float32 TF tensors, so p is a float32

@@ -121,3 +121,61 @@ def test_dp_update_equals_single_process():
     # and the update did move the weights
     w0 = load_weights("di_seed0_0")
     assert not np.allclose(ref["critic"], _flat(w0["critic"]).numpy())
+
+
+# ------------------------------------------------------------------ PER over replay shards
+def _per_shard(rank):
+    from oracle import buffer as obuf
+    rng = np.random.default_rng(100 + rank)
+    o = obuf.PrioritizedReplayBuffer(1024, 5, 0.6, 0.6, 1e-2, 0.95, 32)
+    n = 300 + 200 * rank                                   # shards of different fill
+    for i, v in enumerate(rng.uniform(0.05, 3.0, size=n) ** 0.6):
+        o.it_sum[i] = float(v)
+        o.it_min[i] = float(v)
+    o.next_idx = n
+    u = rng.uniform(size=32)
+    return o, o.sample_proportional(u)
+
+
+def _per_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cacto_amd.replay_buffer import exchange_shard_stats
+        o, idx = _per_shard(rank)
+        stats = exchange_shard_stats(torch.from_numpy(o.shard_stats()), world, lambda out, t: dist.all_gather(out, t))
+        w = o.sample_weights_global(idx, stats.numpy())
+        q.put((rank, stats.numpy(), np.asarray(idx), w))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_per_shard_exchange_gives_union_weights():
+    from oracle import buffer as obuf
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_per_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (st, idx, w)) for r, st, idx, w in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = [_per_shard(r)[0] for r in range(2)]
+    expect = np.stack([s.shard_stats() for s in shards])
+    for r in range(2):
+        np.testing.assert_array_equal(res[r][0], expect)          # rank order, exact values
+    # the union: each shard draws the same count, so P(i) = p_i / (G T_g) over N = N_0 + N_1 rows
+    N = sum(s.max_idx() for s in shards)
+    P = [np.array([s.it_sum[i] for i in range(s.max_idx())]) / (2 * s.it_sum.sum()) for s in shards]
+    wmax = (N * min(p.min() for p in P)) ** -0.6
+    for r in range(2):
+        idx, w = res[r][1], res[r][2]
+        np.testing.assert_allclose(w, (N * P[r][idx]) ** -0.6 / wmax, rtol=1e-12)
+        assert np.all(w <= 1.0 + 1e-12)
+    # one shard: exactly the single-buffer weights
+    o, idx = _per_shard(0)
+    o2, _ = _per_shard(0)
+    np.testing.assert_array_equal(o.sample_weights_global(idx, o.shard_stats()[None]), o2.sample_weights(idx))

@@ -279,6 +279,27 @@ def test_rollout_di_known_answer():
         np.testing.assert_allclose(out["R"].cpu().numpy()[k], rR, rtol=1e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize("system,tag", [("double_integrator", "di_seed0_final"), ("manipulator", None),
+                                        ("car_park", None)])
+def test_policy_eval_returns(system, tag):
+    """PLOT.rollout (plot_utils.py:245-279): full-NSTEPS rollouts from init_states_sim, returns
+    keyed by (x0, y0) = Python sum of the step rewards, p_ee[:, 2] replaced by s[:, 2]."""
+    from cacto_amd.plot_utils import PLOT
+    conf, genv, oe, nn, rl = _nets(system, tag)
+    plot = PLOT(0, genv, nn, conf, learner=rl)
+    returns = plot.rollout(0, rl.actor_model, conf.init_states_sim)
+    actor = rl.actor_model.get_weights()
+    assert len(returns) == len({(s[0], s[1]) for s in conf.init_states_sim})
+    for k, s0 in enumerate(conf.init_states_sim):
+        rS, rA, rR, rEE = oroll.policy_rollout(oe, actor, s0, conf.NSTEPS)
+        ret = 0
+        for r in rR:
+            ret += r
+        assert abs(returns[s0[0], s0[1]] - ret) <= 1e-3 * abs(ret) + 1e-6, (k, returns[s0[0], s0[1]], ret)
+        np.testing.assert_array_equal(plot.p_ee_all_sim[k][1:, 2], plot.states_all_sim[k][1:, 2])
+        np.testing.assert_allclose(plot.p_ee_all_sim[k][:, :2], rEE[:, :2], rtol=1e-4, atol=2e-4)
+
+
 @pytest.mark.parametrize("system", ["double_integrator", "manipulator"])
 def test_rollout_variable_lengths(system):
     conf, genv, oe, nn, rl = _nets(system, None, seed=3)
@@ -390,6 +411,47 @@ def test_per_sampling_bit_exact(ref_vectors):
     ow = o.sample_weights(ref_vectors["per_idx"])
     np.testing.assert_allclose(w.cpu().numpy(), ow.astype(np.float32), rtol=1e-6)
     np.testing.assert_array_equal(per.exp_counter.cpu().numpy()[:len(leaves)], o.exp_counter[:len(leaves)])
+
+
+def test_per_sample_global_matches_oracle(ref_vectors):
+    """Sharded PER: local stratified indices, IS weights over the union of shards."""
+    from cacto_amd import _lib as L
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    from cacto_amd.system import System, dptr, stream
+    conf = load_conf("double_integrator")
+
+    class C:
+        pass
+    c = C()
+    c.__dict__.update({k: getattr(conf, k) for k in dir(conf) if not k.startswith("__")})
+    c.BATCH_SIZE, c.prioritized_replay_alpha = 64, 0.6
+    per = PrioritizedReplayBuffer(c, System(conf))
+    leaves = ref_vectors["per_leaves"]
+    per.set_leaves(np.arange(len(leaves)), leaves)
+    per.next_idx = len(leaves)
+    u = list(ref_vectors["per_u"])
+    idx0, w0 = per.sample_device(u)
+    stats = torch.empty(3, dtype=torch.float64, device="cuda")
+    L.lib().call("cacto_per_shard_stats", dptr(per.sum_tree), dptr(per.min_tree), per.max_idx(), dptr(stats), stream())
+    one = stats.reshape(1, 3).contiguous()
+    ud = torch.as_tensor(np.asarray(u), device="cuda")
+    for shards in (one, torch.cat([one, torch.tensor([[3.5, 1e-3, 700.0], [0.25, 0.2, 40.0]], dtype=torch.float64,
+                                                     device="cuda")])):
+        idx = torch.empty(len(u), dtype=torch.int32, device="cuda")
+        w = torch.empty(len(u), dtype=torch.float32, device="cuda")
+        L.lib().call("cacto_per_sample_global", dptr(per.sum_tree), dptr(per.min_tree), per.cap, per.max_idx(),
+                     per.beta, dptr(ud), len(u), dptr(shards), shards.shape[0], dptr(idx), dptr(w), None, stream())
+        np.testing.assert_array_equal(idx.cpu().numpy(), idx0.cpu().numpy())
+        if shards.shape[0] == 1:
+            np.testing.assert_array_equal(w.cpu().numpy(), w0.cpu().numpy())
+        o = obuf.PrioritizedReplayBuffer(65536, 5, 0.6, 0.6, 1e-2, 0.95, 64)
+        for i, v in enumerate(leaves):
+            o.it_sum[i] = float(v)
+            o.it_min[i] = float(v)
+        o.next_idx = len(leaves)
+        np.testing.assert_array_equal(shards[0].cpu().numpy(), o.shard_stats())
+        ow = o.sample_weights_global(idx0.cpu().numpy(), shards.cpu().numpy())
+        np.testing.assert_allclose(w.cpu().numpy(), ow.astype(np.float32), rtol=1e-6)
 
 
 def test_per_update_priorities_matches_oracle():
