@@ -38,29 +38,53 @@ __global__ void k_per_level(double* sum_tree, double* min_tree, int64_t lo, int6
   }
 }
 
+// Top of the sum tree staged in LDS by the PER kernels: nodes [1, TOP_NODES).
+constexpr int TOP_NODES = 1024;
+
+__device__ __forceinline__ double tree_at(const double* tree, const double* top, int64_t ntop, int64_t node) {
+  return node < ntop ? top[node] : tree[node];
+}
+
 // _reduce_helper(0, end, 1, 0, cap-1) for the sum tree (end inclusive): right-nested sum of the
-// maximal left-aligned nodes, exactly as the recursion combines them.
-__device__ double prefix_reduce(const double* tree, int64_t cap, int64_t end) {
-  double terms[64];
-  int nt = 0;
+// maximal left-aligned nodes, exactly as the recursion combines them. The path depends on `end`
+// only, so every term is loaded independently (one memory latency, not one per level).
+__device__ double prefix_reduce(const double* tree, const double* top, int64_t ntop, int64_t cap, int64_t end) {
+  constexpr int MAXD = 32;  // capacity <= 2^31 (int32 indices)
+  double t[MAXD];
+  bool v[MAXD];
   int64_t node = 1, ns = 0, ne = cap - 1;
-  while (true) {
-    if (end == ne) {
-      terms[nt++] = tree[node];
-      break;
-    }
-    const int64_t mid = (ns + ne) / 2;
-    if (end <= mid) {
-      node = 2 * node;
-      ne = mid;
-    } else {
-      terms[nt++] = tree[2 * node];
-      node = 2 * node + 1;
-      ns = mid + 1;
+  bool done = false;
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) {
+    v[k] = false;
+    t[k] = 0.0;
+    if (!done) {
+      if (end == ne) {
+        t[k] = tree_at(tree, top, ntop, node);
+        v[k] = true;
+        done = true;
+      } else {
+        const int64_t mid = (ns + ne) / 2;
+        if (end <= mid) {
+          node = 2 * node;
+          ne = mid;
+        } else {
+          t[k] = tree_at(tree, top, ntop, 2 * node);
+          v[k] = true;
+          node = 2 * node + 1;
+          ns = mid + 1;
+        }
+      }
     }
   }
-  double r = terms[nt - 1];
-  for (int k = nt - 2; k >= 0; --k) r = terms[k] + r;
+  double r = 0.0;
+  bool have = false;
+#pragma unroll
+  for (int k = MAXD - 1; k >= 0; --k)
+    if (v[k]) {
+      r = have ? t[k] + r : t[k];
+      have = true;
+    }
   return r;
 }
 
@@ -73,8 +97,12 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
                                                            const double* __restrict__ shards, int n_shards) {
   __shared__ double seg_s, total_s, maxw_s, scale_s;
   __shared__ int32_t idx_s[PER_MAX_B];
+  __shared__ double top_s[TOP_NODES];
+  const int64_t ntop = cap < TOP_NODES ? cap : TOP_NODES;
+  for (int k = threadIdx.x; k < ntop; k += blockDim.x) top_s[k] = k ? sum_tree[k] : 0.0;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const double p_total = prefix_reduce(sum_tree, cap, max_idx - 2);  // sum(0, max_idx - 1)
+    const double p_total = prefix_reduce(sum_tree, top_s, ntop, cap, max_idx - 2);  // sum(0, max_idx - 1)
     seg_s = p_total / B;
     total_s = sum_tree[1];
     if (shards) {
@@ -97,22 +125,102 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
   }
   __syncthreads();
   const double seg = seg_s, total = total_s, maxw = maxw_s, scale = scale_s;
-  for (int i = threadIdx.x; i < B; i += blockDim.x) {
-    double p = uniforms[i] * seg + i * seg;
-    int64_t node = 1;
-    while (node < cap) {
-      if (sum_tree[2 * node] > p) {
-        node = 2 * node;
-      } else {
-        p -= sum_tree[2 * node];
-        node = 2 * node + 1;
+  // find_prefixsum_idx for every sample: the top levels from LDS, the rest in rounds of up to three
+  // levels whose seven candidate left children are loaded together (one memory latency per round
+  // instead of per level). The comparisons and subtractions are the reference's, in its order. The
+  // (up to 8) descents of a thread advance in lock-step so their loads overlap too.
+  constexpr int PT = PER_MAX_B / PER_THREADS;
+  constexpr int PG = 4;  // descents in lock-step per group (register budget at 1024 threads)
+  int64_t node[PT];
+#pragma unroll
+  for (int g = 0; g < PT; g += PG) {
+    if (threadIdx.x + g * blockDim.x >= (unsigned)B) {
+#pragma unroll
+      for (int j = g; j < g + PG; ++j) node[j] = cap;
+      continue;
+    }
+    double p[PG];
+    int64_t nd[PG];
+#pragma unroll
+    for (int jj = 0; jj < PG; ++jj) {
+      const int i = threadIdx.x + (g + jj) * blockDim.x;
+      p[jj] = i < B ? uniforms[i] * seg + i * seg : 0.0;
+      nd[jj] = 1;
+      if (i < B) {
+        while (2 * nd[jj] < ntop) {
+          const double left = top_s[2 * nd[jj]];
+          if (left > p[jj]) {
+            nd[jj] = 2 * nd[jj];
+          } else {
+            p[jj] -= left;
+            nd[jj] = 2 * nd[jj] + 1;
+          }
+        }
       }
     }
-    const int32_t id = (int32_t)(node - cap);
-    idx_s[i] = id;
-    idx_out[i] = id;
-    const double pr = sum_tree[node] / total;
-    w_out[i] = (float)(pow(pr * scale, -beta) / maxw);
+    while (true) {
+      bool any = false;
+#pragma unroll
+      for (int jj = 0; jj < PG; ++jj) any |= (threadIdx.x + (g + jj) * blockDim.x < (unsigned)B) && nd[jj] < cap;
+      if (!any) break;
+      double a[PG], b0[PG], b1[PG], c[PG][4];
+#pragma unroll
+      for (int jj = 0; jj < PG; ++jj) {
+        const int64_t n = nd[jj];
+        const bool live = threadIdx.x + (g + jj) * blockDim.x < (unsigned)B && n < cap;
+        a[jj] = live ? tree_at(sum_tree, top_s, ntop, 2 * n) : 0.0;
+        const bool two = live && 2 * n < cap, three = live && 4 * n < cap;
+        b0[jj] = two ? sum_tree[4 * n] : 0.0;
+        b1[jj] = two ? sum_tree[4 * n + 2] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[jj][q] = three ? sum_tree[8 * n + 2 * q] : 0.0;
+      }
+#pragma unroll
+      for (int jj = 0; jj < PG; ++jj) {
+        const int64_t n = nd[jj];
+        if (threadIdx.x + (g + jj) * blockDim.x >= (unsigned)B || n >= cap) continue;
+        int64_t m;
+        if (a[jj] > p[jj]) {
+          m = 2 * n;
+        } else {
+          p[jj] -= a[jj];
+          m = 2 * n + 1;
+        }
+        if (2 * n < cap) {
+          const double bl = (m & 1) ? b1[jj] : b0[jj];
+          if (bl > p[jj]) {
+            m = 2 * m;
+          } else {
+            p[jj] -= bl;
+            m = 2 * m + 1;
+          }
+          if (4 * n < cap) {
+            const int q = (int)(m - 4 * n);
+            const double cl = q == 0 ? c[jj][0] : q == 1 ? c[jj][1] : q == 2 ? c[jj][2] : c[jj][3];
+            if (cl > p[jj]) {
+              m = 2 * m;
+            } else {
+              p[jj] -= cl;
+              m = 2 * m + 1;
+            }
+          }
+        }
+        nd[jj] = m;
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < PG; ++jj) node[g + jj] = nd[jj];
+  }
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = threadIdx.x + j * blockDim.x;
+    if (i < B) {
+      const int32_t id = (int32_t)(node[j] - cap);
+      idx_s[i] = id;
+      idx_out[i] = id;
+      const double pr = sum_tree[node[j]] / total;
+      w_out[i] = (float)(pow(pr * scale, -beta) / maxw);
+    }
   }
   __syncthreads();
   // exp_counter[idxes] += 1: numpy fancy-index increment counts each distinct index once.
@@ -144,7 +252,8 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, doubl
                                                         const double* __restrict__ exp_counter, double fresh, double eps,
                                                         double alpha, double* max_priority) {
   __shared__ int32_t id_s[PER_MAX_B];
-  __shared__ double maxp_s[PER_THREADS];
+  __shared__ double maxp_s[PER_THREADS / 64];
+  __shared__ double top_sum[TOP_NODES], top_min[TOP_NODES];
   double my_max = -__builtin_inf();
   bool unsorted = false;
   for (int i = threadIdx.x; i < n; i += blockDim.x) id_s[i] = idx[i];
@@ -180,36 +289,72 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, doubl
       min_tree[cap + id_s[i]] = leaf;
     }
   }
-  if (max_priority) {  // max is order-independent: tree reduction
-    maxp_s[threadIdx.x] = my_max;
+  if (max_priority) {  // max is order-independent: wave reduction, then across the waves
+    double m = my_max;
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) maxp_s[threadIdx.x >> 6] = m;
     __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
-      if ((int)threadIdx.x < w) maxp_s[threadIdx.x] = fmax(maxp_s[threadIdx.x], maxp_s[threadIdx.x + w]);
-      __syncthreads();
+    if (threadIdx.x == 0) {
+      double mm = maxp_s[0];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mm = fmax(mm, maxp_s[w]);
+      max_priority[0] = fmax(max_priority[0], mm);
     }
-    if (threadIdx.x == 0) max_priority[0] = fmax(max_priority[0], maxp_s[0]);
   }
   __syncthreads();
-  __threadfence_block();
-  // ancestors: every thread walks its leaf's path one level per barrier
-  int64_t nodes[PER_MAX_B / PER_THREADS];
-  int k = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) nodes[k++] = (cap + id_s[i]) >> 1;
-  while (true) {
-    bool any = false;
-    k = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x, ++k) {
-      const int64_t nd = nodes[k];
-      if (nd >= 1) {
-        sum_tree[nd] = sum_tree[2 * nd] + sum_tree[2 * nd + 1];
-        min_tree[nd] = tree_min(min_tree[2 * nd], min_tree[2 * nd + 1]);
-        nodes[k] = nd >> 1;
-        any = true;
+  // Ancestors below the LDS-staged top, one level per barrier. With sorted indices a node is
+  // refreshed only by the first sample below it (the others would rewrite the same value). Each
+  // thread loads the children of all its nodes before storing any parent, so the loads overlap.
+  constexpr int PT = PER_MAX_B / PER_THREADS;
+  int log2cap = 0;
+  while (((int64_t)1 << log2cap) < cap) ++log2cap;
+  const int64_t ntop = cap < TOP_NODES / 2 ? cap : TOP_NODES / 2;  // rows [ntop, 2 ntop) fit the LDS arrays
+  int log2top = 0;
+  while (((int64_t)1 << log2top) < ntop) ++log2top;
+  for (int shift = 1; shift <= log2cap - log2top; ++shift) {
+    int64_t nd[PT];
+    double s0[PT], s1[PT], m0[PT], m1[PT];
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = threadIdx.x + j * blockDim.x;
+      nd[j] = 0;
+      if (i < n) {
+        const int64_t x = (cap + id_s[i]) >> shift;
+        if (!(sorted && i > 0 && ((cap + id_s[i - 1]) >> shift) == x)) nd[j] = x;
+      }
+      if (nd[j]) {
+        s0[j] = sum_tree[2 * nd[j]];
+        s1[j] = sum_tree[2 * nd[j] + 1];
+        m0[j] = min_tree[2 * nd[j]];
+        m1[j] = min_tree[2 * nd[j] + 1];
       }
     }
+#pragma unroll
+    for (int j = 0; j < PT; ++j)
+      if (nd[j]) {
+        sum_tree[nd[j]] = s0[j] + s1[j];
+        min_tree[nd[j]] = tree_min(m0[j], m1[j]);
+      }
     __syncthreads();
-    __threadfence_block();
-    if (!__syncthreads_or(any)) break;
+  }
+  // The top: its bottom row [ntop, 2 ntop) is current now; rebuild nodes [1, ntop) in LDS. Nodes
+  // no sample touched come out unchanged (the tree is consistent, the op is deterministic).
+  double* ts = top_sum;
+  double* tm = top_min;
+  for (int64_t k = ntop + threadIdx.x; k < 2 * ntop; k += blockDim.x) {
+    ts[k] = sum_tree[k];
+    tm[k] = min_tree[k];
+  }
+  __syncthreads();
+  for (int64_t lo = ntop / 2; lo >= 1; lo /= 2) {
+    for (int64_t k = lo + threadIdx.x; k < 2 * lo; k += blockDim.x) {
+      ts[k] = ts[2 * k] + ts[2 * k + 1];
+      tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
+    }
+    __syncthreads();
+  }
+  for (int64_t k = 1 + threadIdx.x; k < ntop; k += blockDim.x) {
+    sum_tree[k] = ts[k];
+    min_tree[k] = tm[k];
   }
 }
 
