@@ -15,6 +15,18 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 #define CACTO_THREADS (CACTO_WAVE * CACTO_NWAVES)
 #define CACTO_TILE 16                  // samples per workgroup tile (MFMA 16x16x4 N dimension)
 
+#ifdef CACTO_STAMPS
+__shared__ unsigned long long cacto_stamp_s[32];  // per-workgroup phase stamps (diagnostic builds)
+#define PSTAMP(k)                                                                 \
+  do {                                                                            \
+    if (threadIdx.x == 0) cacto_stamp_s[k] = __builtin_amdgcn_s_memtime();       \
+  } while (0)
+#else
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 namespace cacto {
 
 void set_error(const std::string& msg);
@@ -61,6 +73,36 @@ __device__ __forceinline__ void fast_sincos(float x, float* s, float* c) {
   if (__builtin_expect(fabsf(x) > 8192.f, 0)) sincosf(x, &so, &co);
   *s = so;
   *c = co;
+}
+// fast_sincos on 4 values at once: the four polynomial chains interleave (no per-element branch
+// in between), and the large-argument fallback is one branch for the group. Same results as
+// fast_sincos element by element.
+__device__ __forceinline__ void fast_sincos4(const float x[4], float s[4], float c[4]) {
+  bool big = false;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float j = rintf(x[r] * 0.636619772367581343f);
+    float t = fmaf(-j, 1.5703125f, x[r]);
+    t = fmaf(-j, 4.837512969970703125e-4f, t);
+    t = fmaf(-j, 7.54978995489188216e-8f, t);
+    const float t2 = t * t;
+    float ps = fmaf(t2, -1.9515295891e-4f, 8.3321608736e-3f);
+    ps = fmaf(t2, ps, -1.6666654611e-1f);
+    const float sr = fmaf(t * t2, ps, t);
+    float pc = fmaf(t2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    pc = fmaf(t2, pc, 4.166664568298827e-2f);
+    const float cr = fmaf(t2 * t2, pc, fmaf(-0.5f, t2, 1.0f));
+    const int q = (int)j & 3;
+    const float a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;
+    s[r] = (q & 2) ? -a : a;
+    c[r] = ((q + 1) & 2) ? -b : b;
+    big |= fabsf(x[r]) > 8192.f;
+  }
+  if (__builtin_expect(big, 0)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (fabsf(x[r]) > 8192.f) sincosf(x[r], &s[r], &c[r]);
+  }
 }
 __device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
 __device__ __forceinline__ double dmul(double a, double b) { return __dmul_rn(a, b); }

@@ -536,6 +536,65 @@ __device__ inline void env_simulate_const(const SysDevice& sd, const ConstDyn<NJ
 // 1/state_norm when NORMALIZE_INPUTS.
 // Car :408-418 (Fu[2,0] = Fu[4,1] = dt), CarPark :555-565 (Fu[3,0] = dt, Fu[4,1] = dt/tau_delta).
 template <int NJ>
+__device__ inline void env_derivative(const SysDevice& sd, const double* s, double* Fu);
+
+// env_simulate(s, a, f32in) and env_derivative(s) together. For a chain, M(q) is factored once and
+// serves both the step and the columns of M^-1 (env_derivative would rebuild it with v = 0; M does
+// not depend on v, so the factor is the same bits).
+template <int NJ>
+__device__ inline bool env_simulate_derivative(const SysDevice& sd, const double* s, const double* a, bool f32in,
+                                               double* out, double* Fu) {
+  if constexpr (NJ > 0) {
+    const cacto_sys_params& p = sd.p;
+    constexpr int NS = 2 * NJ + 1, NA = NJ;
+    const double dt = p.dt;
+    double M[NJ * NJ], h[NJ], dv[NJ];
+    chain_terms<NJ>(sd, s, s + NJ, M, h);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) dv[i] = a[i] - h[i];
+    const bool ok = cholesky<NJ>(M);
+    chol_solve<NJ>(M, dv);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      const double v = s[NJ + i];
+      if (f32in) {
+        const float vdt = __fmul_rn((float)v, (float)dt);
+        out[i] = s[i] + (double)vdt;
+        out[NJ + i] = (double)(float)(v + dv[i] * dt);
+      } else {
+        out[i] = s[i] + v * dt;
+        out[NJ + i] = v + dv[i] * dt;
+      }
+    }
+    out[2 * NJ] = s[2 * NJ] + dt;
+#pragma unroll
+    for (int k = 0; k < NS * NA; ++k) Fu[k] = 0.0;
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {  // column c of Minv
+      double x[NJ];
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) x[i] = (i == c) ? 1.0 : 0.0;
+      chol_solve<NJ>(M, x);
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) Fu[(NJ + i) * NA + c] = x[i] * dt;
+    }
+    if (p.normalize) {
+#pragma unroll
+      for (int r = 0; r < NS - 1; ++r) {
+        const double inv = 1.0 / p.state_norm[r];
+#pragma unroll
+        for (int c = 0; c < NA; ++c) Fu[r * NA + c] *= inv;
+      }
+    }
+    return ok;
+  } else {
+    const bool ok = env_simulate<NJ>(sd, s, a, f32in, out);
+    env_derivative<NJ>(sd, s, Fu);
+    return ok;
+  }
+}
+
+template <int NJ>
 __device__ inline void env_derivative(const SysDevice& sd, const double* s, double* Fu) {
   const cacto_sys_params& p = sd.p;
   constexpr int NS = NJ == 0 ? 3 : NJ < 0 ? 6 : 2 * NJ + 1;

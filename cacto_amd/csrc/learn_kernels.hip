@@ -12,6 +12,25 @@
 //   -> k_adam : sum chunks in fixed order (deterministic), Adam, packed copies, soft update.
 #include "net_common.h"
 
+#ifdef CACTO_STAMPS
+__device__ unsigned long long g_cstamps[32];
+#define CSTAMP(k) PSTAMP(k)
+#define CSTAMP_DECL
+#define CSTAMP_FLUSH                                                                     \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                             \
+      for (int k_ = 0; k_ < 32; ++k_) g_cstamps[k_] = cacto_stamp_s[k_];                 \
+  } while (0)
+#else
+#define CSTAMP(k) \
+  do {            \
+  } while (0)
+#define CSTAMP_DECL
+#define CSTAMP_FLUSH \
+  do {               \
+  } while (0)
+#endif
+
 namespace cacto {
 
 struct GradBufs {
@@ -63,6 +82,8 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   __shared__ float4 red[4 * 64];
   __shared__ float st[256], stn[256], dvdx[256];
   __shared__ float Rs[16], ds[16], ws[16], Vn[16], V[16], y[16], Vb[16], Vt2[16];
+  CSTAMP_DECL;
+  CSTAMP(0);
   const cacto_sys_params& p = sdp->p;
   const Lane L;
   const int ns = p.nb_state, cols = 3 * ns + 3, s0 = blockIdx.x * CACTO_TILE;
@@ -72,30 +93,44 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   const int goff[4] = {0, 0, 4, 8};
   if (blockIdx.x == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
 
-  if (L.tid < 16) {
-    const int c = L.tid;
-    const bool valid = s0 + c < B;
-    const double* rp = storage + (size_t)(valid ? idx[s0 + c] : 0) * cols;
-    for (int f = 0; f < 16; ++f) {
-      const bool in = valid && f < ns;
-      st[c * 16 + f] = in ? (float)rp[f] : 0.f;
-      stn[c * 16 + f] = in ? (float)rp[ns + 1 + f] : 0.f;
-      dvdx[c * 16 + f] = in ? (float)rp[2 * ns + 1 + f] : 0.f;
+  float4 w5[2];  // W5[:, 0] at this lane's rows of layer-3 out tiles wave, wave + 4
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const float* w = C.flat + C.t.woff[4] + 16 * (L.wave + 4 * t) + 4 * L.g;
+    w5[t] = make_float4(w[0], w[1], w[2], w[3]);
+  }
+  const Norm4 nrm(p, L);  // state_norm of this lane's features, loaded with the rows
+  {  // one (sample, feature) per thread: the row gathers overlap
+    // branch-free gathers (clamped sample and feature indices, then zeroed): no load sits under
+    // a branch, so the waits stay exact
+    const int c = L.tid >> 4, f = L.tid & 15;
+    const bool valid = s0 + c < B, in = valid && f < ns;
+    const int sc = min(s0 + c, B - 1), fc = min(f, ns - 1);
+    const double* rp = storage + (size_t)idx[sc] * cols;
+    const double x = rp[fc], xn = rp[ns + 1 + fc], xd = rp[2 * ns + 1 + fc];
+    const double r = rp[ns], d = rp[3 * ns + 1];
+    const float wv = isw ? isw[sc] : 1.f;
+    st[c * 16 + f] = in ? (float)x : 0.f;
+    stn[c * 16 + f] = in ? (float)xn : 0.f;
+    dvdx[c * 16 + f] = in ? (float)xd : 0.f;
+    if (f == 0) {
+      Rs[c] = valid ? (float)r : 0.f;
+      ds[c] = valid ? (float)d : 0.f;
+      ws[c] = valid ? wv : 0.f;
     }
-    Rs[c] = valid ? (float)rp[ns] : 0.f;
-    ds[c] = valid ? (float)rp[3 * ns + 1] : 0.f;
-    ws[c] = valid ? (isw ? isw[s0 + c] : 1.f) : 0.f;
   }
   __syncthreads();
   if (L.wave == 0) {
-    fill_input_tile(p, st, X0, L);
-    fill_input_tile(p, stn, XT, L);
+    nrm.fill(st, X0, L);
+    nrm.fill(stn, XT, L);
   }
   __syncthreads();
+  CSTAMP(1);
 
   // y = R + (1 - d) * V_tgt(s_next)   (NeuralNetwork.py:153-158)
   if (!cs.MC) critic_forward_tile(Tg, XT, nullptr, nullptr, Hs, red, Vn, L, [](int, int, float4) {});
   __syncthreads();
+  CSTAMP(2);
   if (L.tid < 16) y[L.tid] = cs.MC ? Rs[L.tid] : fadd(Rs[L.tid], fmul(fsub(1.f, ds[L.tid]), Vn[L.tid]));
   if (cs.want_vt) {  // the extra V_tgt(s) of NeuralNetwork.py:178
     critic_forward_tile(Tg, X0, nullptr, nullptr, Hs, red, Vt2, L, [](int, int, float4) {});
@@ -108,13 +143,17 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     store_panel(gb.LT[l + 1], ld, Bp + s0 + L.c, ot, L.g, h4);
   });
   __syncthreads();
+  CSTAMP(3);
 
+  CriticFwdFrags SF;
   if (sob) {
     // first backward: D_l -> RT_l first half; G_l kept in LDS; G_0 = dV/dx0
     critic_first_backward(C, Cs, GB, G, G0, red, L, [&](int l, int ot, int lane, float4 d4) {
       store_panel(gb.RT[l], ld, s0 + (lane & 15), ot, lane >> 4, d4);
     });
     __syncthreads();
+    CSTAMP(4);
+    SF.load<false>(C, L);
     // Sobolev loss gradient w.r.t. dV/ds, then w.r.t. G_0 (NeuralNetwork.py:167-170)
     if (L.wave == 0) {
       const float4 g4 = G0[L.lane];
@@ -125,10 +164,10 @@ __global__ void __launch_bounds__(CACTO_THREADS)
         const int f = 4 * L.g + r;
         gb0[r] = 0.f;
         if (f < ns - 1) {
-          const float dvds = normalize_backward(p, f, gv[r]);
+          const float dvds = nrm.backward(r, gv[r]);
           const float yp = clog(dvds), yt = clog(dvdx[L.c * 16 + f]);
           const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
-          gb0[r] = normalize_backward(p, f, clog_backward(dvds, gyp));
+          gb0[r] = nrm.backward(r, clog_backward(dvds, gyp));
         }
       }
       const float4 v = make_float4(gb0[0], gb0[1], gb0[2], gb0[3]);
@@ -136,19 +175,13 @@ __global__ void __launch_bounds__(CACTO_THREADS)
       store_panel(gb.LT[0], ld, s0 + L.c, 0, L.g, v);
     }
     __syncthreads();
-    // backward of the first backward, l = 0..3 (see oracle/nn.py compute_critic_grad)
-    const float4* cur = GB;
-    for (int l = 0; l < 4; ++l) {
-      float4* nxt = GB + ((l + 1) & 1) * 8 * 64;
-      layer(C.fwd(l), C.t.OT[l], C.t.KT[l], cur, red, L, [&](int ot, floatx4 acc) {
+    CSTAMP(5);
+    // backward of the first backward, l = 0..3 (see oracle/nn.py compute_critic_grad), on the
+    // forward fragments (no bias, loaded before the Sobolev loss above)
+    auto sp_epi = [&](int l, float4* nxt) {
+      return [&, l, nxt](int ot, floatx4 acc) {
         const float4 sz = Hs[(zoff[l] + ot) * 64 + L.lane], cz = Cs[(zoff[l] + ot) * 64 + L.lane];
-        float4 gu;
-        if (l < 3) {
-          gu = G[(goff[l + 1] + ot) * 64 + L.lane];
-        } else {
-          const int f = 16 * ot + 4 * L.g;
-          gu = make_float4(C.w(4, f, 0), C.w(4, f + 1, 0), C.w(4, f + 2, 0), C.w(4, f + 3, 0));
-        }
+        const float4 gu = l < 3 ? G[(goff[l + 1] + ot) * 64 + L.lane] : (ot >= 4 ? w5[1] : w5[0]);
         const float sv[4] = {sz.x, sz.y, sz.z, sz.w}, cv[4] = {cz.x, cz.y, cz.z, cz.w};
         const float gg[4] = {gu.x, gu.y, gu.z, gu.w};
         float zb[4], gn[4];
@@ -160,15 +193,31 @@ __global__ void __launch_bounds__(CACTO_THREADS)
         const float4 g4 = make_float4(gn[0], gn[1], gn[2], gn[3]);
         nxt[ot * 64 + L.lane] = g4;
         store_panel(gb.LT[l + 1], ld, s0 + L.c, ot, L.g, g4);
-      });
-      cur = nxt;
-    }
+      };
+    };
+    float4* nA = GB + 8 * 64;
+    SF.f0.run(GB, nullptr, 4, L.wave, L.lane, sp_epi(0, nA));
+    __syncthreads();
+    CSTAMP(6);
+    SF.f1.run(nA, nullptr, 4, L.wave, L.lane, sp_epi(1, GB));
+    __syncthreads();
+    CSTAMP(7);
+    SF.f2.run(GB, nullptr, 8, L.wave, L.lane, sp_epi(2, nA));
+    __syncthreads();
+    CSTAMP(8);
+    SF.f3.run(nA, nullptr, 8, L.wave, L.lane, sp_epi(3, GB));
+    __syncthreads();
+    CSTAMP(9);
     if (L.tid < 16) gb.RT[4][s0 + L.tid] = 1.f;  // dW5 += Gbar_4 (G_4 = W5[:, 0])
   } else {
     for (int k = L.tid; k < 24 * 64; k += CACTO_THREADS) ZB[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
+  CSTAMP(10);
 
+  // the transposed fragments of the last backward pass, in flight during the value loss
+  CriticBwdFrags HB;
+  HB.load(C, L);
   // value loss: Vbar = (2 * ((wS/B) * w)) * (V - y)   (Keras MSE, SUM_OVER_BATCH_SIZE)
   if (L.tid < 16) {
     const int c = L.tid;
@@ -183,26 +232,24 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     }
   }
   __syncthreads();
-  for (int k = L.tid; k < 8 * 64; k += CACTO_THREADS) {  // zbar_3 += (Vbar * W5) * cos(z3)
-    const int ot = k >> 6, lane = k & 63, g = lane >> 4, c = lane & 15;
-    const float4 z = Cs[(zoff[3] + ot) * 64 + lane];
-    float4 zb = ZB[(zoff[3] + ot) * 64 + lane];
-    const int f = 16 * ot + 4 * g;
-    zb.x = fadd(zb.x, fmul(fmul(Vb[c], C.w(4, f, 0)), z.x));
-    zb.y = fadd(zb.y, fmul(fmul(Vb[c], C.w(4, f + 1, 0)), z.y));
-    zb.z = fadd(zb.z, fmul(fmul(Vb[c], C.w(4, f + 2, 0)), z.z));
-    zb.w = fadd(zb.w, fmul(fmul(Vb[c], C.w(4, f + 3, 0)), z.w));
-    ZB[(zoff[3] + ot) * 64 + lane] = zb;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {  // zbar_3 += (Vbar * W5) * cos(z3): out tiles wave, wave + 4
+    const int ot = L.wave + 4 * t;
+    const float4 z = Cs[(zoff[3] + ot) * 64 + L.lane];
+    float4 zb = ZB[(zoff[3] + ot) * 64 + L.lane];
+    const float4 w = w5[t];
+    const float vb = Vb[L.c];
+    zb.x = fadd(zb.x, fmul(fmul(vb, w.x), z.x));
+    zb.y = fadd(zb.y, fmul(fmul(vb, w.y), z.y));
+    zb.z = fadd(zb.z, fmul(fmul(vb, w.z), z.z));
+    zb.w = fadd(zb.w, fmul(fmul(vb, w.w), z.w));
+    ZB[(zoff[3] + ot) * 64 + L.lane] = zb;
   }
   __syncthreads();
+  CSTAMP(11);
   // backward through the forward graph: zbar_{l-1} += (zbar_l W_l^T) * cos(z_{l-1})
-  for (int l = 3; l >= 0; --l) {
-    for (int k = L.tid; k < C.t.OT[l] * 64; k += CACTO_THREADS) {
-      const int ot = k >> 6, lane = k & 63;
-      store_panel(gb.RT[l], ld, Bp + s0 + (lane & 15), ot, lane >> 4, ZB[(zoff[l] + ot) * 64 + lane]);
-    }
-    if (l == 0) break;
-    layer(C.bwd(l), C.t.KT[l], C.t.OT[l], ZB + zoff[l] * 64, red, L, [&](int it, floatx4 acc) {
+  auto hb_epi = [&](int l) {
+    return [&, l](int it, floatx4 acc) {
       const float4 z = Cs[(zoff[l - 1] + it) * 64 + L.lane];
       float4 zb = ZB[(zoff[l - 1] + it) * 64 + L.lane];
       zb.x = fadd(zb.x, fmul(acc[0], z.x));
@@ -210,8 +257,30 @@ __global__ void __launch_bounds__(CACTO_THREADS)
       zb.z = fadd(zb.z, fmul(acc[2], z.z));
       zb.w = fadd(zb.w, fmul(acc[3], z.w));
       ZB[(zoff[l - 1] + it) * 64 + L.lane] = zb;
-    });
-  }
+    };
+  };
+  auto store_rt = [&](int l) {
+    for (int k = L.tid; k < C.t.OT[l] * 64; k += CACTO_THREADS) {
+      const int ot = k >> 6, lane = k & 63;
+      store_panel(gb.RT[l], ld, Bp + s0 + (lane & 15), ot, lane >> 4, ZB[(zoff[l] + ot) * 64 + lane]);
+    }
+  };
+  store_rt(3);
+  HB.g3.run(ZB + zoff[3] * 64, nullptr, 8, L.wave, L.lane, hb_epi(3));
+  __syncthreads();
+  CSTAMP(12);
+  store_rt(2);
+  HB.g2.run(ZB + zoff[2] * 64, nullptr, 4, L.wave, L.lane, hb_epi(2));
+  __syncthreads();
+  CSTAMP(13);
+  store_rt(1);
+  HB.g1.run(ZB + zoff[1] * 64, nullptr, 4, L.wave, L.lane, hb_epi(1));
+  __syncthreads();
+  CSTAMP(14);
+  store_rt(0);
+  CSTAMP(15);
+  __syncthreads();
+  CSTAMP_FLUSH;
 }
 
 // ---------------------------------------------------------------- actor chain (a12)
@@ -230,6 +299,8 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   __shared__ float Fu[16 * CACTO_MAX_STATE * CACTO_MAX_ACTION];
   __shared__ float dra[16 * CACTO_MAX_ACTION];
   __shared__ float Vn[16];
+  __shared__ double term_s[16];
+  CSTAMP(0);
   const SysDevice& sd = *sdp;
   const cacto_sys_params& p = sd.p;
   const Lane L;
@@ -237,29 +308,32 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   const int ld = gb.ld;
   if (blockIdx.x == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
   double term_c = 0.0;
-  if (L.tid < 16) {
-    const int c = L.tid;
+  {
+    const int c = L.tid >> 4, f = L.tid & 15;
     const bool valid = s0 + c < B;
     const double* rp = storage + (size_t)(valid ? idx[s0 + c] : 0) * cols;
-    for (int f = 0; f < 16; ++f) st[c * 16 + f] = (valid && f < ns) ? (float)rp[f] : 0.f;
-    term_c = valid ? rp[3 * ns + 2] : 0.0;
+    st[c * 16 + f] = (valid && f < ns) ? (float)rp[f] : 0.f;
+    if (f == 0) term_s[c] = valid ? rp[3 * ns + 2] : 0.0;
   }
   __syncthreads();
+  if (L.tid < 16) term_c = term_s[L.tid];
   if (L.wave == 0) {
     fill_input_tile(p, st, X0, L);
     store_panel(gb.LT[0], ld, s0 + L.c, 0, L.g, X0[L.lane]);  // input of layer 0 (normalised)
   }
   __syncthreads();
   // actor forward; h1 -> LT_1, h2 -> LT_2
+  CSTAMP(1);
   actor_forward_tile(Ac, na, X0, ZA, H, red, A, L, [&](int l, int ot, float4, float4 h4) {
     store_panel(gb.LT[l + 1], ld, s0 + L.c, ot, L.g, h4);
   });
   __syncthreads();
+  CSTAMP(2);
   // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
   if (L.tid < 16) {
     constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
     const int c = L.tid;
-    double s[NS], a[NA], sn[NS], F[NS * NA], w[8];
+    double s[NS], a[NA], sn[NS], F[NS * NA];
     float af[NA], g[NA];
 #pragma unroll
     for (int f = 0; f < NS; ++f) s[f] = (double)st[c * 16 + f];
@@ -268,29 +342,32 @@ __global__ void __launch_bounds__(CACTO_THREADS)
       af[i] = A[c * na + i];
       a[i] = (double)af[i];
     }
-    env_simulate<NJ>(sd, s, a, true, sn);
+    env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
 #pragma unroll
     for (int f = 0; f < 16; ++f) stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
-    env_derivative<NJ>(sd, s, F);
 #pragma unroll
     for (int k = 0; k < NS * NA; ++k) Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) w[k] = k >= p.n_weights ? 0.0 : term_c * p.w_terminal[k] + (1.0 - term_c) * p.w_running[k];
-    const double partial = env_reward<NJ>(sd, w, s, nullptr, true);
-    (void)reward_batch_f32<NA>(p, w[6], af, partial, g);
+    // only d reward / d a enters the actor gradient (NeuralNetwork.py:199-204), and only the
+    // control cost depends on a, so the state terms of the reward are not evaluated here
+    const double w6 = 6 >= p.n_weights ? 0.0 : term_c * p.w_terminal[6] + (1.0 - term_c) * p.w_running[6];
+    (void)reward_batch_f32<NA>(p, w6, af, 0.0, g);
 #pragma unroll
     for (int i = 0; i < NA; ++i) dra[c * na + i] = g[i];
   }
   __syncthreads();
+  CSTAMP(3);
   if (L.wave == 0) fill_input_tile(p, stn, XS, L);
   __syncthreads();
   // critic (already updated) at s': V and dV/dx0 (NeuralNetwork.py:190-195)
   float4* HC = H;            // 16 tiles
   float4* ZB2 = H + 16 * 64;  // 16 tiles
+  CSTAMP(4);
   critic_forward_tile(C, XS, ZC, nullptr, HC, red, Vn, L, [](int, int, float4) {});
   __syncthreads();
+  CSTAMP(5);
   critic_first_backward(C, ZC, HC, nullptr, G0, red, L, [](int, int, int, float4) {});
   __syncthreads();
+  CSTAMP(6);
   // dQ/da = dV/ds' Fu + dr/da ; abar = -dQ/da / B  (NeuralNetwork.py:206-231)
   if (L.wave == 0) {
     const int c = L.c;
@@ -315,6 +392,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     store_panel(gb.RT[2], ld, s0 + c, 0, L.g, v);
   }
   __syncthreads();
+  CSTAMP(7);
   // zbar2 = (abar W3^T) * lrelu'(z2) ; zbar1 = (zbar2 W2^T) * lrelu'(z1)
   layer(Ac.bwd(2), Ac.t.KT[2], Ac.t.OT[2], ZB3, red, L, [&](int it, floatx4 acc) {
     const float4 z = ZA[(16 + it) * 64 + L.lane];
@@ -325,6 +403,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     ZB2[it * 64 + L.lane] = v;
     store_panel(gb.RT[1], ld, s0 + L.c, it, L.g, v);
   });
+  CSTAMP(8);
   layer(Ac.bwd(1), Ac.t.KT[1], Ac.t.OT[1], ZB2, red, L, [&](int it, floatx4 acc) {
     const float4 z = ZA[it * 64 + L.lane];
     const float zz[4] = {z.x, z.y, z.z, z.w};
@@ -332,6 +411,9 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     for (int r = 0; r < 4; ++r) o[r] = zz[r] > 0.f ? acc[r] : fmul(acc[r], 0.3f);
     store_panel(gb.RT[0], ld, s0 + L.c, it, L.g, make_float4(o[0], o[1], o[2], o[3]));
   });
+  CSTAMP(9);
+  __syncthreads();
+  CSTAMP_FLUSH;
 }
 
 // ---------------------------------------------------------------- weight-gradient GEMM
@@ -465,6 +547,14 @@ __global__ void __launch_bounds__(256) k_reduce(const float* __restrict__ slab, 
 }
 
 }  // namespace cacto
+
+#ifdef CACTO_STAMPS
+extern "C" int cacto_debug_critic_stamps(unsigned long long* out_h) {
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_cstamps), sizeof(unsigned long long) * 32));
+  return CACTO_OK;
+}
+#endif
 
 using namespace cacto;
 

@@ -69,27 +69,48 @@ struct NetView {
     return pk + (size_t)(t.blocks + t.pkoff[l]) * 64;
   }
   __device__ __forceinline__ float bias(int l, int f) const { return flat[t.boff[l] + f]; }
+  __device__ __forceinline__ const float* biasp(int l) const { return flat + t.boff[l]; }
   __device__ __forceinline__ float w(int l, int i, int o) const { return flat[t.woff[l] + i * t.out[l] + o]; }
 };
 
+// The 4 bias values of out tile ot for this lane (features 16 ot + 4 g + r), or zeros.
+__device__ __forceinline__ float4 tile_bias(const float* __restrict__ bias, int ot, int lane) {
+  if (!bias) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* b = bias + 16 * ot + 4 * (lane >> 4);
+  return make_float4(b[0], b[1], b[2], b[3]);
+}
+
+__device__ __forceinline__ floatx4 add_bias(floatx4 acc, const float* bias, float4 b) {
+  if (bias) {
+    acc[0] = fadd(acc[0], b.x);
+    acc[1] = fadd(acc[1], b.y);
+    acc[2] = fadd(acc[2], b.z);
+    acc[3] = fadd(acc[3], b.w);
+  }
+  return acc;
+}
+
 // out-tile loop of one layer: each wave takes out tiles ot = wave, wave+4, ...; X = LDS tiles.
-// All KT weight fragments of a tile are issued before its MFMAs, and the next tile's fragments
-// are in flight while the current tile's MFMAs run (the A operand comes from L2, so the load
-// latency is paid once per layer rather than once per k-step).
+// All KT weight fragments of a tile (and its biases, when `bias` is given: the epilogue then
+// receives acc + b) are issued before its MFMAs, and the next tile's are in flight while the
+// current tile's MFMAs run (A comes from L2: the load latency is paid once per layer, not once
+// per k-step, and no epilogue waits on a global load).
 template <int KT, typename Epi>
 __device__ __forceinline__ void mm_layer_t(const float4* __restrict__ A, int OT, const float4* X, int wave, int lane,
-                                           Epi&& epi) {
+                                           Epi&& epi, const float* __restrict__ bias) {
   int ot = wave;
   if (ot >= OT) return;
   float4 a[KT];
 #pragma unroll
   for (int k = 0; k < KT; ++k) a[k] = A[((size_t)ot * KT + k) * 64 + lane];
+  float4 bv = tile_bias(bias, ot, lane);
   while (true) {
     const int nxt = ot + CACTO_NWAVES;
-    float4 an[KT];
+    float4 an[KT], bn = bv;
     if (nxt < OT) {
 #pragma unroll
       for (int k = 0; k < KT; ++k) an[k] = A[((size_t)nxt * KT + k) * 64 + lane];
+      bn = tile_bias(bias, nxt, lane);
     }
     // the 4 k-steps of a fragment block go to 4 independent accumulators (issue-bound chain)
     floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
@@ -101,27 +122,87 @@ __device__ __forceinline__ void mm_layer_t(const float4* __restrict__ A, int OT,
       c2 = mfma4(a[k].z, b.z, c2);
       c3 = mfma4(a[k].w, b.w, c3);
     }
-    epi(ot, (c0 + c1) + (c2 + c3));
+    epi(ot, add_bias((c0 + c1) + (c2 + c3), bias, bv));
     if (nxt >= OT) break;
     ot = nxt;
+    bv = bn;
 #pragma unroll
     for (int k = 0; k < KT; ++k) a[k] = an[k];
   }
 }
 
+// A whole layer's weight fragments for one wave, held in registers: NT out tiles
+// (ot = wave + 4 t) x KT k-tiles, plus their biases. A pass over a fixed-shape network (the
+// critic) loads every layer's fragments up front, so the L2/HBM latency is paid once per pass
+// instead of once per layer behind each barrier.
+//
+// The loads are branch-free (tile index clamped, bias presence a template argument): a load
+// under a branch makes the compiler's waitcnt tracking fall back to vmcnt(0) at the join, which
+// would serialise the prefetch.
+template <int KT, int NT>
+struct Frags {
+  float4 a[NT][KT];
+  float4 b[NT];
+  template <bool BIAS>
+  __device__ __forceinline__ void load(const float4* __restrict__ A, const float* __restrict__ bias, int OT, int wave,
+                                       int lane) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int ot = min(wave + CACTO_NWAVES * t, OT - 1);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) a[t][k] = A[((size_t)ot * KT + k) * 64 + lane];
+      if (BIAS) {
+        const float* bp = bias + 16 * ot + 4 * (lane >> 4);
+        b[t] = make_float4(bp[0], bp[1], bp[2], bp[3]);
+      } else {
+        b[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  // same arithmetic as mm_layer_t: 4 accumulators over the k-steps j, then (c0 + c1) + (c2 + c3)
+  // All tiles' MFMAs are issued before the first epilogue, so the epilogue VALU work of tile t
+  // overlaps the matrix core's work on tile t + 1.
+  template <typename Epi>
+  __device__ __forceinline__ void run(const float4* X, const float* bias, int OT, int wave, int lane,
+                                      Epi&& epi) const {
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+      if (wave + CACTO_NWAVES * t < OT) {
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+          const float4 x = X[k * 64 + lane];
+          c0 = mfma4(a[t][k].x, x.x, c0);
+          c1 = mfma4(a[t][k].y, x.y, c1);
+          c2 = mfma4(a[t][k].z, x.z, c2);
+          c3 = mfma4(a[t][k].w, x.w, c3);
+        }
+      }
+      acc[t] = (c0 + c1) + (c2 + c3);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int ot = wave + CACTO_NWAVES * t;
+      if (ot < OT) epi(ot, add_bias(acc[t], bias, b[t]));
+    }
+  }
+};
+
 template <typename Epi>
 __device__ __forceinline__ void mm_layer(const float4* __restrict__ A, int OT, int KT, const float4* X, int wave,
-                                         int lane, Epi&& epi) {
+                                         int lane, Epi&& epi, const float* __restrict__ bias = nullptr) {
   switch (KT) {
-    case 1: mm_layer_t<1>(A, OT, X, wave, lane, epi); break;
-    case 4: mm_layer_t<4>(A, OT, X, wave, lane, epi); break;
-    case 8: mm_layer_t<8>(A, OT, X, wave, lane, epi); break;
-    case 16: mm_layer_t<16>(A, OT, X, wave, lane, epi); break;
+    case 1: mm_layer_t<1>(A, OT, X, wave, lane, epi, bias); break;
+    case 4: mm_layer_t<4>(A, OT, X, wave, lane, epi, bias); break;
+    case 8: mm_layer_t<8>(A, OT, X, wave, lane, epi, bias); break;
+    case 16: mm_layer_t<16>(A, OT, X, wave, lane, epi, bias); break;
     default:
       for (int ot = wave; ot < OT; ot += CACTO_NWAVES) {
+        const float4 bv = tile_bias(bias, ot, lane);
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
         for (int kt = 0; kt < KT; ++kt) acc = mfma_block(A[((size_t)ot * KT + kt) * 64 + lane], X[kt * 64 + lane], acc);
-        epi(ot, acc);
+        epi(ot, add_bias(acc, bias, bv));
       }
   }
 }
