@@ -75,6 +75,8 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
     }
     if (joint_table_h && p.dyn_kind == CACTO_DYN_CHAIN)
       std::memcpy(host.joints, joint_table_h, sizeof(double) * p.n_joints * CACTO_JOINT_COLS);
+    for (int r = 0; r < CACTO_MAX_STATE; ++r)  // IEEE double division: the same bits as on the device
+      host.inv_norm[r] = r < p.nb_state && p.state_norm[r] != 0.0 ? 1.0 / p.state_norm[r] : 0.0;
     cacto_sys* s = new cacto_sys();
     s->host = host;
     hipError_t e = hipMalloc(&s->dev, sizeof(SysDevice));

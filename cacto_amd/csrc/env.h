@@ -13,6 +13,7 @@ namespace cacto {
 struct SysDevice {
   cacto_sys_params p;
   double joints[CACTO_MAX_JOINTS * CACTO_JOINT_COLS];
+  double inv_norm[CACTO_MAX_STATE];  // 1.0 / state_norm (the reference's 1/state_norm_arr, f64)
 };
 
 // ------------------------------------------------------------------ small 3-vector algebra
@@ -581,7 +582,7 @@ __device__ inline bool env_simulate_derivative(const SysDevice& sd, const double
     if (p.normalize) {
 #pragma unroll
       for (int r = 0; r < NS - 1; ++r) {
-        const double inv = 1.0 / p.state_norm[r];
+        const double inv = sd.inv_norm[r];
 #pragma unroll
         for (int c = 0; c < NA; ++c) Fu[r * NA + c] *= inv;
       }
@@ -629,7 +630,7 @@ __device__ inline void env_derivative(const SysDevice& sd, const double* s, doub
   if (p.normalize) {
 #pragma unroll
     for (int r = 0; r < NS - 1; ++r) {
-      const double inv = 1.0 / p.state_norm[r];
+      const double inv = sd.inv_norm[r];
 #pragma unroll
       for (int c = 0; c < NA; ++c) Fu[r * NA + c] *= inv;
     }

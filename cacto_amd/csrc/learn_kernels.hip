@@ -307,7 +307,6 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   const int ns = p.nb_state, na = p.nb_action, cols = 3 * ns + 3, s0 = blockIdx.x * CACTO_TILE;
   const int ld = gb.ld;
   if (blockIdx.x == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
-  double term_c = 0.0;
   {
     const int c = L.tid >> 4, f = L.tid & 15;
     const bool valid = s0 + c < B;
@@ -316,7 +315,6 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     if (f == 0) term_s[c] = valid ? rp[3 * ns + 2] : 0.0;
   }
   __syncthreads();
-  if (L.tid < 16) term_c = term_s[L.tid];
   if (L.wave == 0) {
     fill_input_tile(p, st, X0, L);
     store_panel(gb.LT[0], ld, s0 + L.c, 0, L.g, X0[L.lane]);  // input of layer 0 (normalised)
@@ -334,7 +332,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
     const int c = L.tid;
     double s[NS], a[NA], sn[NS], F[NS * NA];
-    float af[NA], g[NA];
+    float af[NA];
 #pragma unroll
     for (int f = 0; f < NS; ++f) s[f] = (double)st[c * 16 + f];
 #pragma unroll
@@ -347,9 +345,17 @@ __global__ void __launch_bounds__(CACTO_THREADS)
     for (int f = 0; f < 16; ++f) stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
 #pragma unroll
     for (int k = 0; k < NS * NA; ++k) Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
-    // only d reward / d a enters the actor gradient (NeuralNetwork.py:199-204), and only the
-    // control cost depends on a, so the state terms of the reward are not evaluated here
-    const double w6 = 6 >= p.n_weights ? 0.0 : term_c * p.w_terminal[6] + (1.0 - term_c) * p.w_running[6];
+  } else if (L.tid >= 64 && L.tid < 80) {
+    // wave 1, alongside the dynamics: only d reward / d a enters the actor gradient
+    // (NeuralNetwork.py:199-204), and only the control cost depends on a, so the state terms of the
+    // reward are not evaluated here
+    constexpr int NA = Dims<NJ>::NA;
+    const int c = L.tid - 64;
+    float af[NA], g[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) af[i] = A[c * na + i];
+    const double tc = term_s[c];
+    const double w6 = 6 >= p.n_weights ? 0.0 : tc * p.w_terminal[6] + (1.0 - tc) * p.w_running[6];
     (void)reward_batch_f32<NA>(p, w6, af, 0.0, g);
 #pragma unroll
     for (int i = 0; i < NA; ++i) dra[c * na + i] = g[i];
@@ -428,40 +434,114 @@ struct WgArgs {
   int toff[MAX_LAYERS + 1];
 };
 
+// One workgroup per (row chunk, item). An item is a block of up to 4 x 4 output tiles of one layer
+// (the 4 waves split the chunk's rows, each keeping 16 accumulator tiles, then reduce through LDS
+// in a fixed order, so the result is deterministic), or up to 4 bias tiles (one per wave). A
+// block loads each LT/RT panel slice once for 4 tiles instead of once per tile.
+constexpr int WG_BLK = 4;
+
 __global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab) {
-  const int wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wave_id >= a.nch * a.tpc) return;
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int chunk = wave_id / a.tpc, rem = wave_id - chunk * a.tpc;
+  __shared__ float4 part[4 * WG_BLK * WG_BLK * 64];  // 64 KiB
+  const int chunk = blockIdx.x / a.tpc;
+  int rem = blockIdx.x - chunk * a.tpc;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   int li = 0;
   while (rem >= a.toff[li + 1]) ++li;
   const WgLayer& Ly = a.l[li];
-  const int local = rem - a.toff[li];
+  rem -= a.toff[li];
   const int lo = a.r_begin + chunk * a.CH, hi = min(a.r_end, lo + a.CH);
   float* out = slab + (size_t)chunk * a.P;
-  if (local < Ly.IT * Ly.OT) {
-    const int it = local / Ly.OT, ot = local - it * Ly.OT;
-    const float* ap = Ly.LT + (size_t)(16 * it + c) * a.ld + 4 * g;
-    const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
-    int r = lo;
-    for (; r + 16 < hi; r += 32) {
-      acc = mfma_block(*reinterpret_cast<const float4*>(ap + r), *reinterpret_cast<const float4*>(bp + r), acc);
-      acc2 = mfma_block(*reinterpret_cast<const float4*>(ap + r + 16), *reinterpret_cast<const float4*>(bp + r + 16),
-                        acc2);
+  const int nbi = (Ly.IT + WG_BLK - 1) / WG_BLK, nbo = (Ly.OT + WG_BLK - 1) / WG_BLK;
+  if (rem < nbi * nbo) {
+    const int it0 = (rem / nbo) * WG_BLK, ot0 = (rem % nbo) * WG_BLK;
+    const int ni = min(WG_BLK, Ly.IT - it0), no = min(WG_BLK, Ly.OT - ot0);
+    const int span = ((hi - lo) / 16 + 3) / 4 * 16;  // rows per wave, multiple of 16
+    const int r0 = lo + wave * span, r1 = min(hi, r0 + span);
+    floatx4 acc[WG_BLK][WG_BLK];
+#pragma unroll
+    for (int i = 0; i < WG_BLK; ++i)
+#pragma unroll
+      for (int o = 0; o < WG_BLK; ++o) acc[i][o] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* ap = Ly.LT + (size_t)(16 * it0 + c) * a.ld + 4 * g;
+    const float* bp = Ly.RT + (size_t)(16 * ot0 + c) * a.ld + 4 * g;
+    // panel slices of the next 16 rows are in flight while this step's 64 MFMAs run
+    float4 An[WG_BLK], Bn[WG_BLK];
+    auto fetch = [&](int r) {
+      const int rr = min(r, r1 - 16);  // clamped (branch-free); a past-the-end fetch is unused
+#pragma unroll
+      for (int i = 0; i < WG_BLK; ++i)
+        An[i] = *reinterpret_cast<const float4*>(ap + (size_t)16 * min(i, ni - 1) * a.ld + rr);
+#pragma unroll
+      for (int o = 0; o < WG_BLK; ++o)
+        Bn[o] = *reinterpret_cast<const float4*>(bp + (size_t)16 * min(o, no - 1) * a.ld + rr);
+    };
+    if (r0 < r1) fetch(r0);
+    for (int r = r0; r < r1; r += 16) {
+      float4 A[WG_BLK], Bv[WG_BLK];
+#pragma unroll
+      for (int i = 0; i < WG_BLK; ++i) {
+        A[i] = An[i];
+        Bv[i] = Bn[i];
+      }
+      fetch(r + 16);
+#pragma unroll
+      for (int i = 0; i < WG_BLK; ++i)
+#pragma unroll
+        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].x, Bv[o].x, acc[i][o]);
+#pragma unroll
+      for (int i = 0; i < WG_BLK; ++i)
+#pragma unroll
+        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].y, Bv[o].y, acc[i][o]);
+#pragma unroll
+      for (int i = 0; i < WG_BLK; ++i)
+#pragma unroll
+        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].z, Bv[o].z, acc[i][o]);
+#pragma unroll
+      for (int i = 0; i < WG_BLK; ++i)
+#pragma unroll
+        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].w, Bv[o].w, acc[i][o]);
     }
-    if (r < hi) acc = mfma_block(*reinterpret_cast<const float4*>(ap + r), *reinterpret_cast<const float4*>(bp + r), acc);
-    acc = acc + acc2;
-    const int o = 16 * ot + c;
-    for (int q = 0; q < 4; ++q) {
-      const int i = 16 * it + 4 * g + q;
-      if (i < Ly.in && o < Ly.out) out[Ly.woff + i * Ly.out + o] = acc[q];
+#pragma unroll
+    for (int i = 0; i < WG_BLK; ++i)
+#pragma unroll
+      for (int o = 0; o < WG_BLK; ++o) part[((wave * WG_BLK + i) * WG_BLK + o) * 64 + lane] = f4(acc[i][o]);
+    __syncthreads();
+    // wave w finishes tiles t = 4w .. 4w + 3 of the 16: ((p0 + p1) + p2) + p3
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = wave * 4 + k, i = t / WG_BLK, o = t % WG_BLK;
+      if (i >= ni || o >= no) continue;
+      float4 s4 = part[((0 * WG_BLK + i) * WG_BLK + o) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float4 q = part[((w * WG_BLK + i) * WG_BLK + o) * 64 + lane];
+        s4.x += q.x;
+        s4.y += q.y;
+        s4.z += q.z;
+        s4.w += q.w;
+      }
+      const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+      const int oc = 16 * (ot0 + o) + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ii = 16 * (it0 + i) + 4 * g + q;
+        if (ii < Ly.in && oc < Ly.out) out[Ly.woff + ii * Ly.out + oc] = sv[q];
+      }
     }
   } else {
-    const int ot = local - Ly.IT * Ly.OT;
+    const int ot = (rem - nbi * nbo) * WG_BLK + wave;
+    if (ot >= Ly.OT) return;
     const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
     float s = 0.f;
-    for (int r = max(lo, a.bias_r0); r < hi; r += 16) {
+    int r = max(lo, a.bias_r0);
+    for (; r + 64 <= hi; r += 64) {  // 4 loads in flight, summed in row order
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(bp + r + 16 * k);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+    for (; r < hi; r += 16) {
       const float4 v = *reinterpret_cast<const float4*>(bp + r);
       s += (v.x + v.y) + (v.z + v.w);
     }
@@ -510,8 +590,17 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
   const float c1 = (float)(1.0 - a.beta1), c2 = (float)(1.0 - a.beta2), eps = (float)a.eps;
   const float tau = (float)a.tau, omt = (float)(1.0 - a.tau);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < t.params; p += gridDim.x * blockDim.x) {
+    // chunk partials summed in chunk order; loads issued 8 at a time so they overlap
     float g = slab[p];
-    for (int ch = 1; ch < nch; ++ch) g += slab[(size_t)ch * t.params + p];
+    int ch = 1;
+    for (; ch + 8 <= nch; ch += 8) {
+      float q[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q[k] = slab[(size_t)(ch + k) * t.params + p];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g += q[k];
+    }
+    for (; ch < nch; ++ch) g += slab[(size_t)ch * t.params + p];
     float mm = m[p], vv = v[p];
     mm = fadd(mm, fmul(fsub(g, mm), c1));
     vv = fadd(vv, fmul(fsub(fmul(g, g), vv), c2));
@@ -572,7 +661,9 @@ struct LaunchActorChain {
   }
 };
 
-constexpr int WG_CHUNK = 256;
+// Rows per weight-gradient chunk (one slab each): small batches use short chunks so the grid
+// still fills the chip; large ones long chunks so Adam sums few slabs.
+inline int wg_chunk(int rows) { return rows <= 1024 ? 64 : rows <= 4096 ? 128 : 256; }
 
 struct Workspace {
   GradBufs crit, act;
@@ -612,7 +703,8 @@ Workspace plan(const cacto_sys* sys, int B, char* base) {
     aoff += (size_t)16 * ta.OT[l] * w.act.ld;
   }
   off = align64(std::max(coff, aoff));
-  const int nch_c = (2 * Bp + WG_CHUNK - 1) / WG_CHUNK, nch_a = (Bp + WG_CHUNK - 1) / WG_CHUNK;
+  const int nch_a = ceil_div(Bp, wg_chunk(Bp));
+  const int nch_c = std::max(ceil_div(2 * Bp, wg_chunk(2 * Bp)), nch_a);  // Sobolev rows, or the plain half
   w.slab = f ? f + off : nullptr;
   off += align64(std::max((size_t)nch_c * tc.params, (size_t)nch_a * ta.params));
   w.scal = f ? f + off : nullptr;
@@ -628,14 +720,14 @@ WgArgs wg_args(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int
   a.r_begin = r_begin;
   a.r_end = r_end;
   a.bias_r0 = bias_r0;
-  a.CH = WG_CHUNK;
-  a.nch = (r_end - r_begin + WG_CHUNK - 1) / WG_CHUNK;
+  a.CH = wg_chunk(r_end - r_begin);
+  a.nch = ceil_div(r_end - r_begin, a.CH);
   a.P = t.params;
-  int tpc = 0;
+  int tpc = 0;  // workgroups per chunk: 4x4 tile blocks + groups of 4 bias tiles, per layer
   for (int l = 0; l < t.L; ++l) {
     a.l[l] = WgLayer{gb.LT[l], gb.RT[l], t.in[l], t.out[l], t.KT[l], t.OT[l], t.woff[l], t.boff[l]};
     a.toff[l] = tpc;
-    tpc += t.KT[l] * t.OT[l] + t.OT[l];
+    tpc += ceil_div(t.KT[l], WG_BLK) * ceil_div(t.OT[l], WG_BLK) + ceil_div(t.OT[l], WG_BLK);
   }
   a.toff[t.L] = tpc;
   a.tpc = tpc;
@@ -686,8 +778,7 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
   CACTO_CHECK_HIP(hipGetLastError());
   const bool sob = cs.w_S != 0.f;
   WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
-  const int waves = a.nch * a.tpc;
-  hipLaunchKernelGGL(k_wgrad, dim3((waves + 3) / 4), dim3(256), 0, st, a, w.slab);
+  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
   CACTO_CHECK_HIP(hipGetLastError());
   *nch_out = a.nch;
   return CACTO_OK;
@@ -702,8 +793,7 @@ int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, c
   if (int e = dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st))
     return e;
   WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
-  const int waves = a.nch * a.tpc;
-  hipLaunchKernelGGL(k_wgrad, dim3((waves + 3) / 4), dim3(256), 0, st, a, w.slab);
+  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
   CACTO_CHECK_HIP(hipGetLastError());
   *nch_out = a.nch;
   return CACTO_OK;
