@@ -1,0 +1,726 @@
+// Persistent rollout kernel (K18: RL_AC.create_TO_init RL.py:197-233 / PLOT.rollout
+// plot_utils.py:245-279): actor MFMA + float64 dynamics / reward / EE per step, all steps in-kernel.
+//
+// Scheduling. Episode lengths are spread (NSTEPS - int(t/dt), e.g. 1..200 for the double
+// integrator), so a workgroup that ran one fixed tile of episodes would idle once its shortest ones
+// end and the longest tile would set the launch time. Here a workgroup owns SL = 4*NG episode
+// *slots* and a queue of episodes: ranks of the length-sorted order are dealt to the G workgroups
+// in snake order (k*G + w for even rounds k, k*G + G-1-w for odd), and a slot whose episode ends
+// takes the next queue entry at the step boundary (slots in lane order: deterministic). The host
+// picks NG so there are about two episodes per slot; every slot then runs ~T_max steps.
+//
+// Actor on v_mfma_f32_4x4x1_16b_f32 with A-operand broadcast. The 16x16x4 form needs 16 samples
+// per MFMA; the 4x4x1 16-block form runs at the same rate with 4 samples per instruction, so a
+// workgroup can hold 8 (or 4, 16) episodes at full MFMA rate. Per instruction: blocks b = 16 groups
+// of 4 output features (lane 4b+j <-> feature 64*wave + 4b + j, the B operand = one weight row
+// segment W[k][64 wave + lane]), the A operand (4 samples of activation k) broadcast from block q
+// (CBSZ = 4, ABID = q), so one VGPR of activations (lane 4q+i = x[sample i][k0 + q]) feeds 16
+// consecutive k-steps. The result lands with the feature on the lane and the 4 samples in the
+// 4 accumulator registers. Layer-2 rows stay in registers for the whole launch (weight
+// stationary) or in LDS (RoSplit); the 256 -> na output layer is a VALU dot product + lane
+// reduction. Numerics: every dot product is an f32 FMA chain (MFMA) — F32 tolerance as before.
+#include <utility>
+
+#include "net_common.h"
+
+#ifdef CACTO_STAMPS
+__device__ unsigned long long g_rstamps[8];
+#define RSTAMP(k)                                                                     \
+  do {                                                                                \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && it == 20) g_rstamps[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define RSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
+namespace cacto {
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// D[feature lane][sample r] += x[sample r][k0 + Q] * w[k0 + Q][feature lane]
+template <int Q>
+__device__ __forceinline__ floatx4 mfma_bc(float x, float w, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(x, w, c, 4, Q, 0);
+}
+
+// Layer-2 weight rows by residence: [0, REGK) registers (the whole launch), [REGK, REGK + LDSK)
+// LDS, the rest streamed from global memory (L2-resident) at every step. The float64 chain
+// dynamics of the manipulator / UR5 need many registers, so those systems keep fewer rows in
+// registers (and the UR5 streams some); the LDS share is what fits beside the step buffers.
+template <int NJ, int NG>
+struct RoSplit {
+  static constexpr int REGK = NJ <= 2 ? 192 : NJ == 3 ? (NG == 4 ? 160 : 128) : NG == 4 ? 48 : 64;
+  static constexpr int LDSK = NJ <= 2 ? 64 : NJ == 3 ? (NG == 4 ? 96 : 128) : NG == 4 ? 80 : 64;
+  static_assert(REGK % 16 == 0 && LDSK % 16 == 0 && REGK + LDSK <= 256, "row split");
+};
+
+template <int NG>
+struct RoCfg {
+  static constexpr int SL = 4 * NG;     // episode slots per workgroup
+  static constexpr int GPW = 64 / SL;   // lane groups of SL lanes per wave (env-term fan-out)
+  static constexpr int P = 256 / SL;    // threads per slot in the output layer
+  static constexpr int H2S = 256 + P;   // h2 row stride: slots of one wave on distinct banks
+  static constexpr int H1B = 320;       // h1 floats per (group, 64-k block): 16 q x 20 (padded)
+};
+
+template <int NS, int REGK>
+struct RoActorRegs {
+  float w2[REGK];     // W2[k][64 wave + lane]
+  float w1[NS];       // W1[q][64 wave + lane]
+  float b1, b2;
+};
+
+template <int NG, int NA, int LDSK>
+struct RoActorLds {
+  float4 w2[LDSK / 4 * 4 * 64];                 // W2[REGK + 4kq + j][64w + lane] at (kq*4 + w)*64 + lane
+  float h1[NG * 4 * RoCfg<NG>::H1B];            // layer-1 output, layer-2 broadcast layout
+  float h2[RoCfg<NG>::SL * RoCfg<NG>::H2S];     // layer-2 output [slot][feature]
+  float w3[NA * 256];                           // W3^T [a][f]
+  float b3[8];
+  float x0[NG * 64];                            // normalised input: [g][q][i] = x[slot 4g+i][feature q]
+  float a[RoCfg<NG>::SL * NA];                  // actions [slot][a]
+};
+
+template <int NG, int NS, int NA, int REGK, int LDSK>
+__device__ __forceinline__ void ro_load_actor(const NetView& N, const Lane& L, RoActorRegs<NS, REGK>& R,
+                                              RoActorLds<NG, NA, LDSK>& W) {
+  const float* W1 = N.flat + N.t.woff[0];
+  const float* W2 = N.flat + N.t.woff[1];
+  const float* W3 = N.flat + N.t.woff[2];
+  const int f = 64 * L.wave + L.lane;
+#pragma unroll
+  for (int k = 0; k < REGK; ++k) R.w2[k] = W2[k * 256 + f];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) R.w1[q] = W1[q * 256 + f];
+  R.b1 = N.bias(0, f);
+  R.b2 = N.bias(1, f);
+  for (int e = L.tid; e < LDSK * 64; e += CACTO_THREADS) {
+    const int lane = e & 63, w = (e >> 6) & 3, kq = e >> 8;
+    const int k = REGK + 4 * kq, col = 64 * w + lane;
+    W.w2[e] = make_float4(W2[k * 256 + col], W2[(k + 1) * 256 + col], W2[(k + 2) * 256 + col], W2[(k + 3) * 256 + col]);
+  }
+  for (int e = L.tid; e < NA * 256; e += CACTO_THREADS) W.w3[e] = W3[(e & 255) * NA + (e >> 8)];
+  if (L.tid < 8) W.b3[L.tid] = L.tid < NA ? N.bias(2, L.tid) : 0.f;
+}
+
+__device__ __forceinline__ float lrelu(float z) { return z > 0.f ? z : fmul(z, 0.3f); }
+
+// Actor forward of the workgroup's SL slots: x0 -> h1 -> h2 -> a. Contains 3 barriers (the last
+// one publishes W.a).
+template <int NG, int NS, int NA, int REGK, int LDSK>
+__device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActorLds<NG, NA, LDSK>& W,
+                                         const float* __restrict__ W2g, const Lane& L) {
+  using C = RoCfg<NG>;
+  // ---- layer 1 (K = NS): one activation VGPR per group covers every k
+  {
+    floatx4 acc[NG];
+    float x[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+      x[g] = W.x0[g * 64 + L.lane];
+    }
+    static_for<NS>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acc[g] = mfma_bc<q>(x[g], R.w1[q], acc[g]);
+    });
+    // feature k = 64 wave + lane of sample 4g + i -> h1 block (g, kb = wave), q = lane & 15, v = lane >> 4
+    const int q = L.lane & 15, v = L.lane >> 4;
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) W.h1[(g * 4 + L.wave) * C::H1B + q * 20 + 4 * i + v] = lrelu(fadd(acc[g][i], R.b1));
+  }
+  __syncthreads();
+  // ---- layer 2 (K = 256): k = 64 kb + 16 v + q; lane 4q+i reads {x[i][64kb + 16v + q], v = 0..3}
+  {
+    floatx4 acc[NG][2];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[g][0] = acc[g][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int rd = (L.lane >> 2) * 20 + 4 * (L.lane & 3);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      float4 xv[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) xv[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb) * C::H1B + rd]);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int k0 = 64 * kb + 16 * v;  // a 16-row block lies in one residence region
+        float4 wl[4];
+        float wg[16];
+        if (k0 >= REGK && k0 < REGK + LDSK) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) wl[qq] = W.w2[(((k0 - REGK) / 4 + qq) * 4 + L.wave) * 64 + L.lane];
+        } else if (k0 >= REGK + LDSK) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) wg[q] = W2g[(k0 + q) * 256 + 64 * L.wave + L.lane];
+        }
+        static_for<16>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          const int k = k0 + q;
+          const float w = k < REGK ? R.w2[k < REGK ? k : 0] : k < REGK + LDSK ? get4(wl[q >> 2], q & 3) : wg[q];
+#pragma unroll
+          for (int g = 0; g < NG; ++g) acc[g][q & 1] = mfma_bc<q>(get4(xv[g], v), w, acc[g][q & 1]);
+        });
+      }
+    }
+    const int f = 64 * L.wave + L.lane;
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        W.h2[(4 * g + i) * C::H2S + f] = lrelu(fadd(fadd(acc[g][0][i], acc[g][1][i]), R.b2));
+  }
+  __syncthreads();
+  // ---- layer 3 (256 -> NA): one summation order for every NG (so the schedule never changes a
+  //      result): 64 partial chains, chain j = features j, j + 64, j + 128, j + 192 (FMA in that
+  //      order), combined by a butterfly over j with offsets 32, 16, ..., 1. Thread (slot s,
+  //      segment seg) holds chains seg + P r (r < NG); the offsets >= P are the in-thread steps.
+  {
+    constexpr int NR = 64 / C::P;  // == NG
+    const int s = L.tid / C::P, seg = L.tid % C::P;
+    float pa[NA][NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) pa[a][r] = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int f = seg + C::P * r + 64 * m;
+        const float h = W.h2[s * C::H2S + f];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) pa[a][r] = fmaf(W.w3[a * 256 + f], h, pa[a][r]);
+      }
+    }
+#pragma unroll
+    for (int half = NR / 2; half >= 1; half >>= 1)
+#pragma unroll
+      for (int r = 0; r < half; ++r)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) pa[a][r] = pa[a][r] + pa[a][r + half];
+#pragma unroll
+    for (int off = C::P / 2; off >= 1; off >>= 1)
+#pragma unroll
+      for (int a = 0; a < NA; ++a) pa[a][0] += __shfl_xor(pa[a][0], off);
+    if (seg == 0)
+#pragma unroll
+      for (int a = 0; a < NA; ++a) W.a[s * NA + a] = fadd(pa[a][0], W.b3[a]);
+  }
+  __syncthreads();
+}
+
+// Chain dynamics workspace of the rollout, structure of arrays [joint][component][slot] (slot
+// fastest: the slot lanes of a wave read consecutive doubles). The joint placements X(q_i) of every
+// (slot, joint) are computed in parallel by all threads; the RNEA and CRBA recursions then read
+// them (and park their per-joint forces / composite inertias) here instead of holding NJ of each
+// in registers — a 6-joint chain in float64 would otherwise not fit beside the actor.
+template <int NJ, int SL>
+struct RoChain {
+  static constexpr int J = NJ > 0 ? NJ : 1;
+  double X[J * 12 * SL];   // SE3: R (9, row-major), p (3)
+  double f[J * 6 * SL];    // RNEA forces: l (3), a (3)
+  double Ic[J * 10 * SL];  // CRBA composite inertias: m, h (3), Io (6)
+};
+
+template <int SL>
+__device__ __forceinline__ void se3_st(double* b, const SE3& X) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) b[k * SL] = X.R.m[k];
+  b[9 * SL] = X.p.x;
+  b[10 * SL] = X.p.y;
+  b[11 * SL] = X.p.z;
+}
+template <int SL>
+__device__ __forceinline__ SE3 se3_ld(const double* b) {
+  SE3 X;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) X.R.m[k] = b[k * SL];
+  X.p = v3(b[9 * SL], b[10 * SL], b[11 * SL]);
+  return X;
+}
+template <int SL>
+__device__ __forceinline__ void sv_st(double* b, const SV& v) {
+  b[0] = v.l.x, b[SL] = v.l.y, b[2 * SL] = v.l.z;
+  b[3 * SL] = v.a.x, b[4 * SL] = v.a.y, b[5 * SL] = v.a.z;
+}
+template <int SL>
+__device__ __forceinline__ SV sv_ld(const double* b) {
+  return SV{v3(b[0], b[SL], b[2 * SL]), v3(b[3 * SL], b[4 * SL], b[5 * SL])};
+}
+template <int SL>
+__device__ __forceinline__ void inertia_st(double* b, const Inertia& I) {
+  b[0] = I.m;
+  b[SL] = I.h.x, b[2 * SL] = I.h.y, b[3 * SL] = I.h.z;
+  b[4 * SL] = I.Io.xx, b[5 * SL] = I.Io.xy, b[6 * SL] = I.Io.xz;
+  b[7 * SL] = I.Io.yy, b[8 * SL] = I.Io.yz, b[9 * SL] = I.Io.zz;
+}
+template <int SL>
+__device__ __forceinline__ Inertia inertia_ld(const double* b) {
+  Inertia I;
+  I.m = b[0];
+  I.h = v3(b[SL], b[2 * SL], b[3 * SL]);
+  I.Io = S3{b[4 * SL], b[5 * SL], b[6 * SL], b[7 * SL], b[8 * SL], b[9 * SL]};
+  return I;
+}
+
+// X(q_i) of every active (slot, joint): item e -> slot e % SL, joint e / SL, spread over the waves.
+template <int NJ, int SL>
+__device__ __forceinline__ void ro_placements(const SysDevice& sd, RoChain<NJ, SL>& C, const double* sS,
+                                              const int* sact, const Lane& L) {
+  constexpr int ns = Dims<NJ>::NS;
+  const int e = (L.tid & 63) * 4 + L.wave;  // consecutive items on different waves
+  if (e < SL * NJ) {
+    const int c = e % SL, i = e / SL;
+    if (sact[c]) se3_st<SL>(C.X + i * 12 * SL + c, joint_placement(JointView{sd.joints + i * CACTO_JOINT_COLS}, sS[c * ns + i]));
+  }
+}
+
+// Joint loops: unrolled for short chains; a 6-joint chain keeps one joint's values live at a time.
+#define RO_JU (NJ <= 3 ? NJ : 1)
+
+// chain_nle (env.h) with X from the workspace and the forces parked there: same operations in the
+// same order, so h is bit-identical.
+template <int NJ, int SL>
+__device__ __forceinline__ void ro_chain_nle(const SysDevice& sd, RoChain<NJ, SL>& C, int c, const double* q,
+                                             const double* v, double* hout) {
+  const SV gacc{v3(-sd.p.gravity[0], -sd.p.gravity[1], -sd.p.gravity[2]), v3(0, 0, 0)};
+  SV vp{v3(0, 0, 0), v3(0, 0, 0)}, ap = gacc, fc;
+#pragma unroll RO_JU
+  for (int i = 0; i < NJ; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    const SE3 X = se3_ld<SL>(C.X + i * 12 * SL + c);
+    const SV S = joint_S(j);
+    SV vi = act_motion_inv(X, vp);
+    const SV Sq{v[i] * S.l, v[i] * S.a};
+    vi.l = vi.l + Sq.l;
+    vi.a = vi.a + Sq.a;
+    SV ai = act_motion_inv(X, ap);
+    const SV cm = cross_motion(vi, Sq);
+    ai.l = ai.l + cm.l;
+    ai.a = ai.a + cm.a;
+    const Inertia I = j.inertia();
+    const SV Iv = inertia_mul(I, vi);
+    const SV Ia = inertia_mul(I, ai);
+    const SV vf = cross_force(vi, Iv);
+    fc.l = Ia.l + vf.l;
+    fc.a = Ia.a + vf.a;
+    if (i < NJ - 1) sv_st<SL>(C.f + i * 6 * SL + c, fc);
+    vp = vi;
+    ap = ai;
+  }
+#pragma unroll RO_JU
+  for (int i = NJ - 1; i >= 0; --i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    hout[i * SL] = sdot(joint_S(j), fc);
+    if (i > 0) {
+      const SV fp = act_force(se3_ld<SL>(C.X + i * 12 * SL + c), fc);
+      const SV fo = sv_ld<SL>(C.f + (i - 1) * 6 * SL + c);
+      fc.l = fo.l + fp.l;
+      fc.a = fo.a + fp.a;
+    }
+  }
+}
+
+// chain_mass (env.h) from the workspace placements; M written to Mout[k * SL] (k = row-major
+// index). Same operations in the same order.
+template <int NJ, int SL>
+__device__ __forceinline__ void ro_chain_mass(const SysDevice& sd, RoChain<NJ, SL>& C, int c, double* Mout) {
+  Inertia acc = JointView{sd.joints + (NJ - 1) * CACTO_JOINT_COLS}.inertia();
+  inertia_st<SL>(C.Ic + (NJ - 1) * 10 * SL + c, acc);
+#pragma unroll RO_JU
+  for (int i = NJ - 1; i > 0; --i) {
+    Inertia a = JointView{sd.joints + (i - 1) * CACTO_JOINT_COLS}.inertia();
+    add_inertia(a, act_inertia(se3_ld<SL>(C.X + i * 12 * SL + c), acc));
+    acc = a;
+    if (i > 1) inertia_st<SL>(C.Ic + (i - 1) * 10 * SL + c, acc);
+  }
+#pragma unroll RO_JU
+  for (int i = 0; i < NJ; ++i) {
+    JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    SV F = inertia_mul(i == 0 ? acc : inertia_ld<SL>(C.Ic + i * 10 * SL + c), joint_S(j));
+    Mout[(i * NJ + i) * SL] = sdot(joint_S(j), F);
+#pragma unroll RO_JU
+    for (int k = i; k > 0; --k) {
+      F = act_force(se3_ld<SL>(C.X + k * 12 * SL + c), F);
+      JointView jp{sd.joints + (k - 1) * CACTO_JOINT_COLS};
+      const double mij = sdot(joint_S(jp), F);
+      Mout[(i * NJ + (k - 1)) * SL] = mij;
+      Mout[((k - 1) * NJ + i) * SL] = mij;
+    }
+  }
+}
+
+// Per-episode constant dynamics (prismatic chains, ConstDyn) only for short chains: the 6-joint
+// chain_terms in one thread would not fit beside the actor, and those chains take the per-step
+// RNEA/CRBA path.
+template <int NJ>
+struct RoConstDyn {
+  static constexpr bool ok = NJ > 0 && NJ <= 3;
+};
+
+template <int NJ, int NG>
+struct RoShared {
+  static constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA, SL = RoCfg<NG>::SL;
+  RoActorLds<NG, na, RoSplit<NJ, NG>::LDSK> W;
+  double sS[SL * ns];                                                 // s_t of every slot
+  double MS[NJ > 0 ? SL * NJ * NJ : 1], hS[NJ > 0 ? SL * NJ : 1];    // chain M(q) (or its Cholesky factor), nle: [k][slot]
+  RoChain<NJ, SL> ch;
+  int sb[SL], sn[SL], st[SL], sact[SL];
+  int anyact;
+};
+
+// Slot refill (wave 0; every lane calls it, lanes with `need` take the next queue entries in lane
+// order). A new episode's s_0 goes to the slot's state and the actor input; episodes of length 0
+// are completed on the spot (status 0: RL.py never rolls out NSTEPS_SH == 0).
+template <int NJ, int NG>
+__device__ __forceinline__ void ro_refill(bool need, int c, int& head, RoShared<NJ, NG>& Sh, const SysDevice& sd,
+                                          const double* __restrict__ S0,
+                                          const int32_t* __restrict__ nsteps, const int32_t* __restrict__ order, int T,
+                                          int B, int G, double* __restrict__ Straj, int32_t* __restrict__ status,
+                                          const Lane& L) {
+  constexpr int ns = Dims<NJ>::NS, SL = RoCfg<NG>::SL;
+  const cacto_sys_params& p = sd.p;
+  while (true) {
+    const uint64_t m = __ballot(need);
+    if (m == 0) break;
+    const int rank = __popcll(m & ((1ull << L.lane) - 1ull));
+    const int k = head + rank;
+    head += __popcll(m);
+    if (need) {
+      const int r = k * G + ((k & 1) ? G - 1 - (int)blockIdx.x : (int)blockIdx.x);
+      if (r >= B) {
+        need = false;
+        Sh.sact[c] = 0;
+      } else {
+        const int b = order ? order[r] : r;
+        const int n = min(nsteps[b], T);
+        double s[ns];
+#pragma unroll
+        for (int i = 0; i < ns; ++i) {
+          s[i] = S0[(size_t)b * ns + i];
+          if (Straj) Straj[(size_t)b * (T + 1) * ns + i] = s[i];
+        }
+        if (n == 0) {
+          if (status) status[b] = 0;
+        } else {
+          need = false;
+          Sh.sb[c] = b;
+          Sh.sn[c] = n;
+          Sh.st[c] = 0;
+          Sh.sact[c] = 1;
+#pragma unroll
+          for (int i = 0; i < ns; ++i) Sh.sS[c * ns + i] = s[i];
+#pragma unroll
+          for (int q = 0; q < ns; ++q) Sh.W.x0[(c >> 2) * 64 + 4 * q + (c & 3)] = normalize_feature(p, q, (float)s[q]);
+          if constexpr (RoConstDyn<NJ>::ok) {
+            if (p.const_dyn) {
+              // prismatic chain: M factored once per episode, kept in the slot's MS / hS
+              ConstDyn<NJ> cd;
+                          const_dyn_init<NJ>(sd, s, cd);
+#pragma unroll
+              for (int k = 0; k < NJ * NJ; ++k) Sh.MS[k * SL + c] = cd.L[k];
+#pragma unroll
+              for (int i = 0; i < NJ; ++i) Sh.hS[i * SL + c] = cd.h[i];
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// Wave 0, lane c (< SL): after s' = f(s, a) of slot c: state + next actor input, the trajectory
+// stores of (a_t, s_{t+1}), and the end of the episode (status, slot refill).
+template <int NJ, int NG>
+__device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* sn, const float* a,
+                                           RoShared<NJ, NG>& Sh, const SysDevice& sd, int T,
+                                           double* __restrict__ Straj, float* __restrict__ Atraj,
+                                           int32_t* __restrict__ status) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  const cacto_sys_params& p = sd.p;
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < ns; ++i) {
+    Sh.sS[c * ns + i] = sn[i];
+    bad |= isnan(sn[i]);
+    Sh.W.x0[(c >> 2) * 64 + 4 * i + (c & 3)] = normalize_feature(p, i, (float)sn[i]);
+  }
+  if (Atraj)
+#pragma unroll
+    for (int i = 0; i < na; ++i) Atraj[((size_t)b * T + tc) * na + i] = a[i];
+  if (Straj)
+#pragma unroll
+    for (int i = 0; i < ns; ++i) Straj[((size_t)b * (T + 1) + tc + 1) * ns + i] = sn[i];
+  const int n = Sh.sn[c];
+  if (bad && Straj) {
+    // RL.py:229-231 drops the episode; the rest of its trajectory is NaN (the reward / EE pass
+    // skips NaN states)
+    for (int t = tc + 2; t <= n; ++t)
+#pragma unroll
+      for (int i = 0; i < ns; ++i) Straj[((size_t)b * (T + 1) + t) * ns + i] = __builtin_nan("");
+  }
+  const bool fin = bad || tc + 1 >= n;
+  if (fin) {
+    if (status) status[b] = bad ? 1 : 0;
+  } else {
+    Sh.st[c] = tc + 1;
+  }
+  return fin;
+}
+
+// One workgroup = SL episode slots (lane c < SL of wave 0 <-> slot c). Per step:
+//   actor (4 waves, MFMA, weights stationary)                                -> a (LDS)
+//   wave 0: s' = f(s, a) (chains with configuration-dependent M: RNEA on wave 0 and CRBA on
+//   wave 3 first, then the Cholesky step), the next actor input, the stores of (a_t, s_{t+1}),
+//   finished episodes retired and their slots refilled.
+// Rewards and end-effector positions depend only on (s_t, a_t): k_rollout_rewards computes them
+// for every recorded step afterwards, fully parallel, so the sequential per-step chain is only
+// actor -> dynamics.
+template <int NJ, int NG>
+__global__ void __launch_bounds__(CACTO_THREADS, 1)
+    k_rollout(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
+              const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
+              float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  using C = RoCfg<NG>;
+  constexpr int SL = C::SL;
+  __shared__ RoShared<NJ, NG> Sh;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const Lane L;
+  const int G = gridDim.x;
+  // chains with configuration-dependent M: RNEA (wave 0) and CRBA (wave 3) run concurrently
+  const bool split_dyn = NJ > 0 && !(RoConstDyn<NJ>::ok && p.const_dyn);
+  constexpr int REGK = RoSplit<NJ, NG>::REGK, LDSK = RoSplit<NJ, NG>::LDSK;
+  RoActorRegs<ns, REGK> R;
+  if (use_actor) ro_load_actor<NG, ns, na, REGK, LDSK>(N, L, R, Sh.W);
+  const float* W2g = N.flat + N.t.woff[1];
+  for (int e = L.tid; e < NG * 64; e += CACTO_THREADS) Sh.W.x0[e] = 0.f;
+  if (L.tid < SL) Sh.sact[L.tid] = 0;
+  __syncthreads();
+  int head = 0;  // queue position (wave 0, uniform)
+  if (L.wave == 0) {
+    ro_refill<NJ, NG>(L.lane < SL, L.lane, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, L);
+    const uint64_t m = __ballot(L.lane < SL && Sh.sact[L.lane]);
+    if (L.lane == 0) Sh.anyact = m != 0;
+  }
+  __syncthreads();
+  const int c = L.lane % SL;  // slot of this lane
+  for (int it = 0; Sh.anyact; ++it) {
+    RSTAMP(0);
+    // joint placements of s_t (published by the actor's first barrier)
+    if constexpr (NJ > 0) {
+      if (split_dyn) {
+        ro_placements<NJ, SL>(sd, Sh.ch, Sh.sS, Sh.sact, L);
+        if (!use_actor) __syncthreads();
+      }
+    }
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK>(R, Sh.W, W2g, L);
+    RSTAMP(1);
+    const bool active = L.lane < SL && Sh.sact[c] != 0;
+    if (split_dyn) {
+      if constexpr (NJ > 0) {
+        if (L.wave == 0 && active) {
+          ro_chain_nle<NJ, SL>(sd, Sh.ch, c, Sh.sS + c * ns, Sh.sS + c * ns + NJ, Sh.hS + c);
+        } else if (L.wave == 3 && active) {
+          ro_chain_mass<NJ, SL>(sd, Sh.ch, c, Sh.MS + c);
+        }
+      }
+      __syncthreads();
+    }
+    RSTAMP(2);
+    if (L.wave == 0) {
+      bool fin = false;
+      if (active) {
+        const int b = Sh.sb[c], tc = Sh.st[c];
+        double s[ns], ad[na], sn[ns];
+        float a[na];
+#pragma unroll
+        for (int i = 0; i < ns; ++i) s[i] = Sh.sS[c * ns + i];
+#pragma unroll
+        for (int i = 0; i < na; ++i) {
+          a[i] = use_actor ? Sh.W.a[c * na + i] : 0.f;
+          ad[i] = (double)a[i];
+        }
+        if constexpr (NJ > 0) {
+          if (split_dyn) {
+            double M[NJ * NJ], h[NJ];
+#pragma unroll
+            for (int k = 0; k < NJ * NJ; ++k) M[k] = Sh.MS[k * SL + c];
+#pragma unroll
+            for (int i = 0; i < NJ; ++i) h[i] = Sh.hS[i * SL + c];
+            chain_step<NJ>(sd, s, ad, M, h, sn);
+          } else {
+            ConstDyn<NJ> cd;
+#pragma unroll
+            for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = Sh.MS[k * SL + c];
+#pragma unroll
+            for (int i = 0; i < NJ; ++i) cd.h[i] = Sh.hS[i * SL + c];
+            env_simulate_const<NJ>(sd, cd, s, ad, sn);
+          }
+        } else {
+          env_simulate<NJ>(sd, s, ad, false, sn);
+        }
+        fin = ro_advance<NJ, NG>(c, b, tc, sn, a, Sh, sd, T, Straj, Atraj, status);
+      }
+      ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, L);
+      const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
+      if (L.lane == 0) Sh.anyact = m != 0;
+    }
+    __syncthreads();
+    RSTAMP(3);
+  }
+}
+
+// Rewards and end-effector positions of every recorded step (Env.step's reward and
+// get_end_effector_position, environment.py:70-78, :146-156): one thread per (episode, t),
+// r_t = reward(w, s_t, a_t) for t < n, EE_t = EE(s_t) for t <= n; NaN states (a dropped episode)
+// are skipped.
+template <int NJ>
+__global__ void __launch_bounds__(256) k_rollout_rewards(const SysDevice* __restrict__ sdp, const double* __restrict__ Straj,
+                                                         const float* __restrict__ Atraj, const int32_t* __restrict__ nsteps,
+                                                         int T, int use_actor, const double* __restrict__ Wext,
+                                                         double* __restrict__ Rtraj, double* __restrict__ EEtraj, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  const SysDevice& sd = *sdp;
+  const int64_t total = (int64_t)B * (T + 1);
+  double w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = k >= sd.p.n_weights ? 0.0 : Wext ? Wext[k] : sd.p.w_running[k];
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / (T + 1)), t = (int)(e % (T + 1));
+    const int n = min(nsteps[b], T);
+    if (t > n) continue;
+    double s[ns];
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < ns; ++i) {
+      s[i] = Straj[(size_t)e * ns + i];
+      bad |= isnan(s[i]);
+    }
+    if (bad) continue;
+    if (EEtraj) {
+      const V3 v = env_ee<NJ>(sd, s);
+      EEtraj[(size_t)e * 3 + 0] = v.x;
+      EEtraj[(size_t)e * 3 + 1] = v.y;
+      EEtraj[(size_t)e * 3 + 2] = v.z;
+    }
+    if (Rtraj && t < n) {
+      double a[na];
+#pragma unroll
+      for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)Atraj[((size_t)b * T + t) * na + i] : 0.0;
+      Rtraj[(size_t)b * T + t] = env_reward<NJ>(sd, w, s, a, false);
+    }
+  }
+}
+
+// Episode slots per workgroup and workgroup count for B episodes: about two episodes per slot
+// (their lengths pair up long + short), one workgroup per CU.
+inline int ro_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = v;
+    else
+      cus = 256;
+  }
+  return cus;
+}
+
+}  // namespace cacto
+
+using namespace cacto;
+
+namespace {
+template <int NJ>
+struct LaunchRollout {
+  static int run(const cacto_sys* sys, NetView v, const double* S0, const int32_t* n, int T, int use_actor,
+                 const double* W, double* S, float* A, double* R, double* EE, int32_t* status, const int32_t* order,
+                 int B, int groups, int wgs, hipStream_t st) {
+    const int cus = ro_cus();
+    // the float64 6-joint chain dynamics need the registers that more slots would take
+    constexpr int gmax = 4;
+    if (groups <= 0) {
+      // about two episodes per slot; chains of 4+ joints at least 2 groups (their step time is set
+      // by the per-slot float64 dynamics, nearly independent of the slot count)
+      const int per = B / (2 * 4 * cus);
+      groups = std::min(gmax, per >= 4 ? 4 : per >= 2 ? 2 : NJ >= 4 ? 2 : 1);
+    }
+    if (groups > gmax) {
+      set_error("cacto_rollout_sched: groups above this system's maximum (1 for 6 joints)");
+      return CACTO_EINVAL;
+    }
+    if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 4 * groups));
+    wgs = std::max(1, std::min(wgs, ceil_div(B, 4 * groups)));
+    switch (groups) {
+      case 1:
+        hipLaunchKernelGGL((k_rollout<NJ, 1>), dim3(wgs), dim3(CACTO_THREADS), 0, st, sys->dev, v, S0, n, T, use_actor,
+                           S, A, status, order, B);
+        break;
+      case 2:
+        hipLaunchKernelGGL((k_rollout<NJ, (gmax >= 2 ? 2 : 1)>), dim3(wgs), dim3(CACTO_THREADS), 0, st, sys->dev, v, S0,
+                           n, T, use_actor, S, A, status, order, B);
+        break;
+      case 4:
+        hipLaunchKernelGGL((k_rollout<NJ, (gmax >= 4 ? 4 : 1)>), dim3(wgs), dim3(CACTO_THREADS), 0, st, sys->dev, v, S0,
+                           n, T, use_actor, S, A, status, order, B);
+        break;
+      default:
+        set_error("cacto_rollout_sched: groups must be 1, 2 or 4");
+        return CACTO_EINVAL;
+    }
+    CACTO_CHECK_HIP(hipGetLastError());
+    if (R || EE) {
+      const int64_t total = (int64_t)B * (T + 1);
+      const int grid = (int)std::min<int64_t>((total + 255) / 256, 8 * cus);
+      hipLaunchKernelGGL(k_rollout_rewards<NJ>, dim3(grid), dim3(256), 0, st, sys->dev, S, A, n, T, use_actor, W, R,
+                         EE, B);
+      CACTO_CHECK_HIP(hipGetLastError());
+    }
+    return CACTO_OK;
+  }
+};
+}  // namespace
+
+#ifdef CACTO_STAMPS
+extern "C" int cacto_debug_rollout_stamps(unsigned long long* out_h) {
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 8));
+  return CACTO_OK;
+}
+#endif
+
+extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
+                                   const int32_t* nsteps_d, int T, int use_actor, const double* W_d, double* S_traj_d,
+                                   float* A_traj_d, double* R_traj_d, double* EE_traj_d, int32_t* status_d,
+                                   const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
+  CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
+  CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4, "cacto_rollout_sched: groups must be 0, 1, 2 or 4");
+  CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
+  CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
+                "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");
+  if (B == 0) return CACTO_OK;
+  NetView v = cacto_make_view(sys, CACTO_NET_ACTOR, actor_netbuf_d);
+  return dispatch_nj<LaunchRollout>(sys->host.p, sys, v, S0_d, nsteps_d, T, use_actor, W_d, S_traj_d, A_traj_d,
+                                    R_traj_d, EE_traj_d, status_d, order_d, B, groups, workgroups, as_stream(stream));
+}
+
+extern "C" int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
+                             const int32_t* nsteps_d, int T, int use_actor, const double* W_d, double* S_traj_d,
+                             float* A_traj_d, double* R_traj_d, double* EE_traj_d, int32_t* status_d,
+                             const int32_t* order_d, int B, void* stream) {
+  return cacto_rollout_sched(sys, actor_netbuf_d, S0_d, nsteps_d, T, use_actor, W_d, S_traj_d, A_traj_d, R_traj_d,
+                             EE_traj_d, status_d, order_d, B, 0, 0, stream);
+}

@@ -275,33 +275,37 @@ class RL_AC:
                 torch.as_tensor(nsteps, device=DEVICE).contiguous(), torch.as_tensor(order, device=DEVICE))
 
     def rollout_batch(self, S0, nsteps, T, ep=1, weights=None, want=("S", "A", "R", "EE"), inputs=None, out=None,
-                      actor=None):
-        """Roll out len(S0) episodes in one persistent kernel (K18), episodes packed by length.
-        `actor` (an NN-held network, default self.actor_model) gives the policy."""
+                      actor=None, sched=(0, 0)):
+        """Roll out len(S0) episodes in one persistent kernel (K18); episode slots are refilled
+        longest-first as episodes end. `actor` (an NN-held network, default self.actor_model) gives
+        the policy; `sched` = (groups, workgroups) of cacto_rollout_sched (0 = automatic)."""
         S0, n, order = inputs if inputs is not None else self.rollout_inputs(S0, nsteps)
         R = S0.shape[0]
         ns, na = self.conf.nb_state, self.conf.nb_action
         if out is not None:
-            return self._launch_rollout(S0, n, order, T, ep, weights, out, actor)
+            return self._launch_rollout(S0, n, order, T, ep, weights, out, actor, sched)
         f64 = dict(dtype=torch.float64, device=DEVICE)
         out = {}
-        if "S" in want:
+        # rewards and EE positions are evaluated from the recorded (s_t, a_t) after the rollout
+        need_sa = "R" in want or "EE" in want
+        if "S" in want or need_sa:
             out["S"] = torch.empty(R, T + 1, ns, **f64)
-        if "A" in want:
+        if "A" in want or (need_sa and ep != 0):
             out["A"] = torch.empty(R, T, na, dtype=torch.float32, device=DEVICE)
         if "R" in want:
             out["R"] = torch.empty(R, T, **f64)
         if "EE" in want:
             out["EE"] = torch.empty(R, T + 1, 3, **f64)
         out["status"] = torch.empty(R, dtype=torch.int32, device=DEVICE)
-        return self._launch_rollout(S0, n, order, T, ep, weights, out, actor)
+        return self._launch_rollout(S0, n, order, T, ep, weights, out, actor, sched)
 
-    def _launch_rollout(self, S0, n, order, T, ep, weights, out, actor=None):
+    def _launch_rollout(self, S0, n, order, T, ep, weights, out, actor=None, sched=(0, 0)):
         W = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float64), device=DEVICE)
         actor = self.actor_model if actor is None else actor
-        L.lib().call("cacto_rollout", self.sys.handle, dptr(actor.buf), dptr(S0), dptr(n), T,
+        L.lib().call("cacto_rollout_sched", self.sys.handle, dptr(actor.buf), dptr(S0), dptr(n), T,
                      int(ep != 0), dptr(W), dptr(out.get("S")), dptr(out.get("A")), dptr(out.get("R")),
-                     dptr(out.get("EE")), dptr(out.get("status")), dptr(order), S0.shape[0], stream())
+                     dptr(out.get("EE")), dptr(out.get("status")), dptr(order), S0.shape[0], int(sched[0]),
+                     int(sched[1]), stream())
         return out
 
     def nsteps_sh(self, s0):

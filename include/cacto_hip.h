@@ -221,12 +221,23 @@ int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_updat
  * Outputs (any may be NULL): S_traj [B,T+1,ns] f64, A_traj [B,T,na] f32, R_traj [B,T] f64,
  * EE_traj [B,T+1,3] f64. Steps past nsteps_d[b] are not written. W_d: weights [n_weights] or NULL
  * (running). status_d [B] int32 (optional): 0 ok, 1 NaN state encountered (RL.py:229-231).
- * order_d [B] int32 (optional): workgroup slot k runs episode order_d[k] (a permutation). Passing
- * the episodes sorted by length packs equal-length episodes into the same 16-episode MFMA tile. */
+ * order_d [B] int32 (optional): a permutation of the episodes, longest first (e.g. a stable
+ * argsort of -nsteps). Its ranks are dealt to the workgroups in snake order and each workgroup's
+ * episode slots take them longest first as earlier episodes end, so every slot runs about the same
+ * number of steps. Results do not depend on the order or on the schedule. */
 int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
                   const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
                   double* S_traj_d, float* A_traj_d, double* R_traj_d, double* EE_traj_d,
                   int32_t* status_d, const int32_t* order_d, int B, void* stream);
+
+/* cacto_rollout with an explicit schedule: `groups` 4-episode groups per workgroup (1, 2 or 4;
+ * 0 = automatic: about two episodes per slot) and `workgroups` (0 = one per CU, capped by B).
+ * Same outputs as cacto_rollout for any schedule (tests use it to force slot refills). */
+int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
+                        const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
+                        double* S_traj_d, float* A_traj_d, double* R_traj_d, double* EE_traj_d,
+                        int32_t* status_d, const int32_t* order_d, int B, int groups, int workgroups,
+                        void* stream);
 
 /* ---------------------------------------------------------------- replay ------------------ */
 

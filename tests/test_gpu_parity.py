@@ -349,6 +349,50 @@ def test_rollout_per_step_consistency(system):
     assert (out["status"].cpu().numpy() == 0).all()
 
 
+@pytest.mark.parametrize("system,sched", [("double_integrator", (1, 3)), ("double_integrator", (2, 2)),
+                                          ("manipulator", (4, 1)), ("car_park", (1, 2)), ("ur5", (2, 1))])
+def test_rollout_slot_refill_matches_one_episode_per_slot(system, sched):
+    """Few workgroups force every slot to run several episodes back to back (refill at the step
+    boundary, zero-length episodes completed on the spot); every episode must come out exactly as
+    in a schedule with one episode per slot, and agree with the oracle's step-by-step semantics."""
+    conf, genv, oe, nn, rl = _nets(system, None, seed=4)
+    rng = random.Random(11)
+    n_ep = 45
+    S0 = np.array([oe.reset(rng) for _ in range(n_ep)])
+    ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    ns_[3] = 0
+    ns_[17] = 1
+    T = max(ns_)
+    ref = rl.rollout_batch(S0, ns_, T, sched=(1, n_ep))
+    got = rl.rollout_batch(S0, ns_, T, sched=sched)
+    torch.cuda.synchronize()
+    for k in range(n_ep):
+        n = ns_[k]
+        np.testing.assert_array_equal(got["S"][k, :n + 1].cpu().numpy(), ref["S"][k, :n + 1].cpu().numpy())
+        np.testing.assert_array_equal(got["A"][k, :n].cpu().numpy(), ref["A"][k, :n].cpu().numpy())
+        np.testing.assert_array_equal(got["R"][k, :n].cpu().numpy(), ref["R"][k, :n].cpu().numpy())
+        np.testing.assert_array_equal(got["EE"][k, :n + 1].cpu().numpy(), ref["EE"][k, :n + 1].cpu().numpy())
+    assert (got["status"].cpu().numpy() == 0).all()
+    S, A, R, EE = (got[k].cpu().numpy() for k in ("S", "A", "R", "EE"))
+    actor = rl.actor_model.get_weights()
+    norm = conf.state_norm_arr.astype(np.float64)
+    w = conf.cost_weights_running
+    for k in range(0, n_ep, 5):
+        n = ns_[k]
+        if n == 0:
+            np.testing.assert_array_equal(S[k, 0], S0[k])
+            continue
+        ts = sorted(set([0, n // 2, n - 1]))
+        a_ref = onn.actor_forward(actor, S[k, ts].astype(np.float32).astype(np.float64), norm)
+        bound = F32_TOL * abs_bound("actor", actor, S[k, ts].astype(np.float32).astype(np.float64), norm)
+        assert np.all(np.abs(A[k, ts] - a_ref) <= bound)
+        for t in ts:
+            a = A[k, t].astype(np.float64)
+            np.testing.assert_allclose(S[k, t + 1], oe.simulate(S[k, t], a), rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(R[k, t], oe.reward(w, S[k, t], a), rtol=1e-10, atol=1e-14)
+        np.testing.assert_allclose(EE[k, n], oe.get_end_effector_position(S[k, n]), rtol=1e-12, atol=1e-12)
+
+
 def test_rollout_zero_controls_ep0_exact():
     conf, genv, oe, nn, rl = _nets("double_integrator", None)
     rng = random.Random(6)

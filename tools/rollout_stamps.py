@@ -2,7 +2,7 @@
 CACTO_STAMPS build. Not part of the product path.
 
     python -c "from cacto_amd.build import build_variant; build_variant('libcacto_hip_stamps', ['CACTO_STAMPS'])"
-    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/rollout_stamps.py [system]
+    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/rollout_stamps.py [system [R]]
 """
 import ctypes
 import os
@@ -22,7 +22,8 @@ import bench  # noqa: E402
 def main():
     system = sys.argv[1]
     conf, env, rl = bench.make_learner(system)
-    S0, n = bench.initial_states(env, conf, 4096, seed=0)
+    R = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    S0, n = bench.initial_states(env, conf, R, seed=0)
     T = int(n.max())
     inputs = rl.rollout_inputs(S0, n)
     for _ in range(3):
@@ -31,8 +32,8 @@ def main():
     st = (ctypes.c_ulonglong * 8)()
     L.lib().dll.cacto_debug_rollout_stamps(st)
     t = np.array(st[:4], dtype=np.float64)
-    names = ["actor", "E1 (dynamics | reward terms)", "E2 (reward combine + stores | EE(s') | next input tile)"]
-    print(system, "step cycles %.0f: " % (t[3] - t[0]) + ", ".join("%s %.0f" % (nm, d) for nm, d in zip(names, np.diff(t))))
+    names = ["actor", "E1 (dynamics | reward terms)", "E2 (reward combine + stores + refill | EE(s'))"]
+    print(system, R, "step cycles %.0f: " % (t[3] - t[0]) + ", ".join("%s %.0f" % (nm, d) for nm, d in zip(names, np.diff(t))))
 
 
 if __name__ == "__main__":
