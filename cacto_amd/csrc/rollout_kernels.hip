@@ -644,6 +644,19 @@ using namespace cacto;
 
 namespace {
 template <int NJ>
+struct LaunchRolloutRewards {
+  static int run(const cacto_sys* sys, const double* S, const float* A, const int32_t* n, int T, int use_actor,
+                 const double* W, double* R, double* EE, int B, hipStream_t st) {
+    const int64_t total = (int64_t)B * (T + 1);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8 * ro_cus()));
+    hipLaunchKernelGGL(k_rollout_rewards<NJ>, dim3(grid), dim3(256), 0, st, sys->dev, S, A, n, T, use_actor, W, R,
+                       EE, B);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
+};
+
+template <int NJ>
 struct LaunchRollout {
   static int run(const cacto_sys* sys, NetView v, const double* S0, const int32_t* n, int T, int use_actor,
                  const double* W, double* S, float* A, double* R, double* EE, int32_t* status, const int32_t* order,
@@ -681,13 +694,7 @@ struct LaunchRollout {
         return CACTO_EINVAL;
     }
     CACTO_CHECK_HIP(hipGetLastError());
-    if (R || EE) {
-      const int64_t total = (int64_t)B * (T + 1);
-      const int grid = (int)std::min<int64_t>((total + 255) / 256, 8 * cus);
-      hipLaunchKernelGGL(k_rollout_rewards<NJ>, dim3(grid), dim3(256), 0, st, sys->dev, S, A, n, T, use_actor, W, R,
-                         EE, B);
-      CACTO_CHECK_HIP(hipGetLastError());
-    }
+    if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
     return CACTO_OK;
   }
 };
@@ -715,6 +722,16 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
   NetView v = cacto_make_view(sys, CACTO_NET_ACTOR, actor_netbuf_d);
   return dispatch_nj<LaunchRollout>(sys->host.p, sys, v, S0_d, nsteps_d, T, use_actor, W_d, S_traj_d, A_traj_d,
                                     R_traj_d, EE_traj_d, status_d, order_d, B, groups, workgroups, as_stream(stream));
+}
+
+extern "C" int cacto_rollout_rewards(const cacto_sys* sys, const double* S_traj_d, const float* A_traj_d,
+                                     const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
+                                     double* R_traj_d, double* EE_traj_d, int B, void* stream) {
+  CACTO_REQUIRE(sys && S_traj_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout_rewards: bad arguments");
+  CACTO_REQUIRE(!use_actor || A_traj_d, "cacto_rollout_rewards: use_actor needs A_traj");
+  if (B == 0 || !(R_traj_d || EE_traj_d)) return CACTO_OK;
+  return dispatch_nj<LaunchRolloutRewards>(sys->host.p, sys, S_traj_d, A_traj_d, nsteps_d, T, use_actor, W_d,
+                                           R_traj_d, EE_traj_d, B, as_stream(stream));
 }
 
 extern "C" int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,

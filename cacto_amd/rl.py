@@ -308,6 +308,14 @@ class RL_AC:
                      int(sched[1]), stream())
         return out
 
+    def rollout_rewards(self, out, n, T, ep=1, weights=None):
+        """Rewards / EE positions of a recorded rollout (cacto_rollout_rewards) into out["R"] /
+        out["EE"]: the second kernel of a rollout, launched on its own (bench times it apart)."""
+        W = None if weights is None else torch.as_tensor(np.asarray(weights, dtype=np.float64), device=DEVICE)
+        L.lib().call("cacto_rollout_rewards", self.sys.handle, dptr(out["S"]), dptr(out.get("A")), dptr(n), T,
+                     int(ep != 0), dptr(W), dptr(out.get("R")), dptr(out.get("EE")), out["S"].shape[0], stream())
+        return out
+
     def nsteps_sh(self, s0):
         return self.conf.NSTEPS - int(s0[-1] / self.conf.dt)
 

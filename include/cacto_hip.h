@@ -10,6 +10,7 @@
  *   cacto_env_step         Env.step + get_end_effector_position (float64 rollout semantics)
  *                          environment.py:70-78, :146-156; plot_utils.py:262-264
  *   cacto_rollout          RL_AC.create_TO_init loop RL.py:223-231 / PLOT.rollout plot_utils.py:245-279
+ *   cacto_rollout_rewards  Env.step reward / get_end_effector_position over recorded trajectories
  *   cacto_mlp_pack         (layout transform for the kernels; no reference counterpart)
  *   cacto_actor_forward    NN.eval(actor, s)  NeuralNetwork.py:130-138 (+ utils.py:17-24)
  *   cacto_critic_forward   NN.eval(critic, s)
@@ -221,6 +222,8 @@ int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_updat
  * Outputs (any may be NULL): S_traj [B,T+1,ns] f64, A_traj [B,T,na] f32, R_traj [B,T] f64,
  * EE_traj [B,T+1,3] f64. Steps past nsteps_d[b] are not written. W_d: weights [n_weights] or NULL
  * (running). status_d [B] int32 (optional): 0 ok, 1 NaN state encountered (RL.py:229-231).
+ * R_traj / EE_traj are evaluated from the recorded trajectory after the sequential pass
+ * (cacto_rollout_rewards), so they need S_traj (and A_traj when use_actor).
  * order_d [B] int32 (optional): a permutation of the episodes, longest first (e.g. a stable
  * argsort of -nsteps). Its ranks are dealt to the workgroups in snake order and each workgroup's
  * episode slots take them longest first as earlier episodes end, so every slot runs about the same
@@ -238,6 +241,15 @@ int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netbuf_d, const
                         double* S_traj_d, float* A_traj_d, double* R_traj_d, double* EE_traj_d,
                         int32_t* status_d, const int32_t* order_d, int B, int groups, int workgroups,
                         void* stream);
+
+/* Env.step's reward r_t = reward(W, s_t, a_t) (t < nsteps[b]) and EE_t = EE(s_t) (t <= nsteps[b])
+ * of recorded trajectories (environment.py:70-78, :146-156): S_traj [B,T+1,ns] f64, A_traj
+ * [B,T,na] f32 (ignored, a = 0, when use_actor == 0), outputs R_traj [B,T] / EE_traj [B,T+1,3] f64
+ * (either may be NULL). NaN states (a dropped episode) are skipped. Fully parallel over (b, t);
+ * cacto_rollout calls it when R_traj or EE_traj is requested. */
+int cacto_rollout_rewards(const cacto_sys* sys, const double* S_traj_d, const float* A_traj_d,
+                          const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
+                          double* R_traj_d, double* EE_traj_d, int B, void* stream);
 
 /* ---------------------------------------------------------------- replay ------------------ */
 

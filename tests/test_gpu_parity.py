@@ -279,6 +279,32 @@ def test_rollout_di_known_answer():
         np.testing.assert_allclose(out["R"].cpu().numpy()[k], rR, rtol=1e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize("system", ["double_integrator", "manipulator", "car_park", "ur5"])
+def test_rollout_rewards_separate_launch(system):
+    """cacto_rollout_rewards over a recorded S/A-only rollout gives exactly the R / EE of the
+    combined cacto_rollout call (bench.py launches the two kernels apart)."""
+    conf, genv, oe, nn, rl = _nets(system, None, seed=2)
+    rng = random.Random(5)
+    S0 = np.array([oe.reset(rng) for _ in range(37)])
+    ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    T = max(ns_)
+    ref = rl.rollout_batch(S0, ns_, T)
+    got = rl.rollout_batch(S0, ns_, T, want=("S", "A"))
+    got["R"] = torch.full_like(ref["R"], float("nan"))
+    got["EE"] = torch.full_like(ref["EE"], float("nan"))
+    rl.rollout_rewards(got, torch.as_tensor(np.asarray(ns_, dtype=np.int32), device="cuda"), T)
+    torch.cuda.synchronize()
+    for k, n in enumerate(ns_):
+        np.testing.assert_array_equal(got["R"][k, :n].cpu().numpy(), ref["R"][k, :n].cpu().numpy())
+        np.testing.assert_array_equal(got["EE"][k, :n + 1].cpu().numpy(), ref["EE"][k, :n + 1].cpu().numpy())
+    w = conf.cost_weights_running
+    S, A, R = got["S"].cpu().numpy(), got["A"].cpu().numpy(), got["R"].cpu().numpy()
+    for k in range(0, len(S0), 6):
+        t = ns_[k] // 2
+        np.testing.assert_allclose(R[k, t], oe.reward(w, S[k, t], A[k, t].astype(np.float64)), rtol=1e-10,
+                                   atol=1e-14)
+
+
 @pytest.mark.parametrize("system,tag", [("double_integrator", "di_seed0_final"), ("manipulator", None),
                                         ("car_park", None)])
 def test_policy_eval_returns(system, tag):

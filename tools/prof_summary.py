@@ -14,7 +14,7 @@ import sys
 
 
 def short(name):
-    m = re.match(r"(?:void )?(?:cacto::)?([\w:<>\-]+?)\(", name)
+    m = re.match(r"(?:void )?(?:cacto::)?([\w:<>\-, ]+?)\(", name)
     return m.group(1) if m else name[:80]
 
 
