@@ -235,10 +235,36 @@ def episode_groups(nsteps, max_rows):
     return groups
 
 
-def fill_buffer(rl, conf, roll, env, seed, per=False):
+def ddp_labels(rl, conf, env, roll, K=5):
+    """Sobolev labels dV/dx of every rollout episode by the DDP backward pass (TO.backward_pass,
+    TO.py:119-202, cacto_ddp_backward) along the rollout trajectory — the stand-in for the TO
+    solution the reference labels (the NLP solve is host-side CasADi, out of scope). Returns the
+    labels [R, T+1, ns] f64 (None for systems the kernel does not cover) and its timing."""
+    from cacto_amd.to import TO
+    system = conf.__name__.rsplit(".", 1)[-1][len("conf_"):]
+    if system not in ("single_integrator", "double_integrator", "car"):
+        return None, None
+    to = TO(env, conf, w_S=rl.w_S)
+    S, A = roll["out"]["S"], roll["out"]["A"].double()
+    n = torch.as_tensor(roll["nsteps"].astype(np.int32), device="cuda")
+    out = to.backward_pass_batch(S, A, n)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(K):
+        to.backward_pass_batch(S, A, n, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / K
+    steps = int(roll["nsteps"].sum())
+    return out, dict(kernel="k_ddp_backward", ms_per_call=ms, episodes=len(roll["nsteps"]), riccati_steps=steps,
+                     steps_per_s=steps / (ms * 1e-3), source="rollout trajectories (TO NLP solve is host-side)")
+
+
+def fill_buffer(rl, conf, roll, env, seed, per=False, dVdx=None):
     """Replay rows from the rollouts on the device: RL_Solve n-step targets fused with the ring add
-    (cacto_rl_solve_add), rewards = the rollout rewards + terminal reward, dVdx synthetic N(0,1).
-    Episodes go in groups of <= 8192 rows until the ring has wrapped once, so `full` latches."""
+    (cacto_rl_solve_add), rewards = the rollout rewards + terminal reward, dVdx = the DDP labels
+    when given, else synthetic N(0,1). Episodes go in groups of <= 8192 rows until the ring has
+    wrapped once, so `full` latches."""
     from cacto_amd.replay_buffer import PrioritizedReplayBuffer, ReplayBuffer
     buf = PrioritizedReplayBuffer(conf, rl.sys) if per else ReplayBuffer(conf, rl.sys)
     S, R, nsteps = roll["out"]["S"], roll["out"]["R"], roll["nsteps"]
@@ -248,7 +274,8 @@ def fill_buffer(rl, conf, roll, env, seed, per=False):
     added = 0
     while added < conf.REPLAY_SIZE + 8192:
         for lo, hi in episode_groups(nsteps, 8192):
-            dV = torch.randn(hi - lo, S.shape[1], S.shape[2], dtype=torch.float64, device="cuda", generator=gen)
+            dV = dVdx[lo:hi] if dVdx is not None else torch.randn(hi - lo, S.shape[1], S.shape[2],
+                                                                  dtype=torch.float64, device="cuda", generator=gen)
             buf.add_episodes(S[lo:hi], R[lo:hi], nsteps[lo:hi], R_term=R_term[lo:hi], dVdx=dV)
             added += int((nsteps[lo:hi] + 1).sum())
             if added >= conf.REPLAY_SIZE + 8192:
@@ -256,7 +283,7 @@ def fill_buffer(rl, conf, roll, env, seed, per=False):
     return buf
 
 
-def episode_to_buffer_phase(rl, conf, roll, env, K):
+def episode_to_buffer_phase(rl, conf, roll, env, K, dVdx=None):
     """The whole rollout batch through cacto_rl_solve_add into one ring that holds it (RL_Solve +
     buffer.add for every episode of a create_TO_init batch). Returns rows/s and the kernel's
     algorithmic bandwidth: per row it reads s and dVdx (8*ns each) and r (8), writes 8*(3ns+3)."""
@@ -268,7 +295,7 @@ def episode_to_buffer_phase(rl, conf, roll, env, K):
     buf = ReplayBuffer(c, rl.sys)
     S, R = roll["out"]["S"], roll["out"]["R"]
     R_term = terminal_rewards(env, conf, roll)
-    dV = torch.randn(S.shape, dtype=torch.float64, device="cuda")
+    dV = dVdx if dVdx is not None else torch.randn(S.shape, dtype=torch.float64, device="cuda")
     buf.add_episodes(S, R, nsteps, R_term=R_term, dVdx=dV)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -420,8 +447,9 @@ def main():
     # the dominant kernel is the sequential pass (k_rollout); its own HIP-event time
     achieved = roll["steps_per_call"] * fa_flops(ns, na) / (roll["seq_kernel_ms"] * 1e-3)
     diag = None if args.no_diagnostics else rollout_diagnostics(rl, conf, roll)
-    buf = fill_buffer(rl, conf, roll, env, seed=rank)
-    e2b = episode_to_buffer_phase(rl, conf, roll, env, 5)
+    labels, ddp = ddp_labels(rl, conf, env, roll)
+    buf = fill_buffer(rl, conf, roll, env, seed=rank, dVdx=labels)
+    e2b = episode_to_buffer_phase(rl, conf, roll, env, 5, dVdx=labels)
     updates = {}
     for B in [int(b) for b in args.batches.split(",") if b]:
         K = args.update_steps
@@ -452,7 +480,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32 (MLP, MFMA) / f64 (dynamics)",
             "data": "synthetic: Env.reset initial states (random.seed(rank)), reference DI seed-0 weights, "
-                    "N(0,1) dVdx labels",
+                    "dVdx labels from the DDP backward pass along the rollouts (cacto_ddp_backward)",
             "config": {"workload": "double_integrator, w-S=1e-2, %d rollouts per GPU (BASELINE configs[1])"
                                    % args.rollouts,
                        "system": args.system, "rollouts_per_gpu": args.rollouts,
@@ -466,6 +494,7 @@ def main():
                          "env_steps_per_launch": roll["steps_per_call"]},
             "critic_updates": updates,
             "episode_to_buffer": e2b,
+            "ddp_labels": ddp,
             "rollout_diagnostics": diag,
             "cpu_baseline": cpu,
             "extra_systems": extra,

@@ -77,6 +77,7 @@ _SIGS = {
     "cacto_rollout_sched": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int,
                                       C.c_int, C.c_int, vp]),
     "cacto_rollout_rewards": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int, vp]),
+    "cacto_ddp_backward": (C.c_int, [vp, vp, i64, vp, i64, vp, C.c_int, C.c_double, vp, vp]),
     "cacto_buffer_add": (C.c_int, [vp, vp, i64, i64, vp, i64, vp]),
     "cacto_rl_solve_add": (C.c_int, [vp, vp, i64, vp, i64, vp, vp, vp, C.c_int, C.c_int, i64, C.c_int, C.c_int, vp,
                                      i64, i64, vp, vp]),

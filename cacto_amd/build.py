@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "libcacto_hip.so")
 ARCH = os.environ.get("CACTO_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=" + ARCH,
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
-SOURCES = ["core.hip", "env_kernels.hip", "net_kernels.hip", "rollout_kernels.hip", "learn_kernels.hip", "replay_kernels.hip"]
+SOURCES = ["core.hip", "env_kernels.hip", "net_kernels.hip", "rollout_kernels.hip", "ddp_kernels.hip", "learn_kernels.hip", "replay_kernels.hip"]
 
 
 def hipcc():

@@ -1,0 +1,372 @@
+// Sobolev labels without CasADi: the DDP backward pass of TO.backward_pass
+// (TO.py:119-202) along recorded trajectories, on the GPU.
+//
+// Per episode (one thread; the recursion is sequential in t, episodes are independent):
+//   V_x, V_xx      = d/dx, d2/dx2 of the terminal reward at x_T            (TO.py:166-168)
+//   for i = T-1 .. 0:
+//     A, B         = augmented_derivative(x_i, u_i)                        (environment.py:111-132,
+//                                                                            SI :221-233, Car :420-435)
+//     l_x, l_xx, l_u, l_uu of the running reward (l_xu = 0: the cost separates in x and u)
+//     Q_x = l_x + A^T V_x   Q_u = l_u + B^T V_x   Q_xx = l_xx + A^T V_xx A
+//     Q_uu = l_uu + B^T V_xx B   Q_xu = A^T V_xx B   (TO.py:182-186)
+//     V_x = Q_x - Q_xu Qbar^-1 Q_u,  V_xx = Q_xx - Q_xu Qbar^-1 Q_xu^T, Qbar = Q_uu + mu I (:188-194)
+// The reference differentiates the TO cost (environment_TO.py, = -reward) symbolically with CasADi;
+// here the planar-family derivatives are closed forms of the same expression (ellipses and the
+// peak term as softplus of their arguments: d softplus(z)/dz = sigmoid(z)). Qbar is inverted by
+// Gauss-Jordan with partial pivoting (np.linalg.pinv in the reference equals the inverse for the
+// nonsingular, mu-regularised Qbar): float64 results within 1e-9 relative of the oracle.
+//
+// Supported: the planar-cost systems with closed-form Jacobians — single integrator (NJ = 0), car
+// (NJ = -1) and prismatic Pinocchio chains (the double integrator: M and nle constant, so
+// ddq_dq = ddq_dv = 0 and Fu = dt [0; M^-1]). Others return CACTO_EUNSUPPORTED.
+#include "internal.h"
+
+namespace cacto {
+
+template <int NJ>
+struct DdpDims {
+  static constexpr int N = Dims<NJ>::NS - 1, M = Dims<NJ>::NA;
+  static constexpr bool ok = NJ == 0 || NJ == -1 || NJ == 2;
+};
+
+// Reward derivatives w.r.t. the EE position p = (px, py) of the planar family (environment_TO.py
+// :208-234 DI, :90-111 SI, :339-360 Car; reward = -cost), without the scale factor.
+struct PosDerivs {
+  double g[2];
+  double H[3];  // xx, xy, yy
+};
+
+__device__ inline void planar_pos_derivs(const cacto_sys_params& p, const double* w, double px, double py, PosDerivs& d) {
+  const double dx = px - p.target[0], dy = py - p.target[1];
+  // - w0 * dist
+  d.g[0] = -w[0] * (2.0 * dx);
+  d.g[1] = -w[0] * (2.0 * dy);
+  d.H[0] = -w[0] * 2.0;
+  d.H[1] = 0.0;
+  d.H[2] = -w[0] * 2.0;
+  // + w1 * peak, peak = softplus(-alpha2 s) / alpha2, s = sqrt(dx2+.1) - .1 + sqrt(dy2+.1) - .1 - 2 sqrt(.1)
+  {
+    const double rx = sqrt(dx * dx + 0.1), ry = sqrt(dy * dy + 0.1);
+    const double s = rx - 0.1 + ry - 0.1 - 2.0 * sqrt(0.1);
+    const double sg = 1.0 / (1.0 + exp(p.alpha2 * s));  // sigmoid(-alpha2 s)
+    const double sx = dx / rx, sy = dy / ry;
+    const double k2 = p.alpha2 * sg * (1.0 - sg);
+    d.g[0] += w[1] * (-sg * sx);
+    d.g[1] += w[1] * (-sg * sy);
+    d.H[0] += w[1] * (-sg * (0.1 / (rx * rx * rx)) + k2 * sx * sx);
+    d.H[1] += w[1] * (k2 * sx * sy);
+    d.H[2] += w[1] * (-sg * (0.1 / (ry * ry * ry)) + k2 * sy * sy);
+  }
+  // - w_{3+k} * ell_k, ell = softplus(alpha (1 - e)) / alpha, e = (dx/a)^2 + (dy/b)^2
+  for (int k = 0; k < 3; ++k) {
+    const double a = p.obs[6 + 2 * k] / 2, b = p.obs[7 + 2 * k] / 2;
+    const double ex = px - p.obs[2 * k], ey = py - p.obs[2 * k + 1];
+    const double e = (ex * ex) / (a * a) + (ey * ey) / (b * b);
+    const double sg = 1.0 / (1.0 + exp(-(p.alpha * -(e - 1.0))));
+    const double gx = 2.0 * ex / (a * a), gy = 2.0 * ey / (b * b);
+    const double k2 = p.alpha * sg * (1.0 - sg);
+    const double wk = w[3 + k];
+    d.g[0] -= wk * (-sg * gx);
+    d.g[1] -= wk * (-sg * gy);
+    d.H[0] -= wk * (-sg * (2.0 / (a * a)) + k2 * gx * gx);
+    d.H[1] -= wk * (k2 * gx * gy);
+    d.H[2] -= wk * (-sg * (2.0 / (b * b)) + k2 * gy * gy);
+  }
+}
+
+// l_x [N], l_xx [N*N] of the reward with weights w at state x (time excluded).
+template <int NJ>
+__device__ inline void ddp_lx(const SysDevice& sd, const double* w, const double* x, double* lx, double* lxx) {
+  constexpr int N = DdpDims<NJ>::N;
+  const cacto_sys_params& p = sd.p;
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) lxx[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) lx[k] = 0.0;
+  PosDerivs d;
+  planar_pos_derivs(p, w, x[0], x[1], d);  // p_ee = (x0, x1): SI / car states, DI q (unit prismatic axes)
+  lx[0] = p.scale * d.g[0];
+  lx[1] = p.scale * d.g[1];
+  lxx[0] = p.scale * d.H[0];
+  lxx[1] = lxx[N] = p.scale * d.H[1];
+  lxx[N + 1] = p.scale * d.H[2];
+  if constexpr (NJ > 0) {
+    // DI: - w2 * |v|^2 (environment_TO.py:227-230)
+#pragma unroll
+    for (int i = NJ; i < N; ++i) {
+      lx[i] = p.scale * (-w[2] * (2.0 * x[i]));
+      lxx[i * N + i] = p.scale * (-w[2] * 2.0);
+    }
+  }
+}
+
+// Discrete dynamics Jacobians A [N*N], B [N*M] (augmented_derivative).
+template <int NJ>
+__device__ inline void ddp_jacobians(const SysDevice& sd, const double* x, const double* Minv, double* A, double* B) {
+  constexpr int N = DdpDims<NJ>::N, M = DdpDims<NJ>::M;
+  const double dt = sd.p.dt;
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) A[k] = (k % (N + 1) == 0) ? 1.0 : 0.0;
+#pragma unroll
+  for (int k = 0; k < N * M; ++k) B[k] = 0.0;
+  if constexpr (NJ == 0) {
+    B[0 * M + 0] = dt;
+    B[1 * M + 1] = dt;
+  } else if constexpr (NJ == -1) {
+    const double s2 = sin(x[2]), c2 = cos(x[2]);
+    A[0 * N + 2] = -dt * x[3] * s2 - dt * dt * x[4] * s2 / 2;
+    A[0 * N + 3] = dt * c2;
+    A[0 * N + 4] = dt * dt * c2 / 2;
+    A[1 * N + 2] = dt * x[3] * c2 + dt * dt * x[4] * c2 / 2;
+    A[1 * N + 3] = dt * s2;
+    A[1 * N + 4] = dt * dt * s2 / 2;
+    A[3 * N + 4] = dt;
+    B[2 * M + 0] = dt;
+    B[4 * M + 1] = dt;
+  } else {
+    constexpr int nv = NJ > 0 ? NJ : 1;
+#pragma unroll
+    for (int i = 0; i < nv; ++i) A[i * N + nv + i] = dt;  // I + dt [[0, I], [ddq_dq = 0, ddq_dv = 0]]
+#pragma unroll
+    for (int i = 0; i < nv; ++i)
+#pragma unroll
+      for (int j = 0; j < M; ++j) B[(nv + i) * M + j] = Minv[i * M + j] * dt;
+  }
+}
+
+// In-place inverse of a small matrix (Gauss-Jordan, partial pivoting).
+template <int M>
+__device__ inline void small_inverse(double* a, double* inv) {
+#pragma unroll
+  for (int i = 0; i < M * M; ++i) inv[i] = (i % (M + 1) == 0) ? 1.0 : 0.0;
+#pragma unroll
+  for (int c = 0; c < M; ++c) {
+    int piv = c;
+    double best = fabs(a[c * M + c]);
+#pragma unroll
+    for (int r = c + 1; r < M; ++r)
+      if (fabs(a[r * M + c]) > best) {
+        best = fabs(a[r * M + c]);
+        piv = r;
+      }
+#pragma unroll
+    for (int r = 0; r < M; ++r)  // swap rows c and piv (branch-free over the fixed row set)
+      if (r == piv && r != c)
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          double t = a[c * M + k];
+          a[c * M + k] = a[r * M + k];
+          a[r * M + k] = t;
+          t = inv[c * M + k];
+          inv[c * M + k] = inv[r * M + k];
+          inv[r * M + k] = t;
+        }
+    const double d = 1.0 / a[c * M + c];
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+      a[c * M + k] *= d;
+      inv[c * M + k] *= d;
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      if (r != c) {
+        const double f = a[r * M + c];
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          a[r * M + k] -= f * a[c * M + k];
+          inv[r * M + k] -= f * inv[c * M + k];
+        }
+      }
+  }
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
+                                                      int64_t ldS, const double* __restrict__ U, int64_t ldU,
+                                                      const int32_t* __restrict__ nsteps, int n_ep, double mu,
+                                                      double* __restrict__ dVdx) {
+  constexpr int N = DdpDims<NJ>::N, M = DdpDims<NJ>::M, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_ep) return;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const int Te = nsteps[e];
+  const double* Se = S + (size_t)e * ldS * ns;
+  const double* Ue = U + (size_t)e * ldU * na;
+  double* Oe = dVdx + (size_t)e * ldS * ns;
+  double Minv[NJ > 0 ? M * M : 1];
+  if constexpr (NJ > 0) {
+    // prismatic chain: M constant; its inverse once per episode
+    double Mm[M * M], q[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) q[i] = Se[i];
+    chain_mass<NJ>(sd, q, Mm);
+    small_inverse<M>(Mm, Minv);
+  }
+  double w_run[7], w_term[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    w_run[k] = p.w_running[k];
+    w_term[k] = p.w_terminal[k];
+  }
+  double Vx[N], Vxx[N * N], x[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) x[k] = Se[(size_t)Te * ns + k];
+  ddp_lx<NJ>(sd, w_term, x, Vx, Vxx);
+#pragma unroll
+  for (int k = 0; k < N; ++k) Oe[(size_t)Te * ns + k] = Vx[k];
+  Oe[(size_t)Te * ns + N] = 0.0;
+  for (int i = Te - 1; i >= 0; --i) {
+    double u[M], A[N * N], B[N * M], lx[N], lxx[N * N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = Se[(size_t)i * ns + k];
+#pragma unroll
+    for (int k = 0; k < M; ++k) u[k] = Ue[(size_t)i * na + k];
+    ddp_jacobians<NJ>(sd, x, Minv, A, B);
+    ddp_lx<NJ>(sd, w_run, x, lx, lxx);
+    // Q_x = l_x + A^T V_x, Q_u = l_u + B^T V_x
+    double Qx[N], Qu[M], Qxx[N * N], Quu[M * M], Qxu[N * M], VA[N * N], VB[N * M];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) s += A[k * N + r] * Vx[k];
+      Qx[r] = lx[r] + s;
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      // l_u, l_uu: - w6 * (u^2 + w_b (u / u_max)^10) (bound_control_cost, environment_TO.py:201-206)
+      const double um = p.u_max[j];
+      const double lu = p.scale * (-w_run[6] * (2.0 * u[j] + p.w_b * 10.0 * pow(u[j] / um, 9.0) / um));
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) s += B[k * M + j] * Vx[k];
+      Qu[j] = lu + s;
+    }
+    // V_xx A, V_xx B
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+#pragma unroll
+      for (int c = 0; c < N; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += Vxx[r * N + k] * A[k * N + c];
+        VA[r * N + c] = s;
+      }
+#pragma unroll
+      for (int c = 0; c < M; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += Vxx[r * N + k] * B[k * M + c];
+        VB[r * M + c] = s;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+#pragma unroll
+      for (int c = 0; c < N; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += A[k * N + r] * VA[k * N + c];
+        Qxx[r * N + c] = lxx[r * N + c] + s;
+      }
+#pragma unroll
+      for (int c = 0; c < M; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += A[k * N + r] * VB[k * M + c];
+        Qxu[r * M + c] = s;  // + l_xu = 0
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+      for (int c = 0; c < M; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += B[k * M + r] * VB[k * M + c];
+        const double um = p.u_max[r];
+        const double luu = r == c ? p.scale * (-w_run[6] * (2.0 + p.w_b * 90.0 * pow(u[r] / um, 8.0) / (um * um))) : 0.0;
+        Quu[r * M + c] = luu + s + (r == c ? mu : 0.0);
+      }
+    double Qi[M * M];
+    small_inverse<M>(Quu, Qi);
+    // K = Qbar^-1 Q_xu^T [M x N], k = Qbar^-1 Q_u [M]
+    double Kk[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) s += Qi[r * M + k] * Qu[k];
+      Kk[r] = s;
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) s += Qxu[r * M + k] * Kk[k];
+      Vx[r] = Qx[r] - s;
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      double QK[M];  // row r of Q_xu Qbar^-1
+#pragma unroll
+      for (int c = 0; c < M; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) s += Qxu[r * M + k] * Qi[k * M + c];
+        QK[c] = s;
+      }
+#pragma unroll
+      for (int c = 0; c < N; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) s += QK[k] * Qxu[c * M + k];
+        Vxx[r * N + c] = Qxx[r * N + c] - s;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) Oe[(size_t)i * ns + k] = Vx[k];
+    Oe[(size_t)i * ns + N] = 0.0;
+  }
+}
+
+}  // namespace cacto
+
+using namespace cacto;
+
+namespace {
+template <int NJ>
+struct LaunchDdp {
+  static int run(const cacto_sys* sys, const double* S, int64_t ldS, const double* U, int64_t ldU, const int32_t* n,
+                 int n_ep, double mu, double* out, hipStream_t st) {
+    if constexpr (!DdpDims<NJ>::ok) {
+      set_error("cacto_ddp_backward: supported for the single integrator, car and prismatic chains (double integrator)");
+      return CACTO_EUNSUPPORTED;
+    } else {
+      if (NJ > 0 && !sys->host.p.const_dyn) {
+        set_error("cacto_ddp_backward: chains need ABA derivatives (only prismatic chains are supported)");
+        return CACTO_EUNSUPPORTED;
+      }
+      if (sys->host.p.reward_kind != CACTO_REW_PLANAR) {
+        set_error("cacto_ddp_backward: planar-family costs only");
+        return CACTO_EUNSUPPORTED;
+      }
+      hipLaunchKernelGGL(k_ddp_backward<NJ>, dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS, U, ldU, n,
+                         n_ep, mu, out);
+      CACTO_CHECK_HIP(hipGetLastError());
+      return CACTO_OK;
+    }
+  }
+};
+}  // namespace
+
+extern "C" int cacto_ddp_backward(const cacto_sys* sys, const double* S_traj_d, int64_t ldS, const double* U_traj_d,
+                                  int64_t ldU, const int32_t* nsteps_d, int n_ep, double mu, double* dVdx_d,
+                                  void* stream) {
+  CACTO_REQUIRE(sys && S_traj_d && U_traj_d && nsteps_d && dVdx_d && n_ep >= 0 && ldS >= 1 && ldU >= 0,
+                "cacto_ddp_backward: bad arguments");
+  if (n_ep == 0) return CACTO_OK;
+  return dispatch_nj<LaunchDdp>(sys->host.p, sys, S_traj_d, ldS, U_traj_d, ldU, nsteps_d, n_ep, mu, dVdx_d,
+                                as_stream(stream));
+}

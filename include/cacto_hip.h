@@ -11,6 +11,7 @@
  *                          environment.py:70-78, :146-156; plot_utils.py:262-264
  *   cacto_rollout          RL_AC.create_TO_init loop RL.py:223-231 / PLOT.rollout plot_utils.py:245-279
  *   cacto_rollout_rewards  Env.step reward / get_end_effector_position over recorded trajectories
+ *   cacto_ddp_backward     TO.backward_pass TO.py:119-202 (dV/dx Sobolev labels)
  *   cacto_mlp_pack         (layout transform for the kernels; no reference counterpart)
  *   cacto_actor_forward    NN.eval(actor, s)  NeuralNetwork.py:130-138 (+ utils.py:17-24)
  *   cacto_critic_forward   NN.eval(critic, s)
@@ -250,6 +251,18 @@ int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netbuf_d, const
 int cacto_rollout_rewards(const cacto_sys* sys, const double* S_traj_d, const float* A_traj_d,
                           const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
                           double* R_traj_d, double* EE_traj_d, int B, void* stream);
+
+/* Sobolev labels without CasADi: the DDP backward pass of TO.backward_pass
+ * (TO.py:119-202) along n_ep recorded trajectories. Episode e has Te = nsteps_d[e] steps:
+ *   S_traj_d [n_ep, ldS, ns] f64 (s_0..s_Te; the time column is ignored), U_traj_d [n_ep, ldU, na]
+ *   f64 (u_0..u_{Te-1}), output dVdx_d [n_ep, ldS, ns] f64: V_x(s_t) for t = 0..Te, time column 0 —
+ *   the layout cacto_rl_solve_add reads. mu: the Qbar_uu regulariser (1e-9 in the reference).
+ * The reward's derivatives are the closed forms of the planar TO cost (= -reward,
+ * environment_TO.py); dynamics Jacobians as augmented_derivative (environment.py:111-132,
+ * :221-233, :420-435). Supported: single integrator, car, prismatic chains (double integrator);
+ * other systems return CACTO_EUNSUPPORTED. */
+int cacto_ddp_backward(const cacto_sys* sys, const double* S_traj_d, int64_t ldS, const double* U_traj_d,
+                       int64_t ldU, const int32_t* nsteps_d, int n_ep, double mu, double* dVdx_d, void* stream);
 
 /* ---------------------------------------------------------------- replay ------------------ */
 
