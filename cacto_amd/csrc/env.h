@@ -347,6 +347,11 @@ __device__ inline void chain_mass(const SysDevice& sd, const double* q, double* 
   }
 }
 
+// The factor keeps the reciprocal of its diagonal (1/L_jj on the diagonal): one float64
+// division per column instead of one per off-diagonal entry and per solve step (each division is a
+// long dependent instruction sequence on the rollout's per-step critical path). Versus dividing,
+// results move by at most an ulp per operation; for unit diagonals (prismatic chains such as the
+// double integrator) they are identical.
 template <int NJ>
 __device__ inline bool cholesky(double* L) {
   bool ok = true;
@@ -356,14 +361,14 @@ __device__ inline bool cholesky(double* L) {
 #pragma unroll
     for (int k = 0; k < j; ++k) d -= L[j * NJ + k] * L[j * NJ + k];
     ok = ok && d > 0.0;
-    d = sqrt(d);
-    L[j * NJ + j] = d;
+    const double r = 1.0 / sqrt(d);
+    L[j * NJ + j] = r;
 #pragma unroll
     for (int i = j + 1; i < NJ; ++i) {
       double s = L[i * NJ + j];
 #pragma unroll
       for (int k = 0; k < j; ++k) s -= L[i * NJ + k] * L[j * NJ + k];
-      L[i * NJ + j] = s / d;
+      L[i * NJ + j] = s * r;
     }
   }
   return ok;
@@ -375,14 +380,14 @@ __device__ inline void chol_solve(const double* L, double* x) {
     double s = x[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) s -= L[i * NJ + k] * x[k];
-    x[i] = s / L[i * NJ + i];
+    x[i] = s * L[i * NJ + i];
   }
 #pragma unroll
   for (int i = NJ - 1; i >= 0; --i) {
     double s = x[i];
 #pragma unroll
     for (int k = i + 1; k < NJ; ++k) s -= L[k * NJ + i] * x[k];
-    x[i] = s / L[i * NJ + i];
+    x[i] = s * L[i * NJ + i];
   }
 }
 

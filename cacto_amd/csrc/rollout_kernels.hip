@@ -24,7 +24,7 @@
 #include "net_common.h"
 
 #ifdef CACTO_STAMPS
-__device__ unsigned long long g_rstamps[8];
+__device__ unsigned long long g_rstamps[16];
 #define RSTAMP(k)                                                                     \
   do {                                                                                \
     if (blockIdx.x == 0 && threadIdx.x == 0 && it == 20) g_rstamps[k] = __builtin_amdgcn_s_memtime(); \
@@ -118,7 +118,7 @@ __device__ __forceinline__ float lrelu(float z) { return z > 0.f ? z : fmul(z, 0
 // one publishes W.a).
 template <int NG, int NS, int NA, int REGK, int LDSK>
 __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActorLds<NG, NA, LDSK>& W,
-                                         const float* __restrict__ W2g, const Lane& L) {
+                                         const float* __restrict__ W2g, const Lane& L, int it) {
   using C = RoCfg<NG>;
   // ---- layer 1 (K = NS): one activation VGPR per group covers every k
   {
@@ -142,6 +142,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
       for (int i = 0; i < 4; ++i) W.h1[(g * 4 + L.wave) * C::H1B + q * 20 + 4 * i + v] = lrelu(fadd(acc[g][i], R.b1));
   }
   __syncthreads();
+  RSTAMP(4);
   // ---- layer 2 (K = 256): k = 64 kb + 16 v + q; lane 4q+i reads {x[i][64kb + 16v + q], v = 0..3}
   {
     floatx4 acc[NG][2];
@@ -182,6 +183,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
         W.h2[(4 * g + i) * C::H2S + f] = lrelu(fadd(fadd(acc[g][0][i], acc[g][1][i]), R.b2));
   }
   __syncthreads();
+  RSTAMP(5);
   // ---- layer 3 (256 -> NA): one summation order for every NG (so the schedule never changes a
   //      result): 64 partial chains, chain j = features j, j + 64, j + 128, j + 192 (FMA in that
   //      order), combined by a butterfly over j with offsets 32, 16, ..., 1. Thread (slot s,
@@ -379,6 +381,25 @@ struct RoShared {
   int anyact;
 };
 
+// normalize_feature (mlp.h) with the norms held in registers for the whole launch: the per-step
+// input of the next actor pass must not wait on scalar loads of the system parameters (each such
+// load's s_waitcnt also drains the LDS queue). Same f32 arithmetic, branch-free.
+template <int NS>
+struct RoNorm {
+  float n[NS];
+  bool on;
+  __device__ __forceinline__ explicit RoNorm(const cacto_sys_params& p) {
+    on = p.normalize != 0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) n[i] = (float)p.state_norm[i];
+  }
+  __device__ __forceinline__ float operator()(int f, float s) const {
+    const float q = fdiv(s, n[f]);
+    const float v = f == NS - 1 ? fsub(fmul(q, 2.0f), 1.0f) : q;
+    return on ? v : s;
+  }
+};
+
 // Slot refill (wave 0; every lane calls it, lanes with `need` take the next queue entries in lane
 // order). A new episode's s_0 goes to the slot's state and the actor input; episodes of length 0
 // are completed on the spot (status 0: RL.py never rolls out NSTEPS_SH == 0).
@@ -387,7 +408,7 @@ __device__ __forceinline__ void ro_refill(bool need, int c, int& head, RoShared<
                                           const double* __restrict__ S0,
                                           const int32_t* __restrict__ nsteps, const int32_t* __restrict__ order, int T,
                                           int B, int G, double* __restrict__ Straj, int32_t* __restrict__ status,
-                                          const Lane& L) {
+                                          const RoNorm<Dims<NJ>::NS>& nrm, const Lane& L) {
   constexpr int ns = Dims<NJ>::NS, SL = RoCfg<NG>::SL;
   const cacto_sys_params& p = sd.p;
   while (true) {
@@ -421,7 +442,7 @@ __device__ __forceinline__ void ro_refill(bool need, int c, int& head, RoShared<
 #pragma unroll
           for (int i = 0; i < ns; ++i) Sh.sS[c * ns + i] = s[i];
 #pragma unroll
-          for (int q = 0; q < ns; ++q) Sh.W.x0[(c >> 2) * 64 + 4 * q + (c & 3)] = normalize_feature(p, q, (float)s[q]);
+          for (int q = 0; q < ns; ++q) Sh.W.x0[(c >> 2) * 64 + 4 * q + (c & 3)] = nrm(q, (float)s[q]);
           if constexpr (RoConstDyn<NJ>::ok) {
             if (p.const_dyn) {
               // prismatic chain: M factored once per episode, kept in the slot's MS / hS
@@ -445,7 +466,7 @@ template <int NJ, int NG>
 __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* sn, const float* a,
                                            RoShared<NJ, NG>& Sh, const SysDevice& sd, int T,
                                            double* __restrict__ Straj, float* __restrict__ Atraj,
-                                           int32_t* __restrict__ status) {
+                                           int32_t* __restrict__ status, const RoNorm<Dims<NJ>::NS>& nrm) {
   constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
   const cacto_sys_params& p = sd.p;
   bool bad = false;
@@ -453,7 +474,7 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
   for (int i = 0; i < ns; ++i) {
     Sh.sS[c * ns + i] = sn[i];
     bad |= isnan(sn[i]);
-    Sh.W.x0[(c >> 2) * 64 + 4 * i + (c & 3)] = normalize_feature(p, i, (float)sn[i]);
+    Sh.W.x0[(c >> 2) * 64 + 4 * i + (c & 3)] = nrm(i, (float)sn[i]);
   }
   if (Atraj)
 #pragma unroll
@@ -509,8 +530,9 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   if (L.tid < SL) Sh.sact[L.tid] = 0;
   __syncthreads();
   int head = 0;  // queue position (wave 0, uniform)
+  const RoNorm<ns> nrm(p);
   if (L.wave == 0) {
-    ro_refill<NJ, NG>(L.lane < SL, L.lane, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, L);
+    ro_refill<NJ, NG>(L.lane < SL, L.lane, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L);
     const uint64_t m = __ballot(L.lane < SL && Sh.sact[L.lane]);
     if (L.lane == 0) Sh.anyact = m != 0;
   }
@@ -525,7 +547,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (!use_actor) __syncthreads();
       }
     }
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK>(R, Sh.W, W2g, L);
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK>(R, Sh.W, W2g, L, it);
     RSTAMP(1);
     const bool active = L.lane < SL && Sh.sact[c] != 0;
     if (split_dyn) {
@@ -571,11 +593,14 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         } else {
           env_simulate<NJ>(sd, s, ad, false, sn);
         }
-        fin = ro_advance<NJ, NG>(c, b, tc, sn, a, Sh, sd, T, Straj, Atraj, status);
+        RSTAMP(6);
+        fin = ro_advance<NJ, NG>(c, b, tc, sn, a, Sh, sd, T, Straj, Atraj, status, nrm);
+        RSTAMP(7);
       }
-      ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, L);
+      ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L);
       const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
       if (L.lane == 0) Sh.anyact = m != 0;
+      RSTAMP(8);
     }
     __syncthreads();
     RSTAMP(3);
@@ -703,7 +728,7 @@ struct LaunchRollout {
 #ifdef CACTO_STAMPS
 extern "C" int cacto_debug_rollout_stamps(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipDeviceSynchronize());
-  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 8));
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 16));
   return CACTO_OK;
 }
 #endif

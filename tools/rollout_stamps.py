@@ -29,11 +29,15 @@ def main():
     for _ in range(3):
         out = rl.rollout_batch(None, None, T, inputs=inputs)
     torch.cuda.synchronize()
-    st = (ctypes.c_ulonglong * 8)()
+    st = (ctypes.c_ulonglong * 16)()
     L.lib().dll.cacto_debug_rollout_stamps(st)
     t = np.array(st[:4], dtype=np.float64)
+    a1, a2 = float(st[4]) - t[0], float(st[5]) - float(st[4])
     names = ["actor", "E1 (dynamics | reward terms)", "E2 (reward combine + stores + refill | EE(s'))"]
     print(system, R, "step cycles %.0f: " % (t[3] - t[0]) + ", ".join("%s %.0f" % (nm, d) for nm, d in zip(names, np.diff(t))))
+    print("   actor: layer 1 (+ placements) %.0f, layer 2 %.0f, layer 3 %.0f" % (a1, a2, t[1] - float(st[5])))
+    print("   wave 0 after the dynamics phase: s' %.0f, advance/stores %.0f, refill+ballot %.0f, barrier %.0f"
+          % (float(st[6]) - t[2], float(st[7]) - float(st[6]), float(st[8]) - float(st[7]), t[3] - float(st[8])))
 
 
 if __name__ == "__main__":
