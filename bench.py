@@ -11,8 +11,8 @@ Workload (BASELINE.json configs[1]): double_integrator, w_S = 1e-2, 4096 rollout
     rollouts; with N > 1 ranks each rank takes the minibatch locally and the gradients are
     all-reduced over RCCL (data parallel, one global update per iteration).
 Inputs are resident in HBM before timing. Weights: the reference's DI seed-0 initial weights
-(tests/golden/weights/di_seed0_0.npz); dVdx labels are synthetic N(0,1) (TO/CasADi is host-side
-and absent here).
+(tests/golden/weights/di_seed0_0.npz); dVdx labels come from the DDP backward pass along the
+rollouts (cacto_ddp_backward, every system; the TO NLP solve itself is host-side CasADi, absent).
 
     python bench.py [--gpus N --steps K --warmup W]
 """
@@ -247,11 +247,8 @@ def ddp_labels(rl, conf, env, roll, K=5):
     """Sobolev labels dV/dx of every rollout episode by the DDP backward pass (TO.backward_pass,
     TO.py:119-202, cacto_ddp_backward) along the rollout trajectory — the stand-in for the TO
     solution the reference labels (the NLP solve is host-side CasADi, out of scope). Returns the
-    labels [R, T+1, ns] f64 (None for systems the kernel does not cover) and its timing."""
+    labels [R, T+1, ns] f64 and its timing."""
     from cacto_amd.to import TO
-    system = conf.__name__.rsplit(".", 1)[-1][len("conf_"):]
-    if system not in ("single_integrator", "double_integrator", "car"):
-        return None, None
     to = TO(env, conf, w_S=rl.w_S)
     S, A = roll["out"]["S"], roll["out"]["A"].double()
     n = torch.as_tensor(roll["nsteps"].astype(np.int32), device="cuda")
@@ -381,7 +378,8 @@ def extra_system(name, args, world, rank):
     if cfg["per"]:
         conf.prioritized_replay_alpha = 0.6
     r = rollout_phase(rl, conf, env, cfg["R"], args.steps, args.warmup, world, rank)
-    buf = fill_buffer(rl, conf, r, env, seed=rank, per=cfg["per"])
+    labels, ddp = ddp_labels(rl, conf, env, r)
+    buf = fill_buffer(rl, conf, r, env, seed=rank, per=cfg["per"], dVdx=labels)
     if cfg["per"] and world > 1:
         buf.set_data_parallel(world)        # IS weights over the union of the ranks' shards
     ups = {}
@@ -395,7 +393,7 @@ def extra_system(name, args, world, rank):
                                ms_per_update=1e3 * wall / args.update_steps)
     return dict(config=cfg["config"], env_steps_per_s=r["total_steps"] / r["wall"], rollouts_per_gpu=cfg["R"],
                 rollout_kernel_ms=r["kernel_ms"], env_steps_per_launch=r["steps_per_call"],
-                w_S=cfg["w_S"], per=cfg["per"], critic_updates=ups)
+                w_S=cfg["w_S"], per=cfg["per"], critic_updates=ups, ddp_labels=ddp)
 
 
 def cpu_baseline_rollout(conf, rl, roll, seconds):

@@ -16,9 +16,13 @@
 // Gauss-Jordan with partial pivoting (np.linalg.pinv in the reference equals the inverse for the
 // nonsingular, mu-regularised Qbar): float64 results within 1e-9 relative of the oracle.
 //
-// Supported: the planar-cost systems with closed-form Jacobians — single integrator (NJ = 0), car
-// (NJ = -1) and prismatic Pinocchio chains (the double integrator: M and nle constant, so
-// ddq_dq = ddq_dv = 0 and Fu = dt [0; M^-1]). Others return CACTO_EUNSUPPORTED.
+// Every system: the single integrator (NJ = 0), car (NJ = -1) and prismatic Pinocchio chains (the
+// double integrator: M and nle constant, so ddq_dq = ddq_dv = 0 and Fu = dt [0; M^-1]) use closed
+// forms; car_park (NJ = -2) closed-form Jacobians (environment.py:567-582) with its smooth-box cost
+// differentiated by hyper-dual numbers (ad.h); revolute chains (manipulator NJ = 3, UR5 NJ = 6) take
+// ddq_dq, ddq_dv from hyper-dual RNEA (computeABADerivatives) and l_x, l_xx through hyper-dual
+// forward kinematics.
+#include "ad.h"
 #include "internal.h"
 
 namespace cacto {
@@ -26,7 +30,7 @@ namespace cacto {
 template <int NJ>
 struct DdpDims {
   static constexpr int N = Dims<NJ>::NS - 1, M = Dims<NJ>::NA;
-  static constexpr bool ok = NJ == 0 || NJ == -1 || NJ == 2;
+  static constexpr bool ok = NJ >= -2;
 };
 
 // Reward derivatives w.r.t. the EE position p = (px, py) of the planar family (environment_TO.py
@@ -83,19 +87,57 @@ __device__ inline void ddp_lx(const SysDevice& sd, const double* w, const double
   for (int k = 0; k < N * N; ++k) lxx[k] = 0.0;
 #pragma unroll
   for (int k = 0; k < N; ++k) lx[k] = 0.0;
-  PosDerivs d;
-  planar_pos_derivs(p, w, x[0], x[1], d);  // p_ee = (x0, x1): SI / car states, DI q (unit prismatic axes)
-  lx[0] = p.scale * d.g[0];
-  lx[1] = p.scale * d.g[1];
-  lxx[0] = p.scale * d.H[0];
-  lxx[1] = lxx[N] = p.scale * d.H[1];
-  lxx[N + 1] = p.scale * d.H[2];
-  if constexpr (NJ > 0) {
-    // DI: - w2 * |v|^2 (environment_TO.py:227-230)
+  if constexpr (NJ == -2) {
+    // car_park: the reward depends on (x, y, theta, v); one hyper-dual evaluation per pair
+#pragma unroll 1
+    for (int j = 0; j < 4; ++j)
+#pragma unroll 1
+      for (int k = j; k < 4; ++k) {
+        HD xs[4];
 #pragma unroll
-    for (int i = NJ; i < N; ++i) {
-      lx[i] = p.scale * (-w[2] * (2.0 * x[i]));
-      lxx[i * N + i] = p.scale * (-w[2] * 2.0);
+        for (int i = 0; i < 4; ++i) xs[i] = HD(x[i], i == j ? 1.0 : 0.0, i == k ? 1.0 : 0.0, 0.0);
+        const HD r = carpark_reward_t(p, w, xs);
+        if (k == j) lx[j] = r.a;
+        lxx[j * N + k] = lxx[k * N + j] = r.ab;
+      }
+    return;
+  } else {
+    if (NJ > 2 && p.reward_kind != CACTO_REW_PLANAR) {
+      // revolute chains: position terms through hyper-dual forward kinematics, one pass per
+      // (j <= k) joint pair; the velocity term - scale w2 |v|^2 in closed form
+      constexpr int nq = NJ > 0 ? NJ : 1;
+#pragma unroll 1
+      for (int j = 0; j < nq; ++j)
+#pragma unroll 1
+        for (int k = j; k < nq; ++k) {
+          HD q[nq];
+#pragma unroll
+          for (int i = 0; i < nq; ++i) q[i] = HD(x[i], i == j ? 1.0 : 0.0, i == k ? 1.0 : 0.0, 0.0);
+          const HD r = chain_pos_reward_t(p, w, chain_ee_t<nq, HD>(sd, q));
+          if (k == j) lx[j] = r.a;
+          lxx[j * N + k] = lxx[k * N + j] = r.ab;
+        }
+#pragma unroll
+      for (int i = nq; i < N; ++i) {
+        lx[i] = -(p.scale * (w[2] * (2.0 * x[i])));
+        lxx[i * N + i] = -(p.scale * (w[2] * 2.0));
+      }
+      return;
+    }
+    PosDerivs d;
+    planar_pos_derivs(p, w, x[0], x[1], d);  // p_ee = (x0, x1): SI / car states, DI q (unit prismatic axes)
+    lx[0] = p.scale * d.g[0];
+    lx[1] = p.scale * d.g[1];
+    lxx[0] = p.scale * d.H[0];
+    lxx[1] = lxx[N] = p.scale * d.H[1];
+    lxx[N + 1] = p.scale * d.H[2];
+    if constexpr (NJ > 0) {
+      // DI: - w2 * |v|^2 (environment_TO.py:227-230)
+#pragma unroll
+      for (int i = NJ; i < N; ++i) {
+        lx[i] = p.scale * (-w[2] * (2.0 * x[i]));
+        lxx[i * N + i] = p.scale * (-w[2] * 2.0);
+      }
     }
   }
 }
@@ -123,6 +165,17 @@ __device__ inline void ddp_jacobians(const SysDevice& sd, const double* x, const
     A[3 * N + 4] = dt;
     B[2 * M + 0] = dt;
     B[4 * M + 1] = dt;
+  } else if constexpr (NJ == -2) {
+    // CarPark.augmented_derivative (environment.py:567-582); sec^2 = 1 / cos^2
+    const double s2 = sin(x[2]), c2 = cos(x[2]), L = sd.p.L_delta, cd = cos(x[4]);
+    A[0 * N + 2] = -dt * x[3] * s2;
+    A[0 * N + 3] = dt * c2;
+    A[1 * N + 2] = dt * x[3] * c2;
+    A[1 * N + 3] = dt * s2;
+    A[2 * N + 3] = dt * tan(x[4]) / L;
+    A[2 * N + 4] = dt * x[3] * (1.0 / (cd * cd)) / L;
+    B[3 * M + 0] = dt;
+    B[4 * M + 1] = dt / sd.p.tau_delta;
   } else {
     constexpr int nv = NJ > 0 ? NJ : 1;
 #pragma unroll
@@ -180,6 +233,61 @@ __device__ inline void small_inverse(double* a, double* inv) {
   }
 }
 
+// Revolute chains (computeABADerivatives, environment.py:111-132): M(q)^-1, qdd = M^-1 (u - nle),
+// then one hyper-dual RNEA(q + e1 e_k, v + e2 e_k, qdd) per joint k gives column k of dtau/dq (e1
+// part) and dtau/dv (e2 part); ddq_dq = -M^-1 dtau/dq, ddq_dv = -M^-1 dtau/dv.
+// A = I + dt [[0, I], [ddq_dq, ddq_dv]], B = dt [0; M^-1].
+template <int NJ>
+__device__ inline void ddp_chain_jacobians(const SysDevice& sd, const double* x, const double* u, double* A,
+                                           double* B) {
+  if constexpr (NJ > 2) {
+    constexpr int N = 2 * NJ;
+    const double dt = sd.p.dt;
+    double Mm[NJ * NJ], Minv[NJ * NJ], h[NJ], qdd[NJ];
+    chain_mass<NJ>(sd, x, Mm);
+    small_inverse<NJ>(Mm, Minv);
+    chain_nle<NJ>(sd, x, x + NJ, h);
+#pragma unroll
+    for (int r = 0; r < NJ; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) s += Minv[r * NJ + k] * (u[k] - h[k]);
+      qdd[r] = s;
+    }
+#pragma unroll
+    for (int k = 0; k < N * N; ++k) A[k] = (k % (N + 1) == 0) ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) A[i * N + NJ + i] = dt;
+#pragma unroll 1
+    for (int k = 0; k < NJ; ++k) {
+      HD q[NJ], v[NJ], tau[NJ];
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        q[i] = HD(x[i], i == k ? 1.0 : 0.0, 0.0, 0.0);
+        v[i] = HD(x[NJ + i], 0.0, i == k ? 1.0 : 0.0, 0.0);
+      }
+      rnea_t<NJ, HD>(sd, q, v, qdd, tau);
+#pragma unroll
+      for (int r = 0; r < NJ; ++r) {
+        double sq = 0.0, sv = 0.0;
+#pragma unroll
+        for (int c = 0; c < NJ; ++c) {
+          sq += Minv[r * NJ + c] * tau[c].a;
+          sv += Minv[r * NJ + c] * tau[c].b;
+        }
+        A[(NJ + r) * N + k] = -dt * sq;
+        A[(NJ + r) * N + NJ + k] += -dt * sv;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < N * NJ; ++k) B[k] = 0.0;
+#pragma unroll
+    for (int r = 0; r < NJ; ++r)
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) B[(NJ + r) * NJ + c] = Minv[r * NJ + c] * dt;
+  }
+}
+
 template <int NJ>
 __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
                                                       int64_t ldS, const double* __restrict__ U, int64_t ldU,
@@ -195,13 +303,16 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
   const double* Ue = U + (size_t)e * ldU * na;
   double* Oe = dVdx + (size_t)e * ldS * ns;
   double Minv[NJ > 0 ? M * M : 1];
+  const bool chain_const = NJ > 0 && p.const_dyn;
   if constexpr (NJ > 0) {
-    // prismatic chain: M constant; its inverse once per episode
-    double Mm[M * M], q[NJ];
+    if (chain_const) {
+      // prismatic chain: M constant; its inverse once per episode
+      double Mm[M * M], q[NJ];
 #pragma unroll
-    for (int i = 0; i < NJ; ++i) q[i] = Se[i];
-    chain_mass<NJ>(sd, q, Mm);
-    small_inverse<M>(Mm, Minv);
+      for (int i = 0; i < NJ; ++i) q[i] = Se[i];
+      chain_mass<NJ>(sd, q, Mm);
+      small_inverse<M>(Mm, Minv);
+    }
   }
   double w_run[7], w_term[7];
 #pragma unroll
@@ -222,7 +333,10 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
     for (int k = 0; k < N; ++k) x[k] = Se[(size_t)i * ns + k];
 #pragma unroll
     for (int k = 0; k < M; ++k) u[k] = Ue[(size_t)i * na + k];
-    ddp_jacobians<NJ>(sd, x, Minv, A, B);
+    if (NJ > 2 && !chain_const)
+      ddp_chain_jacobians<NJ>(sd, x, u, A, B);
+    else
+      ddp_jacobians<NJ>(sd, x, Minv, A, B);
     ddp_lx<NJ>(sd, w_run, x, lx, lxx);
     // Q_x = l_x + A^T V_x, Q_u = l_u + B^T V_x
     double Qx[N], Qu[M], Qxx[N * N], Quu[M * M], Qxu[N * M], VA[N * N], VB[N * M];
@@ -344,12 +458,14 @@ struct LaunchDdp {
       set_error("cacto_ddp_backward: supported for the single integrator, car and prismatic chains (double integrator)");
       return CACTO_EUNSUPPORTED;
     } else {
-      if (NJ > 0 && !sys->host.p.const_dyn) {
-        set_error("cacto_ddp_backward: chains need ABA derivatives (only prismatic chains are supported)");
-        return CACTO_EUNSUPPORTED;
-      }
-      if (sys->host.p.reward_kind != CACTO_REW_PLANAR) {
-        set_error("cacto_ddp_backward: planar-family costs only");
+      const int rk = sys->host.p.reward_kind;
+      const bool rk_ok = NJ == -2 ? rk == CACTO_REW_CAR_PARK
+                                  : NJ > 0 ? (sys->host.p.const_dyn ? rk == CACTO_REW_PLANAR
+                                                                   : rk == CACTO_REW_MANIPULATOR || rk == CACTO_REW_UR5)
+                                           : rk == CACTO_REW_PLANAR;
+      // chains: the DI's prismatic pair (constant M) or revolute chains of 3 / 6 joints
+      if (!rk_ok || (NJ > 0 && (sys->host.p.const_dyn ? NJ != 2 : NJ == 2))) {
+        set_error("cacto_ddp_backward: unsupported (dynamics, reward) combination");
         return CACTO_EUNSUPPORTED;
       }
       hipLaunchKernelGGL(k_ddp_backward<NJ>, dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS, U, ldU, n,

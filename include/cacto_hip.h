@@ -257,10 +257,12 @@ int cacto_rollout_rewards(const cacto_sys* sys, const double* S_traj_d, const fl
  *   S_traj_d [n_ep, ldS, ns] f64 (s_0..s_Te; the time column is ignored), U_traj_d [n_ep, ldU, na]
  *   f64 (u_0..u_{Te-1}), output dVdx_d [n_ep, ldS, ns] f64: V_x(s_t) for t = 0..Te, time column 0 —
  *   the layout cacto_rl_solve_add reads. mu: the Qbar_uu regulariser (1e-9 in the reference).
- * The reward's derivatives are the closed forms of the planar TO cost (= -reward,
- * environment_TO.py); dynamics Jacobians as augmented_derivative (environment.py:111-132,
- * :221-233, :420-435). Supported: single integrator, car, prismatic chains (double integrator);
- * other systems return CACTO_EUNSUPPORTED. */
+ * The reward's derivatives are those of the TO cost (= -reward, environment_TO.py): closed forms
+ * for the planar family (SI, DI, car), hyper-dual forward-mode derivatives through the forward
+ * kinematics (manipulator, UR5) and the body check points (car_park). Dynamics Jacobians as
+ * augmented_derivative (environment.py:111-132, :221-233, :420-435, :567-582); for revolute chains
+ * ddq_dq, ddq_dv (computeABADerivatives) come from hyper-dual RNEA. Every system is supported; a
+ * (dynamics, reward) combination outside the six systems returns CACTO_EUNSUPPORTED. */
 int cacto_ddp_backward(const cacto_sys* sys, const double* S_traj_d, int64_t ldS, const double* U_traj_d,
                        int64_t ldU, const int32_t* nsteps_d, int n_ep, double mu, double* dVdx_d, void* stream);
 

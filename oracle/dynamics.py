@@ -31,7 +31,7 @@ def _rot(axis, q):
 def _Xmotion(R, p):
     """6x6 motion transform for SE3 (R, p) mapping child-frame motions into the parent frame:
     act(v) = (R v_lin + p x (R v_ang), R v_ang)."""
-    X = np.zeros((6, 6))
+    X = np.zeros((6, 6), dtype=np.result_type(R, p))
     X[:3, :3] = R
     X[:3, 3:] = _skew(p) @ R
     X[3:, 3:] = R
@@ -40,7 +40,7 @@ def _Xmotion(R, p):
 
 def _Xforce(R, p):
     """6x6 force transform (child -> parent): act(f) = (R f_lin, R f_ang + p x (R f_lin))."""
-    X = np.zeros((6, 6))
+    X = np.zeros((6, 6), dtype=np.result_type(R, p))
     X[:3, :3] = R
     X[3:, :3] = _skew(p) @ R
     X[3:, 3:] = R
@@ -60,7 +60,7 @@ def _inertia6(m, c, Ic):
 
 def _crm(v):
     """Motion cross-product matrix v x (.)."""
-    X = np.zeros((6, 6))
+    X = np.zeros((6, 6), dtype=v.dtype)
     X[:3, :3] = _skew(v[3:])
     X[:3, 3:] = _skew(v[:3])
     X[3:, 3:] = _skew(v[3:])
@@ -115,12 +115,12 @@ class Chain:
             R, p = self._placement(i, q[i])
             Xm.append(_Xmotion(R, p))
             Xf.append(_Xforce(R, p))
-        Ic = [I.copy() for I in self.I6]
+        Ic = [I.astype(Xm[0].dtype) for I in self.I6]
         for i in range(n - 1, -1, -1):
             if self.parent[i] >= 0:
                 # composite inertia expressed in parent: Xf Ic Xm^-1
                 Ic[self.parent[i]] += Xf[i] @ Ic[i] @ np.linalg.inv(Xm[i])
-        M = np.zeros((n, n))
+        M = np.zeros((n, n), dtype=Xm[0].dtype)
         for i in range(n):
             F = Ic[i] @ self._S(i)
             M[i, i] = self._S(i) @ F
@@ -133,6 +133,11 @@ class Chain:
 
     def nle(self, q, v):
         """RNEA with qdd = 0: h = C(q, v) v + g(q) (Featherstone Table 5.1, a_0 = -gravity)."""
+        return self.rnea(q, v, np.zeros(self.n))
+
+    def rnea(self, q, v, qdd):
+        """tau = M(q) qdd + h(q, v) (Featherstone Table 5.1). Works on complex inputs too (the
+        complex-step derivatives of oracle/ddp.py)."""
         n = self.n
         vel, acc, f, Xm, Xf = [], [], [], [], []
         for i in range(n):
@@ -147,11 +152,11 @@ class Chain:
             else:
                 vp, ap = vel[self.parent[i]], acc[self.parent[i]]
             vi = Xinv @ vp + S * v[i]
-            ai = Xinv @ ap + _crm(vi) @ (S * v[i])
+            ai = Xinv @ ap + _crm(vi) @ (S * v[i]) + S * qdd[i]
             vel.append(vi)
             acc.append(ai)
             f.append(self.I6[i] @ ai + _crf(vi) @ (self.I6[i] @ vi))
-        tau = np.zeros(n)
+        tau = np.zeros(n, dtype=np.result_type(*f))
         for i in range(n - 1, -1, -1):
             tau[i] = self._S(i) @ f[i]
             if self.parent[i] >= 0:

@@ -77,10 +77,13 @@ def test_ddp_backward_single_episode_api():
     assert (np.abs(got - ref) <= tol).all()
 
 
-@pytest.mark.parametrize("system", ["manipulator", "car_park"])
-def test_ddp_backward_unsupported_systems_fail_loudly(system):
-    conf, oe, to = _setup(system)
+def test_ddp_backward_bad_arguments_fail_loudly():
+    conf, oe, to = _setup("manipulator")
     S = torch.zeros(1, 3, conf.nb_state, dtype=torch.float64, device="cuda")
     U = torch.zeros(1, 3, conf.nb_action, dtype=torch.float64, device="cuda")
+    from cacto_amd import _lib as L
+    from cacto_amd.system import dptr, stream
     with pytest.raises(RuntimeError, match="cacto_ddp_backward"):
-        to.backward_pass_batch(S, U, torch.tensor([2], dtype=torch.int32, device="cuda"))
+        L.lib().call("cacto_ddp_backward", to.sys.handle, dptr(S, torch.float64), 0, dptr(U, torch.float64), 3,
+                     dptr(torch.tensor([2], dtype=torch.int32, device="cuda"), torch.int32), 1, 1e-9,
+                     dptr(S, torch.float64), stream())

@@ -15,6 +15,15 @@ from oracle import env as oenv
 SYSTEMS = list(ddp.SUPPORTED)
 
 
+def _to_reward(conf, env, w, s, u):
+    """The TO cost's reward (-cost) per the oracle env. UR5 is the one system whose Env.reward
+    (environment.py:780-805: u.u) and TO cost (environment_TO.py:741-743: bound_control_cost)
+    differ in the control term; the state part is the same."""
+    if conf.system_id != "ur5":
+        return env.reward(w, s, u)
+    return env.reward(w, s, None) - conf.cost_funct_param[1] * w[6] * env.bound_control_cost(u)
+
+
 def _sample(conf, env, rng):
     s = env.reset(rng)
     s[:-1] *= 1.2
@@ -33,7 +42,7 @@ def test_sympy_cost_is_minus_reference_reward(system):
         for _ in range(20):
             s, u = _sample(conf, env, rng)
             r_sym = float(f["r"](s[:n], u, list(w[:7])))
-            r_ref = env.reward(w, s, u)
+            r_ref = _to_reward(conf, env, w, s, u)
             assert abs(r_sym - r_ref) <= 1e-12 * max(1.0, abs(r_ref)), (r_sym, r_ref)
 
 
@@ -58,7 +67,7 @@ def test_symbolic_derivatives_match_central_differences(system):
         def R(xx, uu):
             ss = s.copy()
             ss[:n] = xx
-            return env.reward(conf.cost_weights_running, ss, uu)
+            return _to_reward(conf, env, conf.cost_weights_running, ss, uu)
 
         for i in range(n):
             e = np.zeros(n)
