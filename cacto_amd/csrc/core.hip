@@ -103,6 +103,7 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
 extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   if (!sys) return CACTO_OK;
   (void)hipFree(sys->dev);
+  if (sys->ddp_ws) (void)hipFree(sys->ddp_ws);
   delete sys;
   return CACTO_OK;
 }

@@ -288,11 +288,66 @@ __device__ inline void ddp_chain_jacobians(const SysDevice& sd, const double* x,
   }
 }
 
+// Per-step derivative record of the split pass (car_park and the revolute chains, whose
+// derivatives cost far more than the recursion): A [N*N], B [N*M], l_x [N], l_xx [N*N] of step t
+// (the terminal step: l_x, l_xx of the terminal weights). Workspace layout [t][k][e]: element k of
+// episode e's step-t record at ws[(t * R + k) * n_ep + e], so the lanes (episodes) of a wave read
+// and write consecutive addresses.
 template <int NJ>
+struct DdpRec {
+  static constexpr int N = DdpDims<NJ>::N, M = DdpDims<NJ>::M;
+  static constexpr int A = 0, B = N * N, LX = B + N * M, LXX = LX + N, R = LXX + N * N;
+};
+
+// One thread per (episode, step): the steps are independent given the trajectory, so the
+// hyper-dual work runs over every step of every episode at once (grid.y = step).
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ddp_derivs(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
+                                                    int64_t ldS, const double* __restrict__ U, int64_t ldU,
+                                                    const int32_t* __restrict__ nsteps, int n_ep,
+                                                    double* __restrict__ ws) {
+  using RC = DdpRec<NJ>;
+  constexpr int N = RC::N, M = RC::M, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.y;
+  if (e >= n_ep) return;
+  const int Te = nsteps[e];
+  if (t > Te) return;
+  const SysDevice& sd = *sdp;
+  double x[N], w[7];
+#pragma unroll
+  for (int k = 0; k < N; ++k) x[k] = S[((size_t)e * ldS + t) * ns + k];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) w[k] = t == Te ? sd.p.w_terminal[k] : sd.p.w_running[k];
+  double* rec = ws + (size_t)t * RC::R * n_ep + e;
+  double lx[N], lxx[N * N];
+  ddp_lx<NJ>(sd, w, x, lx, lxx);
+#pragma unroll
+  for (int k = 0; k < N; ++k) rec[(size_t)(RC::LX + k) * n_ep] = lx[k];
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) rec[(size_t)(RC::LXX + k) * n_ep] = lxx[k];
+  if (t == Te) return;
+  double u[M], A[N * N], B[N * M];
+#pragma unroll
+  for (int k = 0; k < M; ++k) u[k] = U[((size_t)e * ldU + t) * na + k];
+  if constexpr (NJ > 2)
+    ddp_chain_jacobians<NJ>(sd, x, u, A, B);
+  else
+    ddp_jacobians<NJ>(sd, x, nullptr, A, B);
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) rec[(size_t)(RC::A + k) * n_ep] = A[k];
+#pragma unroll
+  for (int k = 0; k < N * M; ++k) rec[(size_t)(RC::B + k) * n_ep] = B[k];
+}
+
+// The Riccati recursion, one thread per episode (sequential in t). WS: read A, B, l_x, l_xx from
+// the k_ddp_derivs records; otherwise (SI, car, DI: closed forms) compute them inline.
+template <int NJ, bool WS>
 __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
                                                       int64_t ldS, const double* __restrict__ U, int64_t ldU,
                                                       const int32_t* __restrict__ nsteps, int n_ep, double mu,
-                                                      double* __restrict__ dVdx) {
+                                                      const double* __restrict__ ws, double* __restrict__ dVdx) {
+  using RC = DdpRec<NJ>;
   constexpr int N = DdpDims<NJ>::N, M = DdpDims<NJ>::M, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_ep) return;
@@ -323,7 +378,15 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
   double Vx[N], Vxx[N * N], x[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) x[k] = Se[(size_t)Te * ns + k];
-  ddp_lx<NJ>(sd, w_term, x, Vx, Vxx);
+  if constexpr (WS) {
+    const double* rec = ws + (size_t)Te * RC::R * n_ep + e;
+#pragma unroll
+    for (int k = 0; k < N; ++k) Vx[k] = rec[(size_t)(RC::LX + k) * n_ep];
+#pragma unroll
+    for (int k = 0; k < N * N; ++k) Vxx[k] = rec[(size_t)(RC::LXX + k) * n_ep];
+  } else {
+    ddp_lx<NJ>(sd, w_term, x, Vx, Vxx);
+  }
 #pragma unroll
   for (int k = 0; k < N; ++k) Oe[(size_t)Te * ns + k] = Vx[k];
   Oe[(size_t)Te * ns + N] = 0.0;
@@ -333,11 +396,20 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
     for (int k = 0; k < N; ++k) x[k] = Se[(size_t)i * ns + k];
 #pragma unroll
     for (int k = 0; k < M; ++k) u[k] = Ue[(size_t)i * na + k];
-    if (NJ > 2 && !chain_const)
-      ddp_chain_jacobians<NJ>(sd, x, u, A, B);
-    else
+    if constexpr (WS) {
+      const double* rec = ws + (size_t)i * RC::R * n_ep + e;
+#pragma unroll
+      for (int k = 0; k < N * N; ++k) A[k] = rec[(size_t)(RC::A + k) * n_ep];
+#pragma unroll
+      for (int k = 0; k < N * M; ++k) B[k] = rec[(size_t)(RC::B + k) * n_ep];
+#pragma unroll
+      for (int k = 0; k < N; ++k) lx[k] = rec[(size_t)(RC::LX + k) * n_ep];
+#pragma unroll
+      for (int k = 0; k < N * N; ++k) lxx[k] = rec[(size_t)(RC::LXX + k) * n_ep];
+    } else {
       ddp_jacobians<NJ>(sd, x, Minv, A, B);
-    ddp_lx<NJ>(sd, w_run, x, lx, lxx);
+      ddp_lx<NJ>(sd, w_run, x, lx, lxx);
+    }
     // Q_x = l_x + A^T V_x, Q_u = l_u + B^T V_x
     double Qx[N], Qu[M], Qxx[N * N], Quu[M * M], Qxu[N * M], VA[N * N], VB[N * M];
 #pragma unroll
@@ -450,6 +522,20 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
 using namespace cacto;
 
 namespace {
+// Grow-only device workspace of the split pass, owned by the system handle (freed by
+// cacto_sys_destroy). Growing frees the old block (hipFree synchronises the device).
+int ddp_workspace(cacto_sys* sys, size_t bytes, double** out) {
+  if (bytes > sys->ddp_ws_bytes) {
+    if (sys->ddp_ws) CACTO_CHECK_HIP(hipFree(sys->ddp_ws));
+    sys->ddp_ws = nullptr;
+    sys->ddp_ws_bytes = 0;
+    CACTO_CHECK_HIP(hipMalloc(&sys->ddp_ws, bytes));
+    sys->ddp_ws_bytes = bytes;
+  }
+  *out = static_cast<double*>(sys->ddp_ws);
+  return CACTO_OK;
+}
+
 template <int NJ>
 struct LaunchDdp {
   static int run(const cacto_sys* sys, const double* S, int64_t ldS, const double* U, int64_t ldU, const int32_t* n,
@@ -468,8 +554,21 @@ struct LaunchDdp {
         set_error("cacto_ddp_backward: unsupported (dynamics, reward) combination");
         return CACTO_EUNSUPPORTED;
       }
-      hipLaunchKernelGGL(k_ddp_backward<NJ>, dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS, U, ldU, n,
-                         n_ep, mu, out);
+      if constexpr (NJ > 2 || NJ == -2) {
+        // split pass: per-step derivatives over (episode, step), then the recursion
+        using RC = DdpRec<NJ>;
+        double* ws = nullptr;
+        const int rc = ddp_workspace(const_cast<cacto_sys*>(sys), (size_t)ldS * RC::R * n_ep * sizeof(double), &ws);
+        if (rc != CACTO_OK) return rc;
+        hipLaunchKernelGGL(k_ddp_derivs<NJ>, dim3(ceil_div(n_ep, 64), (unsigned)ldS), dim3(64), 0, st, sys->dev, S,
+                           ldS, U, ldU, n, n_ep, ws);
+        CACTO_CHECK_HIP(hipGetLastError());
+        hipLaunchKernelGGL((k_ddp_backward<NJ, true>), dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS, U,
+                           ldU, n, n_ep, mu, ws, out);
+      } else {
+        hipLaunchKernelGGL((k_ddp_backward<NJ, false>), dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS,
+                           U, ldU, n, n_ep, mu, nullptr, out);
+      }
       CACTO_CHECK_HIP(hipGetLastError());
       return CACTO_OK;
     }

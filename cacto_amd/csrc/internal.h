@@ -8,6 +8,8 @@ struct cacto_sys {
   cacto::SysDevice host;  // host copy (validated)
   cacto::SysDevice* dev;  // device copy read by every kernel
   cacto::NetTopo actor, critic;
+  void* ddp_ws = nullptr;  // cacto_ddp_backward's per-step derivative records (grow-only)
+  size_t ddp_ws_bytes = 0;
 };
 
 namespace cacto {

@@ -10,6 +10,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import h5
 from .system import DEVICE, dptr, stream
 
 ACTOR, CRITIC = L.CACTO_NET_ACTOR, L.CACTO_NET_CRITIC
@@ -26,12 +27,24 @@ def layer_shapes(kind, ns, na):
     return shapes
 
 
+# Keras layer names of the reference's three models in one process (the .h5 files it writes,
+# e.g. Results Double Integrator/.../N_try_6/{actor,critic,target_critic}_0.h5)
+LAYER_NAMES = {
+    "actor": ["dense", "dense_1", "dense_2"],
+    "critic": ["sinusodial_representation_dense", "sinusodial_representation_dense_1",
+               "sinusodial_representation_dense_2", "sinusodial_representation_dense_3", "dense_3"],
+    "target": ["sinusodial_representation_dense_4", "sinusodial_representation_dense_5",
+               "sinusodial_representation_dense_6", "sinusodial_representation_dense_7", "dense_4"],
+}
+
+
 class Net:
     """Keras-model stand-in: weights live on the device in the net-buffer layout."""
 
-    def __init__(self, sys, kind):
+    def __init__(self, sys, kind, role=None):
         self.sys = sys
         self.kind = kind
+        self.role = role or ("actor" if kind == ACTOR else "critic")
         self.shapes = layer_shapes(kind, sys.ns, sys.na)
         self.P = sys.param_count(kind)
         assert self.P == sum(int(np.prod(s)) for s in self.shapes)
@@ -64,9 +77,21 @@ class Net:
         self.buf.copy_(other.buf)
 
     def save_weights(self, path):
-        np.savez(path, *self.get_weights())
+        """Keras `save_weights` (RL.py:191-195): a Keras-2.11 .h5 file for a `.h5` path (native
+        writer, cacto_amd/h5.py), else an .npz of the Keras-order arrays."""
+        ws = self.get_weights()
+        if str(path).endswith(".h5"):
+            names = LAYER_NAMES[self.role]
+            h5.write_keras_weights(path, [(n, [(n + "/kernel:0", ws[2 * i]), (n + "/bias:0", ws[2 * i + 1])])
+                                          for i, n in enumerate(names)])
+        else:
+            np.savez(path, *ws)
 
     def load_weights(self, path):
+        """Keras `load_weights` (main.py:154-158, RL.py:52-62): a reference .h5 checkpoint or .npz."""
+        if str(path).endswith(".h5"):
+            self.set_weights(h5.read_keras_weights(path))
+            return
         z = np.load(path)
         self.set_weights([z["arr_%d" % i] for i in range(len(self.shapes))])
 

@@ -7,6 +7,7 @@ are drawn up front (the reference draws them with the unseeded global numpy RNG,
 replay_buffer.py:45) and copied once, so the loop enqueues work with no host synchronisation.
 """
 import ctypes as C
+import os
 import math
 
 import numpy as np
@@ -54,16 +55,19 @@ class RL_AC:
         .h5-derived fixtures) instead of fresh initialisers."""
         self.actor_model = self.NN.create_actor()
         self.critic_model = self.NN.create_critic_sine()
-        self.target_critic = Net(self.sys, CRITIC)
+        self.target_critic = Net(self.sys, CRITIC, role="target")
         if weights is not None:
             self.actor_model.set_weights(weights["actor"])
             self.critic_model.set_weights(weights["critic"])
             self.target_critic.set_weights(weights.get("target", weights["critic"]))
         elif recover_training is not None:
+            # RL.py:88-92: <path>/N_try_<n>/{actor,critic,target_critic}_<step>.h5 (the reference's
+            # checkpoints load directly); .npz files of an earlier run of this package also work
             path, n_try, step = recover_training
-            self.actor_model.load_weights("%s/N_try_%s/actor_%s.npz" % (path, n_try, step))
-            self.critic_model.load_weights("%s/N_try_%s/critic_%s.npz" % (path, n_try, step))
-            self.target_critic.load_weights("%s/N_try_%s/target_critic_%s.npz" % (path, n_try, step))
+            for net, name in ((self.actor_model, "actor"), (self.critic_model, "critic"),
+                              (self.target_critic, "target_critic")):
+                base = "%s/N_try_%s/%s_%s" % (path, n_try, name, step)
+                net.load_weights(base + ".h5" if os.path.exists(base + ".h5") else base + ".npz")
         else:
             self.target_critic.copy_from(self.critic_model)       # RL.py:99
         f32 = dict(dtype=torch.float32, device=DEVICE)
@@ -261,10 +265,11 @@ class RL_AC:
         return TO_states, partial, total, s_next, done, rwrd, term, ep_return, None
 
     def RL_save_weights(self, update_step_counter='final'):
+        """RL.py:191-195: Keras-2.11 .h5 files the reference can load."""
         base = "%s/N_try_%s/" % (self.conf.NNs_path, self.N_try)
-        self.actor_model.save_weights(base + "actor_%s.npz" % update_step_counter)
-        self.critic_model.save_weights(base + "critic_%s.npz" % update_step_counter)
-        self.target_critic.save_weights(base + "target_critic_%s.npz" % update_step_counter)
+        self.actor_model.save_weights(base + "actor_%s.h5" % update_step_counter)
+        self.critic_model.save_weights(base + "critic_%s.h5" % update_step_counter)
+        self.target_critic.save_weights(base + "target_critic_%s.h5" % update_step_counter)
 
     # ---- RL.py:197-233, batched over episodes on the GPU ----
     def rollout_inputs(self, S0, nsteps):
