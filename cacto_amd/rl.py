@@ -183,6 +183,36 @@ class RL_AC:
                      dptr(idx, torch.int32), dptr(is_w), B, dptr(y), dptr(V), dptr(Vt), dptr(ws), ws.numel() * 4,
                      stream())
 
+    def capture_updates(self, storage, idx_steps, per_buffer=None, uniforms=None):
+        """One HIP graph of len(idx_steps) consecutive RL.py:101-118 updates (critic chain ->
+        weight-gradient GEMM -> Adam + soft update -> actor chain -> GEMM -> Adam per step), captured
+        without running; `graph.replay()` runs them in order. Every launch of the loop is a kernel
+        on the current stream and the optimiser counters live on the device, so replaying the graph
+        is the same work as calling update_rows per step, without the per-launch host cost.
+        idx_steps [K, B] int32 (device, kept alive by the caller). With `per_buffer` (a
+        PrioritizedReplayBuffer) each step instead samples from `uniforms[k]` ([K, B] f64) and
+        updates the priorities (learn_and_update with PER, RL.py:122-137). Single rank only: the
+        data-parallel update all-reduces between the kernels."""
+        if self.dp_world > 1:
+            raise RuntimeError("capture_updates: the data-parallel update is not captured")
+        K = (uniforms if per_buffer is not None else idx_steps).shape[0]
+        B = (uniforms if per_buffer is not None else idx_steps).shape[1]
+        self.workspace(B)                       # allocated before the capture
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        V = torch.empty_like(y)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for k in range(K):
+                if per_buffer is None:
+                    self.update_rows(storage, idx_steps[k])
+                else:
+                    idx, w = per_buffer.sample_device(uniforms[k])
+                    self.update_rows(per_buffer.storage, idx, w, y, V)
+                    per_buffer.update_priorities_device(idx, y, V)
+        g.keep = (y, V)
+        return g
+
     def _update_rows_dp(self, storage, idx, is_w=None, y=None, V=None, Vt=None):
         import torch.distributed as dist
         dp_update_step(lambda: self.critic_grad_flat(storage, idx, is_w, y, V, Vt),
