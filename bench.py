@@ -53,8 +53,9 @@ def parse():
     p.add_argument("--batches", default="128,4096")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-graph", action="store_true",
-                   help="launch the update loop eagerly instead of replaying it as one HIP graph")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the update loop as one HIP graph (RL_AC.capture_updates) instead of launching "
+                        "it eagerly; measured equal on MI355X (the update is bound by its kernels, not launches)")
     p.add_argument("--extra-systems", default="manipulator,car_park,ur5")
     p.add_argument("--no-diagnostics", action="store_true",
                    help="skip the rollout variants (profiling runs: every k_rollout dispatch is a full rollout)")
@@ -319,14 +320,14 @@ def episode_to_buffer_phase(rl, conf, roll, env, K, dVdx=None):
 
 
 def update_phase(rl, buf, B, K, W, world, seed):
-    """K learn_and_update iterations (RL.py:101-118 each) on pre-drawn minibatch indices. On one
-    rank the K updates are one HIP graph (RL_AC.capture_updates, captured before the timed region):
-    the same kernels with the same arguments, without the host launch cost between them."""
+    """K learn_and_update iterations (RL.py:101-118 each) on pre-drawn minibatch indices. With
+    --graph (one rank) the K updates replay as one HIP graph (RL_AC.capture_updates, captured before
+    the timed region): the same kernels with the same arguments."""
     gen = np.random.Generator(np.random.PCG64(seed))
     idx = torch.as_tensor(gen.integers(0, buf.max_idx(), size=(K + W, B)).astype(np.int32), device="cuda")
     for i in range(W):
         rl.update_rows(buf.storage, idx[i])
-    graph = rl.capture_updates(buf.storage, idx[W:]) if world == 1 and not NO_GRAPH else None
+    graph = rl.capture_updates(buf.storage, idx[W:]) if world == 1 and USE_GRAPH else None
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -368,7 +369,7 @@ def per_update_phase(rl, buf, B, K, W, world, seed):
         buf.update_priorities_device(idx, y, V)
     for i in range(W):
         step(i)
-    graph = rl.capture_updates(None, None, per_buffer=buf, uniforms=U[W:]) if world == 1 and not NO_GRAPH else None
+    graph = rl.capture_updates(None, None, per_buffer=buf, uniforms=U[W:]) if world == 1 and USE_GRAPH else None
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -453,13 +454,13 @@ def cpu_baseline_update(conf, rl, buf, B, seconds):
                 sample="%d updates at B=%d in %.1f s (oracle/nn.py, numpy float64)" % (n, B, dt))
 
 
-NO_GRAPH = False
+USE_GRAPH = False
 
 
 def main():
-    global NO_GRAPH
+    global USE_GRAPH
     args = parse()
-    NO_GRAPH = args.no_graph
+    USE_GRAPH = args.graph
     world, rank = init_dist()
     torch.backends.cuda.matmul.allow_tf32 = False
     conf, env, rl = make_learner(args.system)
