@@ -428,6 +428,32 @@ def cpu_baseline_rollout(conf, rl, roll, seconds):
                        % (e, len(roll["S0"]), steps, dt))
 
 
+def cpu_baseline_rollout_vectorized(conf, rl, roll, seconds):
+    """The same rollouts vectorised over episodes (oracle/rollout.py batched_policy_rollout_di):
+    numpy float64 with its BLAS threads, on growing episode prefixes until `seconds` elapse."""
+    from oracle import env as oenv
+    from oracle import rollout as oroll
+    oe = oenv.make_env(conf)
+    actor = rl.actor_model.get_weights()
+    S0, n = np.asarray(roll["S0"]), np.asarray(roll["nsteps"])
+    steps, e, t0 = 0, 64, time.perf_counter()
+    while True:
+        steps += oroll.batched_policy_rollout_di(oe, actor, S0[:e], n[:e])[0]
+        el = time.perf_counter() - t0
+        if el >= seconds or e >= len(S0):
+            break
+        e = min(2 * e, len(S0))
+    threads = None
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
+    except Exception:
+        pass
+    return dict(value=steps / el, unit="env-steps/s", cores=threads or 1, kind="port",
+                sample="%d env-steps over episode prefixes up to %d of %d, %.1f s, numpy vectorised over episodes"
+                       % (steps, e, len(S0), el))
+
+
 def cpu_baseline_update(conf, rl, buf, B, seconds):
     from oracle import env as oenv
     from oracle import nn as onn
@@ -490,6 +516,8 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline_rollout(conf, rl, roll, args.cpu_seconds)
         cpu["update"] = cpu_baseline_update(conf, rl, buf, 128, args.cpu_seconds / 2)
+        if args.system == "double_integrator":
+            cpu["vectorized"] = cpu_baseline_rollout_vectorized(conf, rl, roll, args.cpu_seconds / 2)
     traffic, traffic_src = pmc_traffic()
     if rank == 0:
         line = {

@@ -36,6 +36,50 @@ def policy_rollout(env, actor, s0, nsteps, weights=None):
     return S, A, R, EE
 
 
+def batched_policy_rollout_di(env, actor, S0, nsteps, weights=None):
+    """The same env-steps as `policy_rollout`, vectorised over episodes with numpy (the CPU
+    baseline SURVEY §8d asks for beside the per-sample port, so the GPU/CPU ratio is not inflated
+    by Python-loop overhead). Double integrator only: its Pinocchio chain has constant M and zero
+    nle (prismatic x, y joints; gravity normal to the plane), so Env.simulate (environment.py:80-91)
+    is v' = v + dt M^-1 u, q' = q + dt v for every episode at once. The actor runs in float64
+    matmuls (BLAS threads); rewards per environment.py:329-351. Returns (env-steps, final states)."""
+    conf = env.conf
+    w = np.asarray(conf.cost_weights_running if weights is None else weights, dtype=np.float64)
+    norm = np.asarray(conf.state_norm_arr, dtype=np.float64)
+    nq = env.chain.n
+    Minv = np.linalg.inv(env.chain.mass_matrix(np.zeros(nq)))
+    assert np.abs(env.chain.nle(np.zeros(nq), np.ones(nq))).max() == 0.0, "constant-dynamics chains only"
+    S = np.array(S0, dtype=np.float64)
+    nsteps = np.asarray(nsteps)
+    dt = conf.dt
+    o, tgt = env.obs, env.target
+    steps = 0
+    for t in range(int(nsteps.max())):
+        act = nsteps > t
+        s = S[act]
+        a = actor_forward(actor, s.astype(np.float32).astype(np.float64), norm).astype(np.float32).astype(np.float64)
+        q, v = s[:, :nq], s[:, nq:2 * nq]
+        x, y = q[:, 0], q[:, 1]
+        # reward at (s, a): - w0 dist + w1 peak - w3..5 ell - w6 u_cost + offset, times scale
+        ell = sum(w[3 + k] * np.log(np.exp(env.alpha * -(((x - o[2 * k]) ** 2) / ((o[6 + 2 * k] / 2) ** 2)
+                                                         + ((y - o[2 * k + 1]) ** 2) / ((o[7 + 2 * k] / 2) ** 2)
+                                                         - 1.0)) + 1) / env.alpha for k in range(3))
+        pk = (np.sqrt((x - tgt[0]) ** 2 + 0.1) - np.sqrt(0.1) - 0.1 + np.sqrt((y - tgt[1]) ** 2 + 0.1)
+              - np.sqrt(0.1) - 0.1)
+        peak = np.log(np.exp(env.alpha2 * -pk) + 1) / env.alpha2
+        u_cost = np.sum(a * a + conf.w_b * (a / conf.u_max) ** 10, axis=1)
+        r = env.scale * (-w[0] * ((x - tgt[0]) ** 2 + (y - tgt[1]) ** 2) + w[1] * peak - ell - w[6] * u_cost
+                         + env.offset)
+        sn = np.empty_like(s)
+        sn[:, :nq] = q + dt * v
+        sn[:, nq:2 * nq] = v + dt * (a @ Minv.T)
+        sn[:, -1] = s[:, -1] + dt
+        S[act] = sn
+        del r                       # the rewards are produced each step, as in PLOT.rollout
+        steps += int(act.sum())
+    return steps, S
+
+
 def nsteps_sh(conf, s0):
     return conf.NSTEPS - int(s0[-1] / conf.dt)
 

@@ -1,3 +1,4 @@
+import os
 """Internal checks that pin the oracle where no reference executable exists:
 finite differences for every gradient (incl. the Sobolev second-order term), an independent
 sympy Lagrangian for the planar manipulator, DI M = I / nle = 0, and the DI final-policy
@@ -262,3 +263,23 @@ def test_ur5_chain_matches_lagrangian():
             Jr[:3, :3] = np.eye(3) + np.sin(q[i]) * K + (1 - np.cos(q[i])) * K @ K
             Tw = Tw @ A @ Jr
         np.testing.assert_allclose(ee, Tw[:3, :3] @ model.ee_p + Tw[:3, 3], atol=1e-12)
+
+
+def test_vectorised_di_rollout_matches_per_sample_port():
+    """bench.py's vectorised CPU baseline computes the same trajectories as the per-sample port."""
+    import random
+    from cacto_amd.confs import load_conf
+    from oracle import env as oenv
+    from oracle import rollout as oroll
+    conf = load_conf("double_integrator")
+    oe = oenv.make_env(conf)
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "weights", "di_seed0_0.npz"))
+    actor = [z["actor_%d" % i] for i in range(6)]
+    rng = random.Random(4)
+    S0 = np.array([oe.reset(rng) for _ in range(12)])
+    n = np.array([oroll.nsteps_sh(conf, s) for s in S0])
+    steps, S = oroll.batched_policy_rollout_di(oe, actor, S0, n)
+    assert steps == int(n.sum())
+    for e in range(len(S0)):
+        ref = oroll.policy_rollout(oe, actor, S0[e], int(n[e]))[0][-1]
+        np.testing.assert_allclose(S[e], ref, rtol=1e-12, atol=1e-12)
