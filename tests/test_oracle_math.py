@@ -1,9 +1,9 @@
-import os
 """Internal checks that pin the oracle where no reference executable exists:
 finite differences for every gradient (incl. the Sobolev second-order term), an independent
 sympy Lagrangian for the planar manipulator, DI M = I / nle = 0, and the DI final-policy
 known-answer test against the reference's figure (SURVEY.md §8c)."""
 import math
+import os
 
 import numpy as np
 import pytest
