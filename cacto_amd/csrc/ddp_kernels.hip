@@ -78,6 +78,67 @@ __device__ inline void planar_pos_derivs(const cacto_sys_params& p, const double
   }
 }
 
+// Position terms of a revolute chain's reward: l_q, l_qq by the chain rule through one float64
+// forward-kinematics pass. With z_i, o_i joint i's world axis and origin and p the EE position:
+// dp/dq_i = z_i x (p - o_i) and d2p/dq_i dq_j = z_i x (z_j x (p - o_j)) for i <= j (0 past the EE's
+// parent joint); dr/dp, d2r/dp2 from hyper-dual evaluations of the position reward (6 passes).
+// l_q = J^T dr/dp, l_qq = J^T (d2r/dp2) J + sum_c dr/dp_c d2p_c/dq2. Returns false (caller falls back
+// to hyper-dual kinematics) if a joint up to the EE is prismatic.
+template <int NJ>
+__device__ inline bool chain_pos_derivs(const SysDevice& sd, const double* w, const double* q, double* lx,
+                                        double* lxx, int ldl) {
+  const cacto_sys_params& p = sd.p;
+  const int e = p.ee_parent;
+  V3 z[NJ], o[NJ];
+  M3 oR;
+  V3 op;
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    const JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    if (i <= e && j.kind() != 0) return false;
+    const SE3 X = joint_placement(j, q[i]);
+    if (i == 0) {
+      oR = X.R;
+      op = X.p;
+    } else {
+      op = mul(oR, X.p) + op;
+      oR = mul(oR, X.R);
+    }
+    z[i] = mul(oR, j.axis());
+    o[i] = op;
+    if (i == e) break;
+  }
+  // EE: oR, op are joint e's frame when the loop ended
+  const V3 pe = mul(oR, v3(p.ee_p[0], p.ee_p[1], p.ee_p[2])) + op;
+  double g[3], H[9];
+  for (int a = 0; a < 3; ++a)
+    for (int b = a; b < 3; ++b) {
+      V3T<HD> P{HD(pe.x, a == 0, b == 0, 0.0), HD(pe.y, a == 1, b == 1, 0.0), HD(pe.z, a == 2, b == 2, 0.0)};
+      const HD r = chain_pos_reward_t(p, w, P);
+      if (a == b) g[a] = r.a;
+      H[a * 3 + b] = H[b * 3 + a] = r.ab;
+    }
+  V3 Jc[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) Jc[i] = i <= e ? cross(z[i], pe - o[i]) : v3(0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    lx[i] = g[0] * Jc[i].x + g[1] * Jc[i].y + g[2] * Jc[i].z;
+    const V3 HJi = v3(H[0] * Jc[i].x + H[1] * Jc[i].y + H[2] * Jc[i].z, H[3] * Jc[i].x + H[4] * Jc[i].y + H[5] * Jc[i].z,
+                      H[6] * Jc[i].x + H[7] * Jc[i].y + H[8] * Jc[i].z);
+#pragma unroll
+    for (int k = i; k < NJ; ++k) {
+      double v = dot(Jc[k], HJi);
+      if (k <= e) {
+        const V3 d2 = cross(z[i], cross(z[k], pe - o[k]));
+        v += g[0] * d2.x + g[1] * d2.y + g[2] * d2.z;
+      }
+      lxx[i * ldl + k] = lxx[k * ldl + i] = v;
+    }
+  }
+  return true;
+}
+
 // l_x [N], l_xx [N*N] of the reward with weights w at state x (time excluded).
 template <int NJ>
 __device__ inline void ddp_lx(const SysDevice& sd, const double* w, const double* x, double* lx, double* lxx) {
@@ -106,17 +167,19 @@ __device__ inline void ddp_lx(const SysDevice& sd, const double* w, const double
       // revolute chains: position terms through hyper-dual forward kinematics, one pass per
       // (j <= k) joint pair; the velocity term - scale w2 |v|^2 in closed form
       constexpr int nq = NJ > 0 ? NJ : 1;
+      if (!chain_pos_derivs<nq>(sd, w, x, lx, lxx, N)) {
 #pragma unroll 1
-      for (int j = 0; j < nq; ++j)
+        for (int j = 0; j < nq; ++j)
 #pragma unroll 1
-        for (int k = j; k < nq; ++k) {
-          HD q[nq];
+          for (int k = j; k < nq; ++k) {
+            HD q[nq];
 #pragma unroll
-          for (int i = 0; i < nq; ++i) q[i] = HD(x[i], i == j ? 1.0 : 0.0, i == k ? 1.0 : 0.0, 0.0);
-          const HD r = chain_pos_reward_t(p, w, chain_ee_t<nq, HD>(sd, q));
-          if (k == j) lx[j] = r.a;
-          lxx[j * N + k] = lxx[k * N + j] = r.ab;
-        }
+            for (int i = 0; i < nq; ++i) q[i] = HD(x[i], i == j ? 1.0 : 0.0, i == k ? 1.0 : 0.0, 0.0);
+            const HD r = chain_pos_reward_t(p, w, chain_ee_t<nq, HD>(sd, q));
+            if (k == j) lx[j] = r.a;
+            lxx[j * N + k] = lxx[k * N + j] = r.ab;
+          }
+      }
 #pragma unroll
       for (int i = nq; i < N; ++i) {
         lx[i] = -(p.scale * (w[2] * (2.0 * x[i])));
@@ -340,14 +403,13 @@ __global__ void __launch_bounds__(64) k_ddp_derivs(const SysDevice* __restrict__
   for (int k = 0; k < N * M; ++k) rec[(size_t)(RC::B + k) * n_ep] = B[k];
 }
 
-// The Riccati recursion, one thread per episode (sequential in t). WS: read A, B, l_x, l_xx from
-// the k_ddp_derivs records; otherwise (SI, car, DI: closed forms) compute them inline.
-template <int NJ, bool WS>
+// The fused pass for the closed-form systems (SI, car, DI): one thread per episode computes each
+// step's A, B, l_x, l_xx inline and runs the Riccati recursion (sequential in t).
+template <int NJ>
 __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
                                                       int64_t ldS, const double* __restrict__ U, int64_t ldU,
                                                       const int32_t* __restrict__ nsteps, int n_ep, double mu,
-                                                      const double* __restrict__ ws, double* __restrict__ dVdx) {
-  using RC = DdpRec<NJ>;
+                                                      double* __restrict__ dVdx) {
   constexpr int N = DdpDims<NJ>::N, M = DdpDims<NJ>::M, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_ep) return;
@@ -358,16 +420,13 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
   const double* Ue = U + (size_t)e * ldU * na;
   double* Oe = dVdx + (size_t)e * ldS * ns;
   double Minv[NJ > 0 ? M * M : 1];
-  const bool chain_const = NJ > 0 && p.const_dyn;
   if constexpr (NJ > 0) {
-    if (chain_const) {
-      // prismatic chain: M constant; its inverse once per episode
-      double Mm[M * M], q[NJ];
+    // prismatic chain (the launcher sends only constant-M chains here): M^-1 once per episode
+    double Mm[M * M], q[NJ];
 #pragma unroll
-      for (int i = 0; i < NJ; ++i) q[i] = Se[i];
-      chain_mass<NJ>(sd, q, Mm);
-      small_inverse<M>(Mm, Minv);
-    }
+    for (int i = 0; i < NJ; ++i) q[i] = Se[i];
+    chain_mass<NJ>(sd, q, Mm);
+    small_inverse<M>(Mm, Minv);
   }
   double w_run[7], w_term[7];
 #pragma unroll
@@ -378,15 +437,7 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
   double Vx[N], Vxx[N * N], x[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) x[k] = Se[(size_t)Te * ns + k];
-  if constexpr (WS) {
-    const double* rec = ws + (size_t)Te * RC::R * n_ep + e;
-#pragma unroll
-    for (int k = 0; k < N; ++k) Vx[k] = rec[(size_t)(RC::LX + k) * n_ep];
-#pragma unroll
-    for (int k = 0; k < N * N; ++k) Vxx[k] = rec[(size_t)(RC::LXX + k) * n_ep];
-  } else {
-    ddp_lx<NJ>(sd, w_term, x, Vx, Vxx);
-  }
+  ddp_lx<NJ>(sd, w_term, x, Vx, Vxx);
 #pragma unroll
   for (int k = 0; k < N; ++k) Oe[(size_t)Te * ns + k] = Vx[k];
   Oe[(size_t)Te * ns + N] = 0.0;
@@ -396,20 +447,8 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
     for (int k = 0; k < N; ++k) x[k] = Se[(size_t)i * ns + k];
 #pragma unroll
     for (int k = 0; k < M; ++k) u[k] = Ue[(size_t)i * na + k];
-    if constexpr (WS) {
-      const double* rec = ws + (size_t)i * RC::R * n_ep + e;
-#pragma unroll
-      for (int k = 0; k < N * N; ++k) A[k] = rec[(size_t)(RC::A + k) * n_ep];
-#pragma unroll
-      for (int k = 0; k < N * M; ++k) B[k] = rec[(size_t)(RC::B + k) * n_ep];
-#pragma unroll
-      for (int k = 0; k < N; ++k) lx[k] = rec[(size_t)(RC::LX + k) * n_ep];
-#pragma unroll
-      for (int k = 0; k < N * N; ++k) lxx[k] = rec[(size_t)(RC::LXX + k) * n_ep];
-    } else {
-      ddp_jacobians<NJ>(sd, x, Minv, A, B);
-      ddp_lx<NJ>(sd, w_run, x, lx, lxx);
-    }
+    ddp_jacobians<NJ>(sd, x, Minv, A, B);
+    ddp_lx<NJ>(sd, w_run, x, lx, lxx);
     // Q_x = l_x + A^T V_x, Q_u = l_u + B^T V_x
     double Qx[N], Qu[M], Qxx[N * N], Quu[M * M], Qxu[N * M], VA[N * N], VB[N * M];
 #pragma unroll
@@ -517,6 +556,140 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
   }
 }
 
+// The Riccati recursion of the split pass with one wavefront per episode: the lanes share each
+// step's matrix products (outputs spread over lanes, operands in LDS), so the N = 12 recursion of
+// UR5 is ~N^3 / 64 dependent FMAs per product instead of N^3 on one thread. Same products, same
+// summation order as k_ddp_backward; Qbar_uu^-1 (M x M) on lane 0.
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ddp_riccati_wave(const SysDevice* __restrict__ sdp,
+                                                         const double* __restrict__ U, int64_t ldU,
+                                                         const int32_t* __restrict__ nsteps, int n_ep, double mu,
+                                                         const double* __restrict__ ws, int64_t ldS,
+                                                         double* __restrict__ dVdx) {
+  using RC = DdpRec<NJ>;
+  constexpr int N = RC::N, M = RC::M, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  __shared__ double sA[N * N], sB[N * M], sLx[N], sLxx[N * N], sVx[N], sVxx[N * N], sU[M];
+  __shared__ double sVA[N * N], sVB[N * M], sQx[N], sQu[M], sQxx[N * N], sQxu[N * M], sQuu[M * M], sQi[M * M];
+  __shared__ double sK[M], sQK[N * M];
+  const int e = blockIdx.x, lane = threadIdx.x;
+  const cacto_sys_params& p = sdp->p;
+  const double w6 = p.w_running[6];
+  const int Te = nsteps[e];
+  double* Oe = dVdx + (size_t)e * ldS * ns;
+  const double* Ue = U + (size_t)e * ldU * na;
+  {
+    const double* rec = ws + (size_t)Te * RC::R * n_ep + e;
+    for (int k = lane; k < N; k += 64) sVx[k] = rec[(size_t)(RC::LX + k) * n_ep];
+    for (int k = lane; k < N * N; k += 64) sVxx[k] = rec[(size_t)(RC::LXX + k) * n_ep];
+  }
+  __syncthreads();
+  for (int k = lane; k <= N; k += 64) Oe[(size_t)Te * ns + k] = k < N ? sVx[k] : 0.0;
+  for (int i = Te - 1; i >= 0; --i) {
+    const double* rec = ws + (size_t)i * RC::R * n_ep + e;
+    for (int k = lane; k < N * N; k += 64) {
+      sA[k] = rec[(size_t)(RC::A + k) * n_ep];
+      sLxx[k] = rec[(size_t)(RC::LXX + k) * n_ep];
+    }
+    for (int k = lane; k < N * M; k += 64) sB[k] = rec[(size_t)(RC::B + k) * n_ep];
+    for (int k = lane; k < N; k += 64) sLx[k] = rec[(size_t)(RC::LX + k) * n_ep];
+    for (int k = lane; k < M; k += 64) sU[k] = Ue[(size_t)i * na + k];
+    __syncthreads();
+    // V_xx A, V_xx B, Q_x = l_x + A^T V_x, Q_u = l_u + B^T V_x
+    for (int o = lane; o < N * N + N * M + N + M; o += 64) {
+      double s = 0.0;
+      if (o < N * N) {
+        const int r = o / N, c = o - r * N;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += sVxx[r * N + k] * sA[k * N + c];
+        sVA[o] = s;
+      } else if (o < N * N + N * M) {
+        const int q = o - N * N, r = q / M, c = q - r * M;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += sVxx[r * N + k] * sB[k * M + c];
+        sVB[q] = s;
+      } else if (o < N * N + N * M + N) {
+        const int r = o - N * N - N * M;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += sA[k * N + r] * sVx[k];
+        sQx[r] = sLx[r] + s;
+      } else {
+        const int j = o - N * N - N * M - N;
+        const double um = p.u_max[j], u = sU[j];
+        const double lu = p.scale * (-w6 * (2.0 * u + p.w_b * 10.0 * pow(u / um, 9.0) / um));
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += sB[k * M + j] * sVx[k];
+        sQu[j] = lu + s;
+      }
+    }
+    __syncthreads();
+    // Q_xx = l_xx + A^T V_xx A, Q_xu = A^T V_xx B, Qbar_uu = l_uu + B^T V_xx B + mu I
+    for (int o = lane; o < N * N + N * M + M * M; o += 64) {
+      double s = 0.0;
+      if (o < N * N) {
+        const int r = o / N, c = o - r * N;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += sA[k * N + r] * sVA[k * N + c];
+        sQxx[o] = sLxx[o] + s;
+      } else if (o < N * N + N * M) {
+        const int q = o - N * N, r = q / M, c = q - r * M;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += sA[k * N + r] * sVB[k * M + c];
+        sQxu[q] = s;
+      } else {
+        const int q = o - N * N - N * M, r = q / M, c = q - r * M;
+#pragma unroll
+        for (int k = 0; k < N; ++k) s += sB[k * M + r] * sVB[k * M + c];
+        const double um = p.u_max[r];
+        const double luu =
+            r == c ? p.scale * (-w6 * (2.0 + p.w_b * 90.0 * pow(sU[r] / um, 8.0) / (um * um))) : 0.0;
+        sQuu[q] = luu + s + (r == c ? mu : 0.0);
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+      double a[M * M], inv[M * M];
+#pragma unroll
+      for (int k = 0; k < M * M; ++k) a[k] = sQuu[k];
+      small_inverse<M>(a, inv);
+#pragma unroll
+      for (int r = 0; r < M; ++r) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) s += inv[r * M + k] * sQu[k];
+        sK[r] = s;
+      }
+#pragma unroll
+      for (int k = 0; k < M * M; ++k) sQi[k] = inv[k];
+    }
+    __syncthreads();
+    // V_x = Q_x - Q_xu (Qbar^-1 Q_u); row r of Q_xu Qbar^-1
+    for (int o = lane; o < N + N * M; o += 64) {
+      double s = 0.0;
+      if (o < N) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) s += sQxu[o * M + k] * sK[k];
+        sVx[o] = sQx[o] - s;
+      } else {
+        const int q = o - N, r = q / M, c = q - r * M;
+#pragma unroll
+        for (int k = 0; k < M; ++k) s += sQxu[r * M + k] * sQi[k * M + c];
+        sQK[q] = s;
+      }
+    }
+    __syncthreads();
+    // V_xx = Q_xx - (Q_xu Qbar^-1) Q_xu^T
+    for (int o = lane; o < N * N; o += 64) {
+      const int r = o / N, c = o - r * N;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) s += sQK[r * M + k] * sQxu[c * M + k];
+      sVxx[o] = sQxx[o] - s;
+    }
+    for (int k = lane; k <= N; k += 64) Oe[(size_t)i * ns + k] = k < N ? sVx[k] : 0.0;
+    __syncthreads();
+  }
+}
+
 }  // namespace cacto
 
 using namespace cacto;
@@ -563,11 +736,11 @@ struct LaunchDdp {
         hipLaunchKernelGGL(k_ddp_derivs<NJ>, dim3(ceil_div(n_ep, 64), (unsigned)ldS), dim3(64), 0, st, sys->dev, S,
                            ldS, U, ldU, n, n_ep, ws);
         CACTO_CHECK_HIP(hipGetLastError());
-        hipLaunchKernelGGL((k_ddp_backward<NJ, true>), dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS, U,
-                           ldU, n, n_ep, mu, ws, out);
+        hipLaunchKernelGGL(k_ddp_riccati_wave<NJ>, dim3(n_ep), dim3(64), 0, st, sys->dev, U, ldU, n, n_ep, mu, ws,
+                           ldS, out);
       } else {
-        hipLaunchKernelGGL((k_ddp_backward<NJ, false>), dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS,
-                           U, ldU, n, n_ep, mu, nullptr, out);
+        hipLaunchKernelGGL(k_ddp_backward<NJ>, dim3(ceil_div(n_ep, 64)), dim3(64), 0, st, sys->dev, S, ldS, U, ldU,
+                           n, n_ep, mu, out);
       }
       CACTO_CHECK_HIP(hipGetLastError());
       return CACTO_OK;
