@@ -5,9 +5,10 @@
 //   * dtau/dq, dtau/dv of RNEA(q, v, qdd) -> ddq_dq = -M^-1 dtau/dq, ddq_dv = -M^-1 dtau/dv, i.e.
 //     Pinocchio's computeABADerivatives (environment.py:111-132) — one RNEA per joint gives the
 //     q-direction (a part) and the v-direction (b part) of that joint;
-//   * l_x, l_xx of the TO running / terminal cost through the forward kinematics (manipulator,
-//     UR5) and the car_park check points (environment_TO.py:605-631, :731-758, :479-503): one
-//     evaluation per (j <= k) pair of state coordinates.
+//   * the TO cost's derivatives in a point: the EE position of a chain (environment_TO.py:605-631,
+//     :731-758) or a car_park check point (:479-503) — three passes give its gradient and Hessian,
+//     which ddp_kernels.hip composes with the kinematics (chain rule); chains with a prismatic joint
+//     before the EE fall back to hyper-dual forward kinematics, one pass per (j <= k) joint pair.
 // The spatial algebra mirrors env.h (Pinocchio ordering (linear, angular)), templated on the
 // scalar; the rigid-body inertias stay float64 constants.
 #pragma once
@@ -302,26 +303,6 @@ __device__ inline T box_cost_t(const T& x, const T& y, double xs, double ys, dou
   const T q3 = sqrt(4.0 + 4.0 * (ax * ax) * (k * k)), q4 = sqrt(4.0 + 4.0 * (bx * bx) * (k * k));
   return (-0.5 * q2 + by * k) / (q1 * q2) * (0.5 * q1 + ay * k) * (0.5 * q3 + ax * k) / (q3 * q4) *
          (-0.5 * q4 + bx * k);
-}
-
-// car_park reward without the control term (environment_TO.py:479-503): x = (x, y, theta, v, delta)
-template <typename T>
-__device__ inline T carpark_reward_t(const cacto_sys_params& P, const double* w, const T* x) {
-  T s, c;
-  sincos(x[2], &s, &c);
-  const double h = P.L_delta / 2.0;
-  const T px = x[0] + c * h, py = x[1] + s * h;
-  T obs = T(0.0);
-  for (int ob = 0; ob < 3; ++ob)
-    for (int k = 0; k < P.n_check; ++k) {
-      const double bx = P.check_points[2 * k], by = P.check_points[2 * k + 1];
-      const T wx = c * bx - s * by + px, wy = s * bx + c * by + py;
-      obs = obs + box_cost_t(wx, wy, P.obs[2 * ob], P.obs[2 * ob + 1], P.obs[6 + 2 * ob], P.obs[7 + 2 * ob], P.k_db);
-    }
-  T d[2] = {px - P.target[0], py - P.target[1]};
-  const T cost = w[0] * (d[0] * d[0] + d[1] * d[1]) - w[1] * peak_t<2>(P.alpha2, d) + w[2] * (x[3] * x[3]) +
-                 w[3] * obs;
-  return -(P.scale * cost);
 }
 
 }  // namespace cacto

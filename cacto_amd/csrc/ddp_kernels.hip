@@ -149,18 +149,49 @@ __device__ inline void ddp_lx(const SysDevice& sd, const double* w, const double
 #pragma unroll
   for (int k = 0; k < N; ++k) lx[k] = 0.0;
   if constexpr (NJ == -2) {
-    // car_park: the reward depends on (x, y, theta, v); one hyper-dual evaluation per pair
+    // car_park (environment_TO.py:479-503): every position term is a function of one planar point
+    // Z(x, y, theta) — p_ee for the target terms, p_ee + R(theta) c_k for the 30 (box, check point)
+    // pairs. Its gradient / Hessian in Z come from 3 hyper-dual passes; the rigid map Z has
+    // dZ/d(x, y) = I, dZ/dtheta = (-(Z_y - y), Z_x - x), d2Z/dtheta2 = -(Z - (x, y)).
+    double sn, cs;
+    sincos(x[2], &sn, &cs);
+    const double h = p.L_delta / 2.0;
+    const double pex = x[0] + cs * h, pey = x[1] + sn * h;
+    auto add_point = [&](double Zx, double Zy, auto&& f) {
+      const HD rxx = f(HD(Zx, 1.0, 1.0, 0.0), HD(Zy));
+      const HD rxy = f(HD(Zx, 1.0, 0.0, 0.0), HD(Zy, 0.0, 1.0, 0.0));
+      const HD ryy = f(HD(Zx), HD(Zy, 1.0, 1.0, 0.0));
+      const double gx = rxy.a, gy = rxy.b, Hxx = rxx.ab, Hxy = rxy.ab, Hyy = ryy.ab;
+      const double tx = -(Zy - x[1]), ty = Zx - x[0];   // dZ/dtheta
+      lx[0] += gx;
+      lx[1] += gy;
+      lx[2] += gx * tx + gy * ty;
+      lxx[0] += Hxx;
+      lxx[1] += Hxy;
+      lxx[N + 1] += Hyy;
+      lxx[2] += Hxx * tx + Hxy * ty;
+      lxx[N + 2] += Hxy * tx + Hyy * ty;
+      lxx[2 * N + 2] += tx * (Hxx * tx + Hxy * ty) + ty * (Hxy * tx + Hyy * ty) - gx * (Zx - x[0]) - gy * (Zy - x[1]);
+    };
+    add_point(pex, pey, [&](HD X, HD Y) {
+      HD d[2] = {X - p.target[0], Y - p.target[1]};
+      return -(p.scale * (w[0] * (d[0] * d[0] + d[1] * d[1]) - w[1] * peak_t<2>(p.alpha2, d)));
+    });
 #pragma unroll 1
-    for (int j = 0; j < 4; ++j)
-#pragma unroll 1
-      for (int k = j; k < 4; ++k) {
-        HD xs[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xs[i] = HD(x[i], i == j ? 1.0 : 0.0, i == k ? 1.0 : 0.0, 0.0);
-        const HD r = carpark_reward_t(p, w, xs);
-        if (k == j) lx[j] = r.a;
-        lxx[j * N + k] = lxx[k * N + j] = r.ab;
-      }
+    for (int k = 0; k < p.n_check; ++k) {
+      const double bx = p.check_points[2 * k], by = p.check_points[2 * k + 1];
+      add_point(cs * bx - sn * by + pex, sn * bx + cs * by + pey, [&](HD X, HD Y) {
+        HD b = HD(0.0);
+        for (int ob = 0; ob < 3; ++ob)
+          b = b + box_cost_t(X, Y, p.obs[2 * ob], p.obs[2 * ob + 1], p.obs[6 + 2 * ob], p.obs[7 + 2 * ob], p.k_db);
+        return -(p.scale * (w[3] * b));
+      });
+    }
+    lxx[N] = lxx[1];
+    lxx[2 * N] = lxx[2];
+    lxx[2 * N + 1] = lxx[N + 2];
+    lx[3] = -(p.scale * (w[2] * (2.0 * x[3])));
+    lxx[3 * N + 3] = -(p.scale * (w[2] * 2.0));
     return;
   } else {
     if (NJ > 2 && p.reward_kind != CACTO_REW_PLANAR) {
