@@ -54,3 +54,40 @@ def test_graph_replay_equals_eager_updates():
     for a, b in zip(_state(eager), _state(graphed)):
         assert torch.equal(a, b)
     assert int(graphed.steps[0]) == K and int(graphed.steps[1]) == K
+
+
+def test_graph_replay_equals_eager_updates_with_per():
+    """learn_and_update with PER (RL.py:122-137): sample -> update -> priority update, replayed as one
+    graph, leaves the weights, the sum / min trees and the experience counters as the eager loop."""
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    conf = load_conf("double_integrator")
+    conf.prioritized_replay_alpha = 0.6
+    env = make_env(conf)
+    ns = conf.nb_state
+    rng = np.random.default_rng(9)
+    N, B, K = 3000, 64, 5
+    S = np.column_stack([rng.uniform(-15, 15, (N, 4)), rng.uniform(0, 9.9, N)])
+    rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.05, rng.normal(size=(N, ns)) * 0.3,
+                           np.zeros((N, 1)), np.zeros((N, 1))], axis=1)
+    U = torch.as_tensor(rng.uniform(size=(K, B)), device="cuda")
+
+    def setup():
+        rl = _learner(conf, env)
+        buf = PrioritizedReplayBuffer(conf, env.sys)
+        buf.add_rows(rows)
+        return rl, buf
+    eager, ebuf = setup()
+    y = torch.empty(B, dtype=torch.float32, device="cuda")
+    V = torch.empty_like(y)
+    for k in range(K):
+        idx, w = ebuf.sample_device(U[k])
+        eager.update_rows(ebuf.storage, idx, w, y, V)
+        ebuf.update_priorities_device(idx, y, V)
+    graphed, gbuf = setup()
+    g = graphed.capture_updates(None, None, per_buffer=gbuf, uniforms=U)
+    g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(_state(eager), _state(graphed)):
+        assert torch.equal(a, b)
+    for name in ("sum_tree", "min_tree", "exp_counter"):
+        assert torch.equal(getattr(ebuf, name), getattr(gbuf, name)), name
