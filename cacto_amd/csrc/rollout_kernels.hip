@@ -114,6 +114,22 @@ __device__ __forceinline__ void ro_load_actor(const NetView& N, const Lane& L, R
 
 __device__ __forceinline__ float lrelu(float z) { return z > 0.f ? z : fmul(z, 0.3f); }
 
+// v + (v of the lane `off` above): the butterfly level of layer 3 as seen by the lanes that keep
+// the result (lane j < off of a segment adds lane j + off, exactly what __shfl_xor gives those
+// lanes, so the sums are bit-identical). Offsets below 16 stay inside a 16-lane DPP row and use a
+// row shift (a few cycles) instead of a ds_bpermute round trip through the LDS pipe.
+__device__ __forceinline__ float add_from_above(float v, int off) {
+  float o;
+  switch (off) {
+    case 8: o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x108, 0xF, 0xF, true)); break;
+    case 4: o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x104, 0xF, 0xF, true)); break;
+    case 2: o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x102, 0xF, 0xF, true)); break;
+    case 1: o = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xF, 0xF, true)); break;
+    default: o = __shfl_down(v, off); break;
+  }
+  return v + o;
+}
+
 // Actor forward of the workgroup's SL slots: x0 -> h1 -> h2 -> a. Contains 3 barriers (the last
 // one publishes W.a).
 template <int NG, int NS, int NA, int REGK, int LDSK>
@@ -213,7 +229,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
 #pragma unroll
     for (int off = C::P / 2; off >= 1; off >>= 1)
 #pragma unroll
-      for (int a = 0; a < NA; ++a) pa[a][0] += __shfl_xor(pa[a][0], off);
+      for (int a = 0; a < NA; ++a) pa[a][0] = add_from_above(pa[a][0], off);
     if (seg == 0)
 #pragma unroll
       for (int a = 0; a < NA; ++a) W.a[s * NA + a] = fadd(pa[a][0], W.b3[a]);
