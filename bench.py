@@ -320,13 +320,18 @@ def episode_to_buffer_phase(rl, conf, roll, env, K, dVdx=None):
 
 
 def update_phase(rl, buf, B, K, W, world, seed):
-    """K learn_and_update iterations (RL.py:101-118 each) on pre-drawn minibatch indices. With
-    --graph (one rank) the K updates replay as one HIP graph (RL_AC.capture_updates, captured before
-    the timed region): the same kernels with the same arguments."""
+    """K learn_and_update iterations (RL.py:101-118 each) on pre-drawn minibatch indices, as the
+    package's learn_and_update runs them: one RL_AC.update_rows_n call (the critic step of update
+    t+1 overlaps the actor step of update t; bit-identical to K sequential updates). With --graph
+    (one rank) the K updates replay as one HIP graph of the sequential loop instead. With N > 1
+    ranks each update is the data-parallel one (RCCL all-reduce of both gradients)."""
     gen = np.random.Generator(np.random.PCG64(seed))
     idx = torch.as_tensor(gen.integers(0, buf.max_idx(), size=(K + W, B)).astype(np.int32), device="cuda")
-    for i in range(W):
-        rl.update_rows(buf.storage, idx[i])
+    if world == 1 and not USE_GRAPH:
+        rl.update_rows_n(buf.storage, idx[:W])     # warm-up on the timed path (creates its stream)
+    else:
+        for i in range(W):
+            rl.update_rows(buf.storage, idx[i])
     graph = rl.capture_updates(buf.storage, idx[W:]) if world == 1 and USE_GRAPH else None
     barrier(world)
     torch.cuda.synchronize()
@@ -334,8 +339,7 @@ def update_phase(rl, buf, B, K, W, world, seed):
     if graph is not None:
         graph.replay()
     else:
-        for i in range(K):
-            rl.update_rows(buf.storage, idx[W + i])
+        rl.update_rows_n(buf.storage, idx[W:])      # K updates, critic(t+1) overlapping actor(t)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)

@@ -104,6 +104,10 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   if (!sys) return CACTO_OK;
   (void)hipFree(sys->dev);
   if (sys->ddp_ws) (void)hipFree(sys->ddp_ws);
+  if (sys->side) (void)hipStreamSynchronize(sys->side);
+  if (sys->ev_critic) (void)hipEventDestroy(sys->ev_critic);
+  if (sys->ev_actor) (void)hipEventDestroy(sys->ev_actor);
+  if (sys->side) (void)hipStreamDestroy(sys->side);
   delete sys;
   return CACTO_OK;
 }

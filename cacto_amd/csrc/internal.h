@@ -10,6 +10,8 @@ struct cacto_sys {
   cacto::NetTopo actor, critic;
   void* ddp_ws = nullptr;  // cacto_ddp_backward's per-step derivative records (grow-only)
   size_t ddp_ws_bytes = 0;
+  hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its two events
+  hipEvent_t ev_critic = nullptr, ev_actor = nullptr;
 };
 
 namespace cacto {

@@ -667,7 +667,8 @@ inline int wg_chunk(int rows) { return rows <= 1024 ? 64 : rows <= 4096 ? 128 : 
 
 struct Workspace {
   GradBufs crit, act;
-  float* slab;
+  float* slab;    // critic weight-gradient slabs
+  float* slab_a;  // actor's (a separate region: cacto_update_n overlaps the two steps)
   float* scal;  // y, V, Vt scratch (3 * Bp)
   size_t bytes;
   int Bp;
@@ -695,18 +696,20 @@ Workspace plan(const cacto_sys* sys, int B, char* base) {
   }
   w.act.ld = Bp;
   w.act.Bp = Bp;
-  size_t aoff = 0;
+  size_t aoff = align64(coff);  // the actor panels follow the critic's (no aliasing, see slab_a)
   for (int l = 0; l < ta.L; ++l) {
     w.act.LT[l] = f ? f + aoff : nullptr;
     aoff += (size_t)16 * ta.KT[l] * w.act.ld;
     w.act.RT[l] = f ? f + aoff : nullptr;
     aoff += (size_t)16 * ta.OT[l] * w.act.ld;
   }
-  off = align64(std::max(coff, aoff));
+  off = align64(aoff);
   const int nch_a = ceil_div(Bp, wg_chunk(Bp));
-  const int nch_c = std::max(ceil_div(2 * Bp, wg_chunk(2 * Bp)), nch_a);  // Sobolev rows, or the plain half
+  const int nch_c = ceil_div(2 * Bp, wg_chunk(2 * Bp));  // Sobolev rows, or the plain half
   w.slab = f ? f + off : nullptr;
-  off += align64(std::max((size_t)nch_c * tc.params, (size_t)nch_a * ta.params));
+  off += align64((size_t)nch_c * tc.params);
+  w.slab_a = f ? f + off : nullptr;
+  off += align64((size_t)nch_a * ta.params);
   w.scal = f ? f + off : nullptr;
   off += align64((size_t)3 * Bp);
   w.bytes = off * sizeof(float);
@@ -784,16 +787,20 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
   return CACTO_OK;
 }
 
-int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
-                                 const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
-                                 int* nch_out) {
+int launch_actor_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                       const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st) {
   NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
   NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
   const ChainScalars cs = chain_scalars(cfg, B);
-  if (int e = dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st))
-    return e;
+  return dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st);
+}
+
+int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                 const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
+                                 int* nch_out) {
+  if (int e = launch_actor_chain(sys, nets, cfg, storage, idx, B, w, st)) return e;
   WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
-  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
+  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
   CACTO_CHECK_HIP(hipGetLastError());
   *nch_out = a.nch;
   return CACTO_OK;
@@ -855,7 +862,7 @@ extern "C" int cacto_actor_grad(const cacto_sys* sys, const cacto_nets* nets, co
   int nch = 0;
   if (int e = launch_actor_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, B, w, st, &nch)) return e;
   const int P = sys->actor.params;
-  hipLaunchKernelGGL(k_reduce, dim3(std::min((P + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, P, grad_d);
+  hipLaunchKernelGGL(k_reduce, dim3(std::min((P + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, nch, P, grad_d);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }
@@ -892,5 +899,52 @@ extern "C" int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const 
     return e;
   if (int e = launch_adam(sys, nets, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st)) return e;
   if (int e = launch_actor_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, B, w, st, &nch)) return e;
-  return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab, nch, 0, st);
+  return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, nch, 0, st);
+}
+
+// K consecutive updates (learn_and_update's loop with its minibatches drawn up front, RL.py:120-143)
+// as a two-stream pipeline. The critic step of update t+1 reads only the critic, the target and the
+// rows — not the actor — so it runs while the actor step of update t is still going:
+//   stream  : critic chain(t), wgrad(t), [wait: actor chain(t-1) has read the critic], Adam(t) + soft
+//   side    : [wait: Adam(t)], actor chain(t), wgrad(t), Adam(t)
+// Every kernel sees the same inputs as in K sequential cacto_update calls, so the results are
+// bit-identical; the side stream joins the caller's stream before returning.
+extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                              const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
+                              size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && idx_d && B > 0 && K >= 0, "cacto_update_n: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  if (K == 0) return CACTO_OK;
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  hipStream_t st = as_stream(stream);
+  cacto_sys* ms = const_cast<cacto_sys*>(sys);
+  if (!ms->side) {
+    CACTO_CHECK_HIP(hipStreamCreateWithFlags(&ms->side, hipStreamNonBlocking));
+    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_critic, hipEventDisableTiming));
+    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_actor, hipEventDisableTiming));
+  }
+  hipStream_t side = ms->side;
+  CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));  // everything the caller queued before
+  CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+  for (int t = 0; t < K; ++t) {
+    const int32_t* idx = idx_d + (size_t)t * B;
+    int nch = 0;
+    if (int e = launch_critic_chain_and_wgrad(sys, nets, cfg, storage_d, idx, nullptr, B, nullptr, nullptr, nullptr, w,
+                                              st, &nch))
+      return e;
+    if (t > 0) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor, 0));  // actor chain(t-1) is done reading
+    if (int e = launch_adam(sys, nets, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st)) return e;
+    CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+    CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+    if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx, B, w, side)) return e;
+    CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor, side));
+    WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
+    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, side, a, w.slab_a);
+    CACTO_CHECK_HIP(hipGetLastError());
+    if (int e = launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, a.nch, 0, side)) return e;
+  }
+  CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor, side));
+  CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor, 0));
+  return CACTO_OK;
 }

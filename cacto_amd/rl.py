@@ -183,6 +183,22 @@ class RL_AC:
                      dptr(idx, torch.int32), dptr(is_w), B, dptr(y), dptr(V), dptr(Vt), dptr(ws), ws.numel() * 4,
                      stream())
 
+    def update_rows_n(self, storage, idx_steps):
+        """len(idx_steps) consecutive RL.py:101-118 updates on the minibatch indices idx_steps [K, B]
+        (int32, device) in one call: `cacto_update_n` overlaps the critic step of update t+1 with the
+        actor step of update t on a second stream (the critic step never reads the actor), with
+        results bit-identical to K update_rows calls. Single rank (the data-parallel update
+        all-reduces between the two steps)."""
+        if self.dp_world > 1:
+            for k in range(idx_steps.shape[0]):
+                self.update_rows(storage, idx_steps[k])
+            return
+        K, B = int(idx_steps.shape[0]), int(idx_steps.shape[1])
+        ws = self.workspace(B)
+        cfg = self._cfg_for(B)
+        L.lib().call("cacto_update_n", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(storage, torch.float64),
+                     dptr(idx_steps.contiguous(), torch.int32), K, B, dptr(ws), ws.numel() * 4, stream())
+
     def capture_updates(self, storage, idx_steps, per_buffer=None, uniforms=None):
         """One HIP graph of len(idx_steps) consecutive RL.py:101-118 updates (critic chain ->
         weight-gradient GEMM -> Adam + soft update -> actor chain -> GEMM -> Adam per step), captured
@@ -257,9 +273,14 @@ class RL_AC:
                 update_step_counter = self._after_step(update_step_counter)
             return update_step_counter
         idx_all = buffer.sample_indices(n, rng)                  # [n, B] int32 on device
-        for i in range(n):
-            self.update_rows(buffer.storage, idx_all[i])
-            update_step_counter = self._after_step(update_step_counter)
+        # the updates between two checkpoint saves (RL.py:139-141) run as one pipelined call
+        i = 0
+        while i < n:
+            k = min(n - i, self.conf.save_interval - update_step_counter % self.conf.save_interval)
+            self.update_rows_n(buffer.storage, idx_all[i:i + k])
+            for _ in range(k):
+                update_step_counter = self._after_step(update_step_counter)
+            i += k
         return update_step_counter
 
     def _after_step(self, counter):

@@ -215,6 +215,15 @@ int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_updat
                  float* y_d, float* V_d, float* Vt_d, void* workspace_d, size_t workspace_bytes,
                  void* stream);
 
+/* K consecutive updates on minibatch indices idx_d [K][B] (learn_and_update's loop with its
+ * minibatches drawn up front, RL.py:120-143; no IS weights). Bit-identical to K cacto_update calls;
+ * internally the critic step of update t+1 overlaps the actor step of update t on a second stream
+ * owned by the system handle (the critic step never reads the actor), joined back into `stream`
+ * before the call returns. */
+int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                   const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
+                   size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- rollouts --------------- */
 
 /* B episodes from S0_d [B,ns] (float64), each for nsteps_d[b] <= T steps:

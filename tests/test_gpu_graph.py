@@ -1,5 +1,6 @@
-"""The update loop replayed as one HIP graph (RL_AC.capture_updates) does exactly what the eager
-loop does: bit-identical weights, Adam moments and optimiser counters after K updates."""
+"""The update loop replayed as one HIP graph (RL_AC.capture_updates), and the pipelined K-update
+call (RL_AC.update_rows_n / cacto_update_n), do exactly what the eager loop does: bit-identical
+weights, Adam moments and optimiser counters after K updates."""
 import os
 
 import numpy as np
@@ -91,3 +92,33 @@ def test_graph_replay_equals_eager_updates_with_per():
         assert torch.equal(a, b)
     for name in ("sum_tree", "min_tree", "exp_counter"):
         assert torch.equal(getattr(ebuf, name), getattr(gbuf, name)), name
+
+
+@pytest.mark.parametrize("system,B", [("double_integrator", 128), ("double_integrator", 1000), ("manipulator", 64)])
+def test_pipelined_updates_equal_sequential(system, B):
+    """cacto_update_n overlaps critic(t+1) with actor(t) on two streams; the result is the same bits."""
+    conf = load_conf(system)
+    env = make_env(conf)
+    ns = conf.nb_state
+    rng = np.random.default_rng(11)
+    N, K = 4096, 7
+    S = np.column_stack([rng.uniform(-3, 3, (N, ns - 1)), rng.uniform(0, 4.9, N)])
+    rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.01, rng.normal(size=(N, ns)) * 0.3,
+                           (rng.uniform(size=(N, 1)) < 0.1).astype(float), (rng.uniform(size=(N, 1)) < 0.1)
+                           .astype(float)], axis=1)
+    storage = torch.as_tensor(rows, device="cuda")
+    idx = torch.as_tensor(rng.integers(0, N, size=(K, B)).astype(np.int32), device="cuda")
+
+    def learner():
+        rl = RL_AC(env, NN(env, conf, w_S=1e-2 if system == "double_integrator" else 0.0, seed=3), conf)
+        rl.setup_model()
+        return rl
+    seq = learner()
+    for k in range(K):
+        seq.update_rows(storage, idx[k])
+    pipe = learner()
+    pipe.update_rows_n(storage, idx)
+    torch.cuda.synchronize()
+    for a, b in zip(_state(seq), _state(pipe)):
+        assert torch.equal(a, b)
+    assert int(pipe.steps[0]) == K and int(pipe.steps[1]) == K
