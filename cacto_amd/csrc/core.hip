@@ -106,7 +106,8 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   if (sys->ddp_ws) (void)hipFree(sys->ddp_ws);
   if (sys->side) (void)hipStreamSynchronize(sys->side);
   if (sys->ev_critic) (void)hipEventDestroy(sys->ev_critic);
-  if (sys->ev_actor) (void)hipEventDestroy(sys->ev_actor);
+  for (hipEvent_t e : sys->ev_actor)
+    if (e) (void)hipEventDestroy(e);
   if (sys->side) (void)hipStreamDestroy(sys->side);
   delete sys;
   return CACTO_OK;

@@ -11,7 +11,7 @@ struct cacto_sys {
   void* ddp_ws = nullptr;  // cacto_ddp_backward's per-step derivative records (grow-only)
   size_t ddp_ws_bytes = 0;
   hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its two events
-  hipEvent_t ev_critic = nullptr, ev_actor = nullptr;
+  hipEvent_t ev_critic = nullptr, ev_actor[2] = {nullptr, nullptr};
 };
 
 namespace cacto {

@@ -572,8 +572,8 @@ __device__ __forceinline__ void write_packed(float4* pk4, const NetTopo& t, int 
      (o & 3)] = val;
 }
 
-__global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, int nch, NetTopo t, float* netbuf,
-                                              float4* packed, float* __restrict__ m, float* __restrict__ v,
+__global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, int nch, NetTopo t, const float* src,
+                                              float* netbuf, float4* packed, float* __restrict__ m, float* __restrict__ v,
                                               const int32_t* __restrict__ step, AdamArgs a, float* target,
                                               float4* target_packed) {
   const int it = step[a.which];  // = Keras iterations + 1
@@ -604,7 +604,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
     float mm = m[p], vv = v[p];
     mm = fadd(mm, fmul(fsub(g, mm), c1));
     vv = fadd(vv, fmul(fsub(fmul(g, g), vv), c2));
-    const float th = fsub(netbuf[p], fdiv(fmul(mm, alpha), fadd(__fsqrt_rn(vv), eps)));
+    const float th = fsub(src[p], fdiv(fmul(mm, alpha), fadd(__fsqrt_rn(vv), eps)));
     m[p] = mm;
     v[p] = vv;
     netbuf[p] = th;
@@ -669,6 +669,7 @@ struct Workspace {
   GradBufs crit, act;
   float* slab;    // critic weight-gradient slabs
   float* slab_a;  // actor's (a separate region: cacto_update_n overlaps the two steps)
+  float* cshadow; // second critic net buffer (cacto_update_n alternates the critic between the two)
   float* scal;  // y, V, Vt scratch (3 * Bp)
   size_t bytes;
   int Bp;
@@ -710,6 +711,8 @@ Workspace plan(const cacto_sys* sys, int B, char* base) {
   off += align64((size_t)nch_c * tc.params);
   w.slab_a = f ? f + off : nullptr;
   off += align64((size_t)nch_a * ta.params);
+  w.cshadow = f ? f + off : nullptr;
+  off += align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
   w.scal = f ? f + off : nullptr;
   off += align64((size_t)3 * Bp);
   w.bytes = off * sizeof(float);
@@ -806,8 +809,10 @@ int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, c
   return CACTO_OK;
 }
 
+// src: the weights the step starts from (nullptr = in place; cacto_update_n steps the critic from one
+// buffer into the other)
 int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, int which,
-                const float* slab, int nch, int soft, hipStream_t st) {
+                const float* slab, int nch, int soft, hipStream_t st, const float* src = nullptr) {
   const NetTopo& t = topo(sys, which);
   float* nb = which == CACTO_NET_CRITIC ? nets->critic_d : nets->actor_d;
   float* m = which == CACTO_NET_CRITIC ? nets->critic_m_d : nets->actor_m_d;
@@ -815,7 +820,7 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
   float4* pk = reinterpret_cast<float4*>(nb + flat_span(t));
   float4* tpk = reinterpret_cast<float4*>(nets->target_d + flat_span(t));
   const int grid = std::min((t.params + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, slab, nch, t, nb, pk, m, v, nets->step_d,
+  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, slab, nch, t, src ? src : nb, nb, pk, m, v, nets->step_d,
                      adam_args(cfg, which, soft && which == CACTO_NET_CRITIC), nets->target_d, tpk);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
@@ -904,11 +909,14 @@ extern "C" int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const 
 
 // K consecutive updates (learn_and_update's loop with its minibatches drawn up front, RL.py:120-143)
 // as a two-stream pipeline. The critic step of update t+1 reads only the critic, the target and the
-// rows — not the actor — so it runs while the actor step of update t is still going:
-//   stream  : critic chain(t), wgrad(t), [wait: actor chain(t-1) has read the critic], Adam(t) + soft
-//   side    : [wait: Adam(t)], actor chain(t), wgrad(t), Adam(t)
-// Every kernel sees the same inputs as in K sequential cacto_update calls, so the results are
-// bit-identical; the side stream joins the caller's stream before returning.
+// rows — never the actor — so it runs while the actor step of update t is still going:
+//   stream : critic chain(t) on C_t, wgrad, Adam(t): C_t -> C_{t+1} (+ soft target update)
+//   side   : [wait Adam(t)], actor chain(t) against C_{t+1}, wgrad, Adam(actor)
+// The critic alternates between the caller's net buffer and a workspace copy (C_t in buffer t % 2),
+// so Adam(t) overwrites the buffer actor chain(t-2) read — the only ordering the stream needs from
+// the side stream (an event two updates old). Every kernel sees the same inputs as in K sequential
+// cacto_update calls, so the results are bit-identical; the final critic is copied back if it ended
+// in the workspace buffer, and the side stream joins the caller's stream before returning.
 extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                               const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
                               size_t workspace_bytes, void* stream) {
@@ -922,29 +930,39 @@ extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, cons
   if (!ms->side) {
     CACTO_CHECK_HIP(hipStreamCreateWithFlags(&ms->side, hipStreamNonBlocking));
     CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_critic, hipEventDisableTiming));
-    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_actor, hipEventDisableTiming));
+    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_actor[0], hipEventDisableTiming));
+    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_actor[1], hipEventDisableTiming));
   }
   hipStream_t side = ms->side;
+  const NetTopo& tc = sys->critic;
+  const size_t nb_bytes = ((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256) * sizeof(float);
+  float* const buf[2] = {nets->critic_d, w.cshadow};
+  CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));  // everything the caller queued before
   CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
   for (int t = 0; t < K; ++t) {
     const int32_t* idx = idx_d + (size_t)t * B;
+    cacto_nets cur = *nets, nxt = *nets;
+    cur.critic_d = buf[t & 1];
+    nxt.critic_d = buf[(t + 1) & 1];
     int nch = 0;
-    if (int e = launch_critic_chain_and_wgrad(sys, nets, cfg, storage_d, idx, nullptr, B, nullptr, nullptr, nullptr, w,
-                                              st, &nch))
+    if (int e = launch_critic_chain_and_wgrad(sys, &cur, cfg, storage_d, idx, nullptr, B, nullptr, nullptr, nullptr,
+                                              w, st, &nch))
       return e;
-    if (t > 0) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor, 0));  // actor chain(t-1) is done reading
-    if (int e = launch_adam(sys, nets, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st)) return e;
+    if (t >= 2) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t & 1], 0));  // actor chain(t-2) read nxt
+    if (int e = launch_adam(sys, &nxt, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st, cur.critic_d))
+      return e;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
     CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
-    if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx, B, w, side)) return e;
-    CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor, side));
+    if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
+    CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t & 1], side));
     WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
     hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, side, a, w.slab_a);
     CACTO_CHECK_HIP(hipGetLastError());
     if (int e = launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, a.nch, 0, side)) return e;
   }
-  CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor, side));
-  CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor, 0));
+  CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, side));
+  CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
+  if (K & 1) CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow, nb_bytes, hipMemcpyDeviceToDevice, st));
   return CACTO_OK;
 }
