@@ -371,14 +371,20 @@ def per_update_phase(rl, buf, B, K, W, world, seed):
         idx, w = buf.sample_device(U[i])
         rl.update_rows(buf.storage, idx, w, y, V)
         buf.update_priorities_device(idx, y, V)
-    for i in range(W):
-        step(i)
+    pipelined = world == 1 and not USE_GRAPH
+    if pipelined:
+        rl.update_rows_n_per(buf, U[:W])        # warm-up on the timed path
+    else:
+        for i in range(W):
+            step(i)
     graph = rl.capture_updates(None, None, per_buffer=buf, uniforms=U[W:]) if world == 1 and USE_GRAPH else None
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if graph is not None:
         graph.replay()
+    elif pipelined:
+        rl.update_rows_n_per(buf, U[W:])        # K updates: sample -> update -> priorities, pipelined
     else:
         for i in range(K):
             step(W + i)

@@ -670,6 +670,8 @@ struct Workspace {
   float* slab;    // critic weight-gradient slabs
   float* slab_a;  // actor's (a separate region: cacto_update_n overlaps the two steps)
   float* cshadow; // second critic net buffer (cacto_update_n alternates the critic between the two)
+  int32_t* pidx;  // cacto_update_n_per: sampled indices, two buffers of Bp
+  float* pisw;    // and the IS weights of the current update
   float* scal;  // y, V, Vt scratch (3 * Bp)
   size_t bytes;
   int Bp;
@@ -713,6 +715,10 @@ Workspace plan(const cacto_sys* sys, int B, char* base) {
   off += align64((size_t)nch_a * ta.params);
   w.cshadow = f ? f + off : nullptr;
   off += align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
+  w.pidx = f ? reinterpret_cast<int32_t*>(f + off) : nullptr;
+  off += align64((size_t)2 * Bp);
+  w.pisw = f ? f + off : nullptr;
+  off += align64((size_t)Bp);
   w.scal = f ? f + off : nullptr;
   off += align64((size_t)3 * Bp);
   w.bytes = off * sizeof(float);
@@ -917,15 +923,18 @@ extern "C" int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const 
 // the side stream (an event two updates old). Every kernel sees the same inputs as in K sequential
 // cacto_update calls, so the results are bit-identical; the final critic is copied back if it ended
 // in the workspace buffer, and the side stream joins the caller's stream before returning.
-extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
-                              const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
-                              size_t workspace_bytes, void* stream) {
-  CACTO_REQUIRE(sys && cfg && storage_d && idx_d && B > 0 && K >= 0, "cacto_update_n: bad arguments");
-  if (int e = check_nets(nets)) return e;
-  CHECK_WS(workspace_d, workspace_bytes, B);
-  if (K == 0) return CACTO_OK;
-  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
-  hipStream_t st = as_stream(stream);
+namespace {
+// PER state of cacto_update_n_per (replay_buffer.py:139-218)
+struct PerArgs {
+  double *sum_tree, *min_tree;
+  int64_t cap, max_idx;
+  double beta, fresh, eps, alpha;
+  const double* uniforms;  // [K][B]
+  double *exp_counter, *max_priority;
+};
+
+int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const double* storage_d,
+                    const int32_t* idx_d, const PerArgs* per, int K, int B, const Workspace& w, hipStream_t st) {
   cacto_sys* ms = const_cast<cacto_sys*>(sys);
   if (!ms->side) {
     CACTO_CHECK_HIP(hipStreamCreateWithFlags(&ms->side, hipStreamNonBlocking));
@@ -940,19 +949,35 @@ extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, cons
   CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));  // everything the caller queued before
   CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+  float* const y = w.scal;
+  float* const V = w.scal + w.Bp;
   for (int t = 0; t < K; ++t) {
+    // actor chain(t-2) read the critic buffer Adam(t) writes and (PER) the index buffer of update t
+    if (t >= 2) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t & 1], 0));
     const int32_t* idx = idx_d + (size_t)t * B;
+    const float* isw = nullptr;
+    if (per) {
+      int32_t* pi = w.pidx + (size_t)(t & 1) * w.Bp;
+      if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                   per->uniforms + (size_t)t * B, B, pi, w.pisw, per->exp_counter, st))
+        return e;
+      idx = pi;
+      isw = w.pisw;
+    }
     cacto_nets cur = *nets, nxt = *nets;
     cur.critic_d = buf[t & 1];
     nxt.critic_d = buf[(t + 1) & 1];
     int nch = 0;
-    if (int e = launch_critic_chain_and_wgrad(sys, &cur, cfg, storage_d, idx, nullptr, B, nullptr, nullptr, nullptr,
-                                              w, st, &nch))
+    if (int e = launch_critic_chain_and_wgrad(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st, &nch))
       return e;
-    if (t >= 2) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t & 1], 0));  // actor chain(t-2) read nxt
     if (int e = launch_adam(sys, &nxt, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st, cur.critic_d))
       return e;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+    if (per) {
+      if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
+                                   per->eps, per->alpha, per->max_priority, B, st))
+        return e;
+    }
     CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t & 1], side));
@@ -965,4 +990,36 @@ extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, cons
   CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
   if (K & 1) CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow, nb_bytes, hipMemcpyDeviceToDevice, st));
   return CACTO_OK;
+}
+}  // namespace
+
+extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                              const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
+                              size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && idx_d && B > 0 && K >= 0, "cacto_update_n: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  if (K == 0) return CACTO_OK;
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  return update_pipeline(sys, nets, cfg, storage_d, idx_d, nullptr, K, B, w, as_stream(stream));
+}
+
+// learn_and_update with PER (RL.py:122-137) for K updates: sample (stratified, IS weights) ->
+// update -> priority update per step, the sampling and priority update on the critic's stream
+// (the next sample depends on them), pipelined with the actor steps as in cacto_update_n.
+extern "C" int cacto_update_n_per(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                  const double* storage_d, double* sum_tree_d, double* min_tree_d, int64_t capacity,
+                                  int64_t max_idx, double beta, const double* uniforms_d, double* exp_counter_d,
+                                  double fresh_factor, double eps, double alpha, double* max_priority_d, int K, int B,
+                                  void* workspace_d, size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && sum_tree_d && min_tree_d && uniforms_d && exp_counter_d &&
+                    max_priority_d && B > 0 && K >= 0,
+                "cacto_update_n_per: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  if (K == 0) return CACTO_OK;
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  const PerArgs per{sum_tree_d, min_tree_d, capacity, max_idx, beta, fresh_factor, eps, alpha, uniforms_d,
+                    exp_counter_d, max_priority_d};
+  return update_pipeline(sys, nets, cfg, storage_d, nullptr, &per, K, B, w, as_stream(stream));
 }

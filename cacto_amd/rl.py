@@ -199,6 +199,22 @@ class RL_AC:
         L.lib().call("cacto_update_n", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(storage, torch.float64),
                      dptr(idx_steps.contiguous(), torch.int32), K, B, dptr(ws), ws.numel() * 4, stream())
 
+    def update_rows_n_per(self, buffer, uniforms):
+        """learn_and_update's PER loop (RL.py:122-137) for K = len(uniforms) updates in one call
+        (`cacto_update_n_per`): per update the stratified sample from uniforms[k] ([K, B] f64 on the
+        device, the reference's random.random() draws in order), the update with IS weights and the
+        priority update, pipelined with the actor steps; bit-identical to the sequential loop.
+        Single rank (the data-parallel PER exchange runs per sample call)."""
+        K, B = int(uniforms.shape[0]), int(uniforms.shape[1])
+        ws = self.workspace(B)
+        cfg = self._cfg_for(B)
+        u = uniforms.to(device=DEVICE, dtype=torch.float64).contiguous()
+        b = buffer
+        L.lib().call("cacto_update_n_per", self.sys.handle, C.byref(self.nets), C.byref(cfg),
+                     dptr(b.storage, torch.float64), dptr(b.sum_tree), dptr(b.min_tree), b.cap, b.max_idx(), b.beta,
+                     dptr(u), dptr(b.exp_counter), b.fresh, b.eps, b.alpha, dptr(b.max_priority), K, B, dptr(ws),
+                     ws.numel() * 4, stream())
+
     def capture_updates(self, storage, idx_steps, per_buffer=None, uniforms=None):
         """One HIP graph of len(idx_steps) consecutive RL.py:101-118 updates (critic chain ->
         weight-gradient GEMM -> Adam + soft update -> actor chain -> GEMM -> Adam per step), captured
@@ -264,6 +280,18 @@ class RL_AC:
         if per:
             if self.dp_world > 1 and buffer.dp_world != self.dp_world:
                 buffer.set_data_parallel(self.dp_world, self.dp_group)
+            if self.dp_world == 1:
+                # the updates between two checkpoint saves as one pipelined call; the uniforms are
+                # the per-step random.random() draws of the sequential loop, in the same order
+                i = 0
+                while i < n:
+                    k = min(n - i, self.conf.save_interval - update_step_counter % self.conf.save_interval)
+                    U = np.array([[buffer.random.random() for _ in range(B)] for _ in range(k)], dtype=np.float64)
+                    self.update_rows_n_per(buffer, torch.as_tensor(U, device=DEVICE))
+                    for _ in range(k):
+                        update_step_counter = self._after_step(update_step_counter)
+                    i += k
+                return update_step_counter
             for _ in range(n):
                 idx, w = buffer.sample_device()
                 y = torch.empty(B, dtype=torch.float32, device=DEVICE)

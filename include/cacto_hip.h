@@ -224,6 +224,15 @@ int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_upd
                    const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
                    size_t workspace_bytes, void* stream);
 
+/* The same pipeline for learn_and_update with PER (RL.py:122-137): per update, the stratified
+ * sample (uniforms_d [K][B], as cacto_per_sample) -> update with IS weights -> priority update
+ * (as cacto_per_update); bit-identical to the K-step sequential loop. */
+int cacto_update_n_per(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                       const double* storage_d, double* sum_tree_d, double* min_tree_d, int64_t capacity,
+                       int64_t max_idx, double beta, const double* uniforms_d, double* exp_counter_d,
+                       double fresh_factor, double eps, double alpha, double* max_priority_d, int K, int B,
+                       void* workspace_d, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- rollouts --------------- */
 
 /* B episodes from S0_d [B,ns] (float64), each for nsteps_d[b] <= T steps:

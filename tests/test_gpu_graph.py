@@ -122,3 +122,40 @@ def test_pipelined_updates_equal_sequential(system, B):
     for a, b in zip(_state(seq), _state(pipe)):
         assert torch.equal(a, b)
     assert int(pipe.steps[0]) == K and int(pipe.steps[1]) == K
+
+
+def test_pipelined_per_updates_equal_sequential():
+    """cacto_update_n_per: sample -> update -> priority update per step, pipelined, equals the
+    sequential PER loop bit for bit (weights, moments, counters, trees, experience counters)."""
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    conf = load_conf("car_park")
+    conf.prioritized_replay_alpha = 0.6
+    env = make_env(conf)
+    ns = conf.nb_state
+    rng = np.random.default_rng(13)
+    N, B, K = 5000, 64, 7
+    S = np.column_stack([rng.uniform(-3, 3, (N, ns - 1)), rng.uniform(0, 4.9, N)])
+    rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.01, rng.normal(size=(N, ns)) * 0.3,
+                           np.zeros((N, 1)), np.zeros((N, 1))], axis=1)
+    U = torch.as_tensor(rng.uniform(size=(K, B)), device="cuda")
+
+    def setup():
+        rl = RL_AC(env, NN(env, conf, w_S=0.0, seed=5), conf)
+        rl.setup_model()
+        buf = PrioritizedReplayBuffer(conf, env.sys)
+        buf.add_rows(rows)
+        return rl, buf
+    seq, sbuf = setup()
+    y = torch.empty(B, dtype=torch.float32, device="cuda")
+    V = torch.empty_like(y)
+    for k in range(K):
+        idx, w = sbuf.sample_device(U[k])
+        seq.update_rows(sbuf.storage, idx, w, y, V)
+        sbuf.update_priorities_device(idx, y, V)
+    pipe, pbuf = setup()
+    pipe.update_rows_n_per(pbuf, U)
+    torch.cuda.synchronize()
+    for a, b in zip(_state(seq), _state(pipe)):
+        assert torch.equal(a, b)
+    for name in ("sum_tree", "min_tree", "exp_counter", "max_priority"):
+        assert torch.equal(getattr(sbuf, name), getattr(pbuf, name)), name
