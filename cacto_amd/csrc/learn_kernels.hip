@@ -441,7 +441,9 @@ struct WgArgs {
 constexpr int WG_BLK = 4;
 
 __global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab) {
-  __shared__ float4 part[4 * WG_BLK * WG_BLK * 64];  // 64 KiB
+  // 32 KiB: the 16 tiles are reduced in two rounds of 8, so a GEMM workgroup fits on a CU beside
+  // a chain workgroup (~110 KiB) — the pipelined update runs the two concurrently
+  __shared__ float4 part[4 * (WG_BLK * WG_BLK / 2) * 64];
   const int chunk = blockIdx.x / a.tpc;
   int rem = blockIdx.x - chunk * a.tpc;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -501,31 +503,36 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ sla
 #pragma unroll
         for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].w, Bv[o].w, acc[i][o]);
     }
+    constexpr int HT = WG_BLK * WG_BLK / 2;  // tiles per round
 #pragma unroll
-    for (int i = 0; i < WG_BLK; ++i)
+    for (int h = 0; h < 2; ++h) {
+      if (h) __syncthreads();  // round 0's partials are consumed
 #pragma unroll
-      for (int o = 0; o < WG_BLK; ++o) part[((wave * WG_BLK + i) * WG_BLK + o) * 64 + lane] = f4(acc[i][o]);
-    __syncthreads();
-    // wave w finishes tiles t = 4w .. 4w + 3 of the 16: ((p0 + p1) + p2) + p3
+      for (int i = 2 * h; i < 2 * h + 2; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int t = wave * 4 + k, i = t / WG_BLK, o = t % WG_BLK;
-      if (i >= ni || o >= no) continue;
-      float4 s4 = part[((0 * WG_BLK + i) * WG_BLK + o) * 64 + lane];
+        for (int o = 0; o < WG_BLK; ++o) part[(wave * HT + (i - 2 * h) * WG_BLK + o) * 64 + lane] = f4(acc[i][o]);
+      __syncthreads();
+      // wave w finishes tiles t = 8h + 2w, 8h + 2w + 1: ((p0 + p1) + p2) + p3, as in one round
 #pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        const float4 q = part[((w * WG_BLK + i) * WG_BLK + o) * 64 + lane];
-        s4.x += q.x;
-        s4.y += q.y;
-        s4.z += q.z;
-        s4.w += q.w;
-      }
-      const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
-      const int oc = 16 * (ot0 + o) + c;
+      for (int k = 0; k < 2; ++k) {
+        const int tl = wave * 2 + k, t = h * HT + tl, i = t / WG_BLK, o = t % WG_BLK;
+        if (i >= ni || o >= no) continue;
+        float4 s4 = part[(0 * HT + tl) * 64 + lane];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ii = 16 * (it0 + i) + 4 * g + q;
-        if (ii < Ly.in && oc < Ly.out) out[Ly.woff + ii * Ly.out + oc] = sv[q];
+        for (int w = 1; w < 4; ++w) {
+          const float4 q = part[(w * HT + tl) * 64 + lane];
+          s4.x += q.x;
+          s4.y += q.y;
+          s4.z += q.z;
+          s4.w += q.w;
+        }
+        const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+        const int oc = 16 * (ot0 + o) + c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ii = 16 * (it0 + i) + 4 * g + q;
+          if (ii < Ly.in && oc < Ly.out) out[Ly.woff + ii * Ly.out + oc] = sv[q];
+        }
       }
     }
   } else {
