@@ -25,7 +25,8 @@ def _rollout(system, R):
     return conf, oe, rl, S0, n
 
 
-@pytest.mark.parametrize("system,R", [("double_integrator", 4096), ("manipulator", 8192)])
+@pytest.mark.parametrize("system,R", [("double_integrator", 4096), ("manipulator", 8192), ("car_park", 4096),
+                                      ("ur5", 2048)])
 def test_fullsize_rollout_properties(system, R):
     conf, oe, rl, S0, n = _rollout(system, R)
     T = int(n.max())
