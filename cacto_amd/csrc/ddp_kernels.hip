@@ -281,6 +281,18 @@ __device__ inline void ddp_jacobians(const SysDevice& sd, const double* x, const
   }
 }
 
+// Structural nonzeros of A, B for the systems of the fused pass (SI, car, prismatic chain). The
+// products below skip the terms that are exactly zero: a sum that leaves out 0 * finite terms is the
+// same number (the fully unrolled loops fold these tests away), at a third of the f64 instructions.
+template <int NJ>
+__device__ __forceinline__ constexpr bool a_nz(int k, int c) {
+  return k == c || (NJ == -1 && ((k <= 1 && c >= 2) || (k == 3 && c == 4))) || (NJ > 0 && k < NJ && c == k + NJ);
+}
+template <int NJ>
+__device__ __forceinline__ constexpr bool b_nz(int k, int j) {
+  return NJ == 0 ? k == j : NJ == -1 ? ((k == 2 && j == 0) || (k == 4 && j == 1)) : k >= NJ;
+}
+
 // In-place inverse of a small matrix (Gauss-Jordan, partial pivoting).
 template <int M>
 __device__ inline void small_inverse(double* a, double* inv) {
@@ -486,7 +498,8 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
     for (int r = 0; r < N; ++r) {
       double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < N; ++k) s += A[k * N + r] * Vx[k];
+      for (int k = 0; k < N; ++k)
+        if (a_nz<NJ>(k, r)) s += A[k * N + r] * Vx[k];
       Qx[r] = lx[r] + s;
     }
 #pragma unroll
@@ -496,7 +509,8 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
       const double lu = p.scale * (-w_run[6] * (2.0 * u[j] + p.w_b * 10.0 * pow(u[j] / um, 9.0) / um));
       double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < N; ++k) s += B[k * M + j] * Vx[k];
+      for (int k = 0; k < N; ++k)
+        if (b_nz<NJ>(k, j)) s += B[k * M + j] * Vx[k];
       Qu[j] = lu + s;
     }
     // V_xx A, V_xx B
@@ -506,14 +520,16 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
       for (int c = 0; c < N; ++c) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < N; ++k) s += Vxx[r * N + k] * A[k * N + c];
+        for (int k = 0; k < N; ++k)
+          if (a_nz<NJ>(k, c)) s += Vxx[r * N + k] * A[k * N + c];
         VA[r * N + c] = s;
       }
 #pragma unroll
       for (int c = 0; c < M; ++c) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < N; ++k) s += Vxx[r * N + k] * B[k * M + c];
+        for (int k = 0; k < N; ++k)
+          if (b_nz<NJ>(k, c)) s += Vxx[r * N + k] * B[k * M + c];
         VB[r * M + c] = s;
       }
     }
@@ -523,14 +539,16 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
       for (int c = 0; c < N; ++c) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < N; ++k) s += A[k * N + r] * VA[k * N + c];
+        for (int k = 0; k < N; ++k)
+          if (a_nz<NJ>(k, r)) s += A[k * N + r] * VA[k * N + c];
         Qxx[r * N + c] = lxx[r * N + c] + s;
       }
 #pragma unroll
       for (int c = 0; c < M; ++c) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < N; ++k) s += A[k * N + r] * VB[k * M + c];
+        for (int k = 0; k < N; ++k)
+          if (a_nz<NJ>(k, r)) s += A[k * N + r] * VB[k * M + c];
         Qxu[r * M + c] = s;  // + l_xu = 0
       }
     }
@@ -540,7 +558,8 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
       for (int c = 0; c < M; ++c) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < N; ++k) s += B[k * M + r] * VB[k * M + c];
+        for (int k = 0; k < N; ++k)
+          if (b_nz<NJ>(k, r)) s += B[k * M + r] * VB[k * M + c];
         const double um = p.u_max[r];
         const double luu = r == c ? p.scale * (-w_run[6] * (2.0 + p.w_b * 90.0 * pow(u[r] / um, 8.0) / (um * um))) : 0.0;
         Quu[r * M + c] = luu + s + (r == c ? mu : 0.0);
