@@ -21,6 +21,8 @@
  *   cacto_adam_step        optimizer.apply_gradients RL.py:105, :109 (Keras-2.11 Adam, RL.py:79-88)
  *   cacto_soft_update      RL_AC.update_target RL.py:113-118
  *   cacto_update           RL_AC.update + update_target (one learn_and_update iteration, RL.py:122-137)
+ *   cacto_update_n[_per]   the learn_and_update loop RL.py:120-143 for K updates (with PER:
+ *                          sample -> update -> priority update), pipelined on two streams
  *   cacto_buffer_gather    ReplayBuffer.sample row gather replay_buffer.py:47-61
  *   cacto_buffer_add       ReplayBuffer.add ring write replay_buffer.py:25-36
  *   cacto_rl_solve_add     RL_AC.RL_Solve n-step targets RL.py:145-189 fused with the
@@ -33,6 +35,9 @@
  *     row-major. Host pointers are named *_h. The library never frees caller memory.
  *   - Every call is asynchronous on `stream` (a hipStream_t passed as void*; NULL = default stream)
  *     and enqueues no host synchronisation, so sequences can be captured into a hipGraph.
+ *     cacto_update_n[_per] also use a side stream owned by the handle, joined back into `stream`
+ *     before they return; cacto_ddp_backward (car_park, revolute chains) grows a device workspace
+ *     owned by the handle (a hipMalloc, so warm it up before capturing).
  *   - Return 0 on success, <0 on error; cacto_last_error() returns a thread-local message.
  *     No C++ exception crosses the ABI.
  *   - Handles (cacto_sys) are created/destroyed by the caller; concurrent calls on one handle are
