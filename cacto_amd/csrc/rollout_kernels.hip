@@ -416,6 +416,41 @@ struct RoNorm {
   }
 };
 
+// The next actor input of one (slot, feature) item per wave-0 lane and round: item e = lane + 64 r
+// -> slot e % SL, feature e / SL. The lane's norm is fixed for the launch, so the per-step work is
+// one division per item spread over the lanes instead of ns divisions on each slot's lane (the
+// same fdiv, so the same bits as RoNorm).
+template <int NS, int SL>
+struct RoX0Lane {
+  static constexpr int R = (SL * NS + 63) / 64;  // rounds
+  float n[R];
+  bool tcol[R], valid[R];
+  __device__ __forceinline__ RoX0Lane(const RoNorm<NS>& nrm, int lane) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = lane + 64 * r, f = e / SL;
+      valid[r] = e < SL * NS;
+      tcol[r] = f == NS - 1;
+      float v = 1.f;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) v = f == q ? nrm.n[q] : v;  // select chain, no dynamic indexing
+      n[r] = v;
+    }
+  }
+  template <typename Sh>
+  __device__ __forceinline__ void write(Sh& S, const RoNorm<NS>& nrm, int lane) const {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = lane + 64 * r, c = e % SL, f = e / SL;
+      if (valid[r]) {
+        const float q = fdiv((float)S.sS[c * NS + f], n[r]);
+        const float v = tcol[r] ? fsub(fmul(q, 2.0f), 1.0f) : q;
+        S.W.x0[(c >> 2) * 64 + 4 * f + (c & 3)] = nrm.on ? v : (float)S.sS[c * NS + f];
+      }
+    }
+  }
+};
+
 // Slot refill (wave 0; every lane calls it, lanes with `need` take the next queue entries in lane
 // order). A new episode's s_0 goes to the slot's state and the actor input; episodes of length 0
 // are completed on the spot (status 0: RL.py never rolls out NSTEPS_SH == 0).
@@ -490,7 +525,6 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
   for (int i = 0; i < ns; ++i) {
     Sh.sS[c * ns + i] = sn[i];
     bad |= isnan(sn[i]);
-    Sh.W.x0[(c >> 2) * 64 + 4 * i + (c & 3)] = nrm(i, (float)sn[i]);
   }
   if (Atraj)
 #pragma unroll
@@ -554,6 +588,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   }
   __syncthreads();
   const int c = L.lane % SL;  // slot of this lane
+  const RoX0Lane<ns, SL> x0l(nrm, L.lane);
   for (int it = 0; Sh.anyact; ++it) {
     RSTAMP(0);
     // joint placements of s_t (published by the actor's first barrier)
@@ -614,6 +649,10 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         RSTAMP(7);
       }
       ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L);
+      // next actor input from s_{t+1} (or a refilled s_0): the slots' lanes wrote sS above; LDS
+      // operations of one wave complete in order, so after this wave-scope fence every lane reads them
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      x0l.write(Sh, nrm, L.lane);
       const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
       if (L.lane == 0) Sh.anyact = m != 0;
       RSTAMP(8);
