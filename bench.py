@@ -167,10 +167,10 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     T = int(nsteps.max())
     inputs = rl.rollout_inputs(S0, nsteps)
     f64 = dict(dtype=torch.float64, device="cuda")
-    out = {"S": torch.empty(R, T + 1, conf.nb_state, **f64), "A": torch.empty(R, T, conf.nb_action,
+    out = {"S": torch.zeros(R, T + 1, conf.nb_state, **f64), "A": torch.zeros(R, T, conf.nb_action,
                                                                               dtype=torch.float32, device="cuda"),
-           "R": torch.empty(R, T, **f64), "EE": torch.empty(R, T + 1, 3, **f64),
-           "status": torch.empty(R, dtype=torch.int32, device="cuda")}
+           "R": torch.zeros(R, T, **f64), "EE": torch.zeros(R, T + 1, 3, **f64),
+           "status": torch.zeros(R, dtype=torch.int32, device="cuda")}
     seq = {k: out[k] for k in ("S", "A", "status")}
     n_d = inputs[1]
 

@@ -59,6 +59,8 @@ _SIGS = {
     "cacto_env_step_batch": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
     "cacto_env_ee": (C.c_int, [vp, vp, vp, C.c_int, vp]),
     "cacto_env_step": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
+    "cacto_env_jacobians": (C.c_int, [vp, vp, vp, C.c_int, vp, vp, vp]),
+    "cacto_env_bound_control_cost": (C.c_int, [vp, vp, vp, C.c_int, vp]),
     "cacto_mlp_param_count": (i64, [vp, C.c_int]),
     "cacto_mlp_netbuf_floats": (i64, [vp, C.c_int]),
     "cacto_mlp_pack": (C.c_int, [vp, C.c_int, vp, vp]),
@@ -87,6 +89,7 @@ _SIGS = {
     "cacto_buffer_gather": (C.c_int, [vp, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp]),
     "cacto_per_init": (C.c_int, [vp, vp, i64, vp]),
     "cacto_per_set_range": (C.c_int, [vp, vp, i64, i64, i64, i64, dbl, vp]),
+    "cacto_per_set_range_max": (C.c_int, [vp, vp, i64, i64, i64, i64, vp, dbl, vp]),
     "cacto_per_sample": (C.c_int, [vp, vp, i64, i64, dbl, vp, C.c_int, vp, vp, vp, vp]),
     "cacto_per_shard_stats": (C.c_int, [vp, vp, i64, vp, vp]),
     "cacto_per_sample_global": (C.c_int, [vp, vp, i64, i64, dbl, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp]),

@@ -446,6 +446,39 @@ __global__ void __launch_bounds__(64) k_ddp_derivs(const SysDevice* __restrict__
   for (int k = 0; k < N * M; ++k) rec[(size_t)(RC::B + k) * n_ep] = B[k];
 }
 
+// Env.augmented_derivative (environment.py:111-132; SI :221-233, Car :420-435, CarPark :567-582) for
+// B independent (state, action) rows: the discrete-time Jacobians Fx [nx, nx], Fu [nx, na] that the
+// DDP pass consumes (the same device code), for host-side callers such as TO.backward_pass
+// (TO.py:181). One thread per row.
+template <int NJ>
+__global__ void __launch_bounds__(64) k_env_jacobians(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
+                                                      const double* __restrict__ U, int B, double* __restrict__ Fx,
+                                                      double* __restrict__ Fu) {
+  constexpr int N = DdpDims<NJ>::N, M = DdpDims<NJ>::M, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const SysDevice& sd = *sdp;
+  double x[N], u[M], A[N * N], Bm[N * M];
+#pragma unroll
+  for (int k = 0; k < N; ++k) x[k] = S[(size_t)b * ns + k];
+#pragma unroll
+  for (int k = 0; k < M; ++k) u[k] = U[(size_t)b * na + k];
+  if constexpr (NJ > 2) {
+    ddp_chain_jacobians<NJ>(sd, x, u, A, Bm);
+  } else if constexpr (NJ > 0) {
+    double Mm[M * M], Minv[M * M];
+    chain_mass<NJ>(sd, x, Mm);
+    small_inverse<M>(Mm, Minv);
+    ddp_jacobians<NJ>(sd, x, Minv, A, Bm);
+  } else {
+    ddp_jacobians<NJ>(sd, x, nullptr, A, Bm);
+  }
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) Fx[(size_t)b * N * N + k] = A[k];
+#pragma unroll
+  for (int k = 0; k < N * M; ++k) Fu[(size_t)b * N * M + k] = Bm[k];
+}
+
 // The fused pass for the closed-form systems (SI, car, DI): one thread per episode computes each
 // step's A, B, l_x, l_xx inline and runs the Riccati recursion (sequential in t).
 template <int NJ>
@@ -797,6 +830,24 @@ struct LaunchDdp {
     }
   }
 };
+template <int NJ>
+struct LaunchJac {
+  static int run(const cacto_sys* sys, const double* S, const double* U, int B, double* Fx, double* Fu,
+                 hipStream_t st) {
+    if constexpr (!DdpDims<NJ>::ok) {
+      set_error("cacto_env_jacobians: unsupported dynamics");
+      return CACTO_EUNSUPPORTED;
+    } else {
+      if (NJ == 2 && !sys->host.p.const_dyn) {
+        set_error("cacto_env_jacobians: 2-joint chains are instantiated for the prismatic pair (double integrator)");
+        return CACTO_EUNSUPPORTED;
+      }
+      hipLaunchKernelGGL(k_env_jacobians<NJ>, dim3(ceil_div(B, 64)), dim3(64), 0, st, sys->dev, S, U, B, Fx, Fu);
+      CACTO_CHECK_HIP(hipGetLastError());
+      return CACTO_OK;
+    }
+  }
+};
 }  // namespace
 
 extern "C" int cacto_ddp_backward(const cacto_sys* sys, const double* S_traj_d, int64_t ldS, const double* U_traj_d,
@@ -807,4 +858,11 @@ extern "C" int cacto_ddp_backward(const cacto_sys* sys, const double* S_traj_d, 
   if (n_ep == 0) return CACTO_OK;
   return dispatch_nj<LaunchDdp>(sys->host.p, sys, S_traj_d, ldS, U_traj_d, ldU, nsteps_d, n_ep, mu, dVdx_d,
                                 as_stream(stream));
+}
+
+extern "C" int cacto_env_jacobians(const cacto_sys* sys, const double* S_d, const double* A_d, int B, double* Fx_d,
+                                   double* Fu_d, void* stream) {
+  CACTO_REQUIRE(sys && S_d && A_d && Fx_d && Fu_d && B >= 0, "cacto_env_jacobians: bad arguments");
+  if (B == 0) return CACTO_OK;
+  return dispatch_nj<LaunchJac>(sys->host.p, sys, S_d, A_d, B, Fx_d, Fu_d, as_stream(stream));
 }

@@ -83,6 +83,20 @@ __global__ void __launch_bounds__(256) k_env_step(const SysDevice* __restrict__ 
   }
 }
 
+// Env.bound_control_cost (environment.py:158-163) for B action rows (float64, action order).
+template <int NJ>
+__global__ void __launch_bounds__(256) k_env_bound_cost(const SysDevice* __restrict__ sdp,
+                                                        const double* __restrict__ A, double* __restrict__ out,
+                                                        int B) {
+  constexpr int na = Dims<NJ>::NA;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  double a[na];
+#pragma unroll
+  for (int i = 0; i < na; ++i) a[i] = A[(size_t)b * na + i];
+  out[b] = bound_control_cost<na>(sdp->p, a);
+}
+
 template <int NJ>
 __global__ void __launch_bounds__(256) k_env_ee(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
                                                 double* __restrict__ EE, int B) {
@@ -205,6 +219,14 @@ struct LaunchStep {
   }
 };
 template <int NJ>
+struct LaunchBoundCost {
+  static int run(const cacto_sys* sys, const double* A, double* out, int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_env_bound_cost<NJ>, dim3(ceil_div(B, 256)), dim3(256), 0, st, sys->dev, A, out, B);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
+};
+template <int NJ>
 struct LaunchEE {
   static int run(const cacto_sys* sys, const double* S, double* EE, int B, hipStream_t st) {
     hipLaunchKernelGGL(k_env_ee<NJ>, dim3(ceil_div(B, 256)), dim3(256), 0, st, sys->dev, S, EE, B);
@@ -234,6 +256,13 @@ extern "C" int cacto_env_ee(const cacto_sys* sys, const double* S_d, double* EE_
   CACTO_REQUIRE(sys && S_d && EE_d && B >= 0, "cacto_env_ee: bad arguments");
   if (B == 0) return CACTO_OK;
   return dispatch_nj<LaunchEE>(sys->host.p, sys, S_d, EE_d, B, as_stream(stream));
+}
+
+extern "C" int cacto_env_bound_control_cost(const cacto_sys* sys, const double* A_d, double* out_d, int B,
+                                            void* stream) {
+  CACTO_REQUIRE(sys && A_d && out_d && B >= 0, "cacto_env_bound_control_cost: bad arguments");
+  if (B == 0) return CACTO_OK;
+  return dispatch_nj<LaunchBoundCost>(sys->host.p, sys, A_d, out_d, B, as_stream(stream));
 }
 
 extern "C" int cacto_buffer_add(const cacto_sys* sys, double* storage_d, int64_t capacity, int64_t next_idx,

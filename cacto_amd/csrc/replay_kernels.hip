@@ -22,7 +22,9 @@ __global__ void k_per_init(double* sum_tree, double* min_tree, int64_t n2) {
 // Recomputing an ancestor from final children yields the value the sequential Python updates
 // leave behind (each node's last recomputation follows its subtree's last leaf write).
 __global__ void k_per_fill_leaves(double* sum_tree, double* min_tree, int64_t cap, int64_t ring, int64_t start, int64_t n,
-                                  double value) {
+                                  double value, const double* __restrict__ max_priority, double alpha) {
+  // replay_buffer.py:133-135: new leaves = max_priority ** alpha, read on the device (no host sync)
+  if (max_priority) value = pow(max_priority[0], alpha);
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t leaf = cap + (start + k) % ring;
     sum_tree[leaf] = value;
@@ -372,16 +374,16 @@ extern "C" int cacto_per_init(double* sum_tree_d, double* min_tree_d, int64_t ca
   return CACTO_OK;
 }
 
-extern "C" int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
-                                   int64_t start, int64_t n, double value, void* stream) {
+namespace {
+int per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size, int64_t start,
+                  int64_t n, double value, const double* max_priority_d, double alpha, hipStream_t st) {
   CACTO_REQUIRE(sum_tree_d && min_tree_d && pow2(capacity) && ring_size > 0 && ring_size <= capacity && n >= 0 &&
                     start >= 0 && start < ring_size,
                 "cacto_per_set_range: bad arguments");
   if (n == 0) return CACTO_OK;
-  hipStream_t st = as_stream(stream);
   n = std::min(n, ring_size);
   hipLaunchKernelGGL(k_per_fill_leaves, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
-                     sum_tree_d, min_tree_d, capacity, ring_size, start, n, value);
+                     sum_tree_d, min_tree_d, capacity, ring_size, start, n, value, max_priority_d, alpha);
   CACTO_CHECK_HIP(hipGetLastError());
   // affected leaf interval(s); refresh the covering node interval per level (superset is harmless)
   const int64_t a = start, b = start + n - 1;
@@ -395,6 +397,20 @@ extern "C" int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64
     CACTO_CHECK_HIP(hipGetLastError());
   }
   return CACTO_OK;
+}
+}  // namespace
+
+extern "C" int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
+                                   int64_t start, int64_t n, double value, void* stream) {
+  return per_set_range(sum_tree_d, min_tree_d, capacity, ring_size, start, n, value, nullptr, 0.0, as_stream(stream));
+}
+
+extern "C" int cacto_per_set_range_max(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
+                                       int64_t start, int64_t n, const double* max_priority_d, double alpha,
+                                       void* stream) {
+  CACTO_REQUIRE(max_priority_d, "cacto_per_set_range_max: null max_priority_d");
+  return per_set_range(sum_tree_d, min_tree_d, capacity, ring_size, start, n, 0.0, max_priority_d, alpha,
+                       as_stream(stream));
 }
 
 extern "C" int cacto_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,

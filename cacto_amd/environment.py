@@ -10,7 +10,7 @@ import random
 import numpy as np
 import torch
 
-from .system import DEVICE, System, dptr, stream
+from .system import DEVICE, dptr, shared_system, stream
 from . import _lib as L
 
 
@@ -25,7 +25,7 @@ class Env:
 
     def __init__(self, conf):
         self.conf = conf
-        self.sys = System(conf)
+        self.sys = shared_system(conf)
         self.nq, self.nv = conf.nq, conf.nv
         self.nx, self.nu = conf.nx, conf.na
         self.offset = conf.cost_funct_param[0]
@@ -108,6 +108,36 @@ class Env:
         EE = torch.empty(1, 3, dtype=torch.float64, device=DEVICE)
         L.lib().call("cacto_env_ee", self.sys.handle, dptr(S), dptr(EE), 1, stream())
         return EE[0].cpu().numpy()
+
+    def augmented_derivative(self, state, action):
+        """environment.py:111-132 (SI :221-233, Car :420-435, CarPark :567-582): discrete-time
+        (Fx [nx, nx], Fu [nx, na]) float64, as TO.backward_pass consumes them (TO.py:181)."""
+        Fx, Fu = self.augmented_derivative_batch(np.asarray(state, dtype=np.float64)[None],
+                                                 np.asarray(action, dtype=np.float64)[None])
+        return Fx[0].cpu().numpy(), Fu[0].cpu().numpy()
+
+    def augmented_derivative_batch(self, S, A):
+        """augmented_derivative over rows on the device: (Fx [B, nx, nx], Fu [B, nx, na]) float64."""
+        S = _as_dev(S, torch.float64)
+        A = _as_dev(A, torch.float64)
+        B, nx = S.shape[0], self.ns - 1
+        Fx = torch.empty(B, nx, nx, dtype=torch.float64, device=DEVICE)
+        Fu = torch.empty(B, nx, self.na, dtype=torch.float64, device=DEVICE)
+        L.lib().call("cacto_env_jacobians", self.sys.handle, dptr(S, torch.float64, (B, self.ns)),
+                     dptr(A, torch.float64, (B, self.na)), B, dptr(Fx), dptr(Fu), stream())
+        return Fx, Fu
+
+    def bound_control_cost(self, action):
+        """environment.py:158-163: sum_i a_i^2 + w_b (a_i / u_max_i)^10 (float64)."""
+        return float(self.bound_control_cost_batch(np.asarray(action, dtype=np.float64)[None])[0].item())
+
+    def bound_control_cost_batch(self, A):
+        A = _as_dev(A, torch.float64)
+        B = A.shape[0]
+        out = torch.empty(B, dtype=torch.float64, device=DEVICE)
+        L.lib().call("cacto_env_bound_control_cost", self.sys.handle, dptr(A, torch.float64, (B, self.na)), dptr(out),
+                     B, stream())
+        return out
 
     def reward(self, weights, state, action=None):
         """Per-system reward (environment.py:252-275, :329-351, :695-723); action=None -> u_cost 0."""

@@ -73,6 +73,22 @@ class Net:
             off += n
         return out
 
+    def split(self, flat):
+        """Views of a flat Keras-order vector (parameters or gradients) per trainable variable."""
+        out, off = [], 0
+        for sh in self.shapes:
+            n = int(np.prod(sh))
+            out.append(flat[off:off + n].reshape(sh))
+            off += n
+        return out
+
+    @property
+    def trainable_variables(self):
+        """Keras `model.trainable_variables`: device views of the flat parameters (kernels [in,out])."""
+        return self.split(self.flat)
+
+    variables = trainable_variables
+
     def copy_from(self, other):
         self.buf.copy_(other.buf)
 
@@ -163,28 +179,71 @@ class NN:
                      stream())
         return V.reshape(B, 1), g
 
-    # ---- gradients on explicit tensors (the training loop uses replay rows directly) ----
+    # ---- NeuralNetwork.py:150-233 with the reference's signatures ----
     @staticmethod
     def _rows(state, R, state_next, dVdx, d, term):
-        f = lambda x: torch.as_tensor(x, device=DEVICE).to(torch.float64).reshape(len(state), -1)
+        f = lambda x: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x,
+                                      device=DEVICE).to(torch.float64).reshape(len(state), -1)
         return torch.cat([f(state), f(R), f(state_next), f(dVdx), f(d), f(term)], dim=1).contiguous()
 
-    def compute_critic_grad(self, learner, state_batch, state_next_rollout_batch, partial_reward_to_go_batch,
-                            dVdx_batch, d_batch, weights_batch, term_batch=None):
-        """NeuralNetwork.py:150-178. Returns (grads [Keras order], y [B,1], V [B,1], V_tgt(s) [B,1]).
-        `learner` is the RL_AC holding the critic/target/optimizer state."""
-        B = len(state_batch)
-        term = np.zeros(B) if term_batch is None else term_batch
-        rows = self._rows(state_batch, partial_reward_to_go_batch, state_next_rollout_batch, dVdx_batch, d_batch,
-                          term)
-        idx = torch.arange(B, dtype=torch.int32, device=DEVICE)
-        w = torch.as_tensor(weights_batch, dtype=torch.float32, device=DEVICE).reshape(B).contiguous()
-        return learner.critic_grad_rows(rows, idx, w)
+    def _cfg(self, B):
+        cfg = L.UpdateCfg()
+        cfg.w_S = float(self.w_S)
+        cfg.MC = int(self.conf.MC)
+        cfg.B_global = int(B)
+        cfg.want_target_V = 1
+        return cfg
 
-    def compute_actor_grad(self, learner, state_batch, term_batch, batch_size=None):
-        """NeuralNetwork.py:180-233 (uses the learner's current critic)."""
+    def _scratch(self, B):
+        """Workspace and a private optimizer-counter pair for the standalone gradient calls: the
+        device gradient kernels advance `step_d` (the fused update's Keras iterations), which a
+        bare compute_*_grad must not do to the learner's counters."""
+        if getattr(self, "_ws_B", 0) < B:
+            self._ws = torch.empty(self.sys.workspace_bytes(B) // 4 + 64, dtype=torch.float32, device=DEVICE)
+            self._ws_B = B
+            self._steps = torch.zeros(2, dtype=torch.int32, device=DEVICE)
+        return self._ws, self._steps
+
+    def _nets(self, actor=None, critic=None, target=None):
+        ws, steps = self._scratch(1)
+        fill = (critic or actor).buf
+        p = lambda n: (n.buf if n is not None else fill).data_ptr()
+        scratch = ws.data_ptr()   # Adam moments are never touched by the gradient kernels
+        return L.Nets(p(actor), scratch, scratch, p(critic), scratch, scratch, p(target), steps.data_ptr())
+
+    def compute_critic_grad(self, critic_model, target_critic, state_batch, state_next_rollout_batch,
+                            partial_reward_to_go_batch, dVdx_batch, d_batch, weights_batch):
+        """NeuralNetwork.py:150-178. Returns (critic_grad [Keras trainable_variables order],
+        reward_to_go_batch [B,1], critic_value [B,1], V_target(state_batch) [B,1])."""
         B = len(state_batch)
+        rows = self._rows(state_batch, partial_reward_to_go_batch, state_next_rollout_batch, dVdx_batch, d_batch,
+                          np.zeros(B))
+        ws, _ = self._scratch(B)
+        nets = self._nets(critic=critic_model, target=target_critic)
+        idx = torch.arange(B, dtype=torch.int32, device=DEVICE)
+        w = torch.as_tensor(np.asarray(weights_batch) if not isinstance(weights_batch, torch.Tensor) else weights_batch,
+                            dtype=torch.float32, device=DEVICE).reshape(B).contiguous()
+        grad = torch.empty(critic_model.P, dtype=torch.float32, device=DEVICE)
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        V, Vt = torch.empty_like(y), torch.empty_like(y)
+        L.lib().call("cacto_critic_grad", self.sys.handle, C.byref(nets), C.byref(self._cfg(B)),
+                     dptr(rows, torch.float64), dptr(idx, torch.int32), dptr(w), B, dptr(grad), dptr(y), dptr(V),
+                     dptr(Vt), dptr(ws), ws.numel() * 4, stream())
+        return critic_model.split(grad), y.reshape(B, 1), V.reshape(B, 1), Vt.reshape(B, 1)
+
+    def compute_actor_grad(self, actor_model, critic_model, state_batch, term_batch, batch_size=None):
+        """NeuralNetwork.py:180-233: grads of mean_b(-dQ/da_b . pi(s_b)) against `critic_model`.
+        `batch_size` only shapes the reference's reshapes; the mean is over len(state_batch)."""
+        B = len(state_batch)
+        if batch_size is not None and int(batch_size) != B:
+            raise ValueError("compute_actor_grad: batch_size %d != len(state_batch) %d" % (batch_size, B))
         z = np.zeros((B, self.sys.ns))
         rows = self._rows(state_batch, np.zeros(B), z, z, np.zeros(B), term_batch)
+        ws, _ = self._scratch(B)
+        nets = self._nets(actor=actor_model, critic=critic_model, target=critic_model)
         idx = torch.arange(B, dtype=torch.int32, device=DEVICE)
-        return learner.actor_grad_rows(rows, idx, batch_size or B)
+        grad = torch.empty(actor_model.P, dtype=torch.float32, device=DEVICE)
+        L.lib().call("cacto_actor_grad", self.sys.handle, C.byref(nets), C.byref(self._cfg(B)),
+                     dptr(rows, torch.float64), dptr(idx, torch.int32), B, dptr(grad), dptr(ws), ws.numel() * 4,
+                     stream())
+        return actor_model.split(grad)

@@ -11,15 +11,16 @@ import numpy as np
 import torch
 
 from . import _lib as L
-from .system import DEVICE, dptr, stream
+from .system import DEVICE, dptr, shared_system, stream
 
 
 class ReplayBuffer:
     prioritized = False
 
-    def __init__(self, conf, sys):
+    def __init__(self, conf, sys=None):
+        """replay_buffer.py:10 `ReplayBuffer(conf)`; `sys` defaults to the conf's shared System."""
         self.conf = conf
-        self.sys = sys
+        self.sys = sys if sys is not None else shared_system(conf)
         self.N = conf.REPLAY_SIZE
         self.ns = conf.nb_state
         self.cols = 3 * self.ns + 3
@@ -143,7 +144,8 @@ class PrioritizedReplayBuffer(ReplayBuffer):
     """replay_buffer.py:87-218 (with the three shipped crash bugs fixed — DESIGN.md §PER)."""
     prioritized = True
 
-    def __init__(self, conf, sys, py_random=None):
+    def __init__(self, conf, sys=None, py_random=None):
+        """replay_buffer.py:88 `PrioritizedReplayBuffer(conf)`."""
         super().__init__(conf, sys)
         cap = 1
         while cap < self.N:
@@ -161,10 +163,9 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         self.random = py_random or random  # replay_buffer.py:150 uses the global `random`
 
     def _rows_added(self, start, n):
-        # leaves = max_priority ** alpha (replay_buffer.py:133-135); max_priority read on the host
-        leaf = float(self.max_priority.item()) ** self.alpha
-        L.lib().call("cacto_per_set_range", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.N, start, n,
-                     leaf, stream())
+        # leaves = max_priority ** alpha (replay_buffer.py:133-135), max_priority read on the device
+        L.lib().call("cacto_per_set_range_max", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.N, start, n,
+                     dptr(self.max_priority, torch.float64), self.alpha, stream())
 
     def sample_device(self, uniforms=None):
         """_sample_proportional + IS weights + exp_counter (replay_buffer.py:139-188)."""
@@ -219,8 +220,9 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         """replay_buffer.py:190-218 ('PER')."""
         idx = torch.as_tensor(np.asarray(idxes, dtype=np.int32) if not isinstance(idxes, torch.Tensor) else idxes,
                               dtype=torch.int32, device=DEVICE).contiguous()
-        self.update_priorities_device(idx, torch.as_tensor(reward_to_go_batch, device=DEVICE),
-                                      torch.as_tensor(critic_value, device=DEVICE))
+        f32 = lambda x: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x, dtype=torch.float32,
+                                        device=DEVICE).reshape(-1).contiguous()
+        self.update_priorities_device(idx, f32(reward_to_go_batch), f32(critic_value))
 
     def set_leaves(self, idx, values):
         idx = torch.as_tensor(np.asarray(idx, dtype=np.int32), device=DEVICE)

@@ -34,6 +34,28 @@ def dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update):
     apply("actor", ga, False)
 
 
+class Adam:
+    """tf.keras.optimizers.Adam surface (RL.py:79-88) over the device Keras-2.11 Adam step
+    (`cacto_adam_step`, with the learner's PiecewiseConstantDecay schedule when LR_SCHEDULE)."""
+
+    def __init__(self, learner, which):
+        self.learner = learner
+        self.which = which
+
+    @property
+    def iterations(self):
+        return int(self.learner.steps[0 if self.which == CRITIC else 1].item())
+
+    def apply_gradients(self, grads_and_vars):
+        """optimizer.apply_gradients(zip(grads, model.trainable_variables)) (RL.py:105, :109)."""
+        grads = [g for g, _ in grads_and_vars]
+        flat = torch.cat([torch.as_tensor(g, dtype=torch.float32, device=DEVICE).reshape(-1) for g in grads])
+        # the device Adam reads the counter as Keras `iterations + 1` (the fused update's gradient
+        # kernels advance it; a standalone apply_gradients advances it here)
+        self.learner.steps[0 if self.which == CRITIC else 1] += 1
+        self.learner.apply_gradients(self.which, flat)
+
+
 class RL_AC:
     def __init__(self, env, NN, conf, N_try=0, w_S=None):
         self.env = env
@@ -80,6 +102,8 @@ class RL_AC:
                            self.critic_model.buf.data_ptr(), self.critic_m.data_ptr(), self.critic_v.data_ptr(),
                            self.target_critic.buf.data_ptr(), self.steps.data_ptr())
         self.cfg = self.make_cfg()
+        self.critic_optimizer = Adam(self, CRITIC)
+        self.actor_optimizer = Adam(self, ACTOR)
 
     def make_cfg(self, B_global=None):
         c = self.conf
@@ -152,19 +176,10 @@ class RL_AC:
         y = torch.empty(B, dtype=torch.float32, device=DEVICE)
         V, Vt = torch.empty_like(y), torch.empty_like(y)
         grad = self.critic_grad_flat(rows, idx, w, y, V, Vt if want_vt else None)
-        return self._split(grad, self.critic_model), y.reshape(B, 1), V.reshape(B, 1), Vt.reshape(B, 1)
+        return self.critic_model.split(grad), y.reshape(B, 1), V.reshape(B, 1), Vt.reshape(B, 1)
 
     def actor_grad_rows(self, rows, idx, batch_size=None):
-        return self._split(self.actor_grad_flat(rows, idx), self.actor_model)
-
-    @staticmethod
-    def _split(flat, net):
-        out, off = [], 0
-        for s in net.shapes:
-            n = int(np.prod(s))
-            out.append(flat[off:off + n].reshape(s))
-            off += n
-        return out
+        return self.actor_model.split(self.actor_grad_flat(rows, idx))
 
     def apply_gradients(self, which, flat_grad, soft_update=False):
         """optimizer.apply_gradients (RL.py:105/:109) for a flat gradient (after the grad call that
@@ -319,9 +334,22 @@ class RL_AC:
 
     # ---- RL.py:145-189 (host, float64 as the reference) ----
     def RL_Solve(self, TO_controls, TO_states, TO_step_cost):
+        """One episode's n-step targets. Returns (state_arr, partial_reward_to_go_arr,
+        total_reward_to_go_arr, state_next_rollout_arr, done_arr, rwrd_arr, term_arr, ep_return,
+        ee_pos_arr). With env_RL the episode is re-simulated from TO_controls on the device
+        (RL.py:157-165: Env.step with the running weights, EE of every state, terminal reward);
+        otherwise states and rewards are the TO's (RL.py:166-167) and ee_pos_arr is the array
+        create_TO_init started (row 0 = EE(s_0); the reference leaves the other rows unset —
+        np.empty — and main.py:192-193 replaces it with the TO's EE positions)."""
         T = self.NSTEPS_SH
-        rwrd = -np.asarray(TO_step_cost, dtype=np.float64)
         ns = self.conf.nb_state
+        self.control_arr = TO_controls
+        if self.conf.env_RL:
+            S, rwrd, EE = self._env_rl_episode(np.asarray(TO_controls, dtype=np.float64), T)
+            self.state_arr, self.ee_pos_arr = S, EE
+        else:
+            self.state_arr = TO_states
+            rwrd = -np.asarray(TO_step_cost, dtype=np.float64)
         s_next = np.zeros((T + 1, ns))
         partial = np.empty(T + 1)
         total = np.empty(T + 1)
@@ -337,11 +365,32 @@ class RL_AC:
                 if final == T:
                     done[i] = 1
                 else:
-                    s_next[i, :] = TO_states[final + 1, :]
+                    s_next[i, :] = self.state_arr[final + 1, :]
             partial[i] = np.float32(sum(rwrd[i:final + 1]))
             total[i] = np.float32(sum(rwrd[i:T + 1]))
         ep_return = sum(rwrd)
-        return TO_states, partial, total, s_next, done, rwrd, term, ep_return, None
+        return self.state_arr, partial, total, s_next, done, rwrd, term, ep_return, self.ee_pos_arr
+
+    def _env_rl_episode(self, controls, T):
+        """RL.py:157-165 on the device: s_{i+1}, r_i = Env.step(w_running, s_i, u_i),
+        ee_{i+1} = EE(s_{i+1}); r_T = reward(w_terminal, s_T). One launch per step, no host sync."""
+        ns = self.conf.nb_state
+        S = torch.empty(T + 1, ns, dtype=torch.float64, device=DEVICE)
+        S[0] = torch.as_tensor(np.asarray(self.state_arr[0], dtype=np.float64), device=DEVICE)
+        R = torch.empty(T + 1, dtype=torch.float64, device=DEVICE)
+        EE = torch.empty(T + 1, 3, dtype=torch.float64, device=DEVICE)
+        U = torch.as_tensor(controls, device=DEVICE)
+        W = torch.as_tensor(np.asarray(self.conf.cost_weights_running, dtype=np.float64), device=DEVICE)
+        h = self.sys.handle
+        for i in range(T):
+            L.lib().call("cacto_env_step", h, dptr(S[i:i + 1]), dptr(U[i:i + 1].contiguous()), dptr(W),
+                         dptr(S[i + 1:i + 2]), dptr(R[i:i + 1]), dptr(EE[i + 1:i + 2]), 1, stream())
+        Wt = torch.as_tensor(np.asarray(self.conf.cost_weights_terminal, dtype=np.float64), device=DEVICE)
+        zero = torch.zeros(1, self.conf.nb_action, dtype=torch.float64, device=DEVICE)
+        L.lib().call("cacto_env_step", h, dptr(S[T:T + 1]), dptr(zero), dptr(Wt), None, dptr(R[T:T + 1]), None, 1,
+                     stream())
+        L.lib().call("cacto_env_ee", h, dptr(S[0:1]), dptr(EE[0:1]), 1, stream())
+        return S.cpu().numpy(), R.cpu().numpy(), EE.cpu().numpy()
 
     def RL_save_weights(self, update_step_counter='final'):
         """RL.py:191-195: Keras-2.11 .h5 files the reference can load."""
@@ -370,16 +419,18 @@ class RL_AC:
             return self._launch_rollout(S0, n, order, T, ep, weights, out, actor, sched)
         f64 = dict(dtype=torch.float64, device=DEVICE)
         out = {}
-        # rewards and EE positions are evaluated from the recorded (s_t, a_t) after the rollout
+        # rewards and EE positions are evaluated from the recorded (s_t, a_t) after the rollout.
+        # Zero-filled: the rows of an episode past its NSTEPS_SH are never written, and consumers
+        # that take whole [R, T+1, .] blocks (DDP labels, RL_Solve, host copies) must not see junk.
         need_sa = "R" in want or "EE" in want
         if "S" in want or need_sa:
-            out["S"] = torch.empty(R, T + 1, ns, **f64)
+            out["S"] = torch.zeros(R, T + 1, ns, **f64)
         if "A" in want or (need_sa and ep != 0):
-            out["A"] = torch.empty(R, T, na, dtype=torch.float32, device=DEVICE)
+            out["A"] = torch.zeros(R, T, na, dtype=torch.float32, device=DEVICE)
         if "R" in want:
-            out["R"] = torch.empty(R, T, **f64)
+            out["R"] = torch.zeros(R, T, **f64)
         if "EE" in want:
-            out["EE"] = torch.empty(R, T + 1, 3, **f64)
+            out["EE"] = torch.zeros(R, T + 1, 3, **f64)
         out["status"] = torch.empty(R, dtype=torch.int32, device=DEVICE)
         return self._launch_rollout(S0, n, order, T, ep, weights, out, actor, sched)
 
@@ -404,15 +455,23 @@ class RL_AC:
         return self.conf.NSTEPS - int(s0[-1] / self.conf.dt)
 
     def create_TO_init(self, ep, ICS):
-        """RL.py:197-233 for one episode."""
+        """RL.py:197-233 for one episode (one cacto_rollout launch). Returns (init_rand_state,
+        init_TO_states, init_TO_controls, NSTEPS_SH, success_init_flag); leaves state_arr,
+        control_arr and ee_pos_arr (row 0 = EE(ICS)) for RL_Solve as the reference does."""
         self.init_rand_state = ICS
         self.NSTEPS_SH = self.nsteps_sh(ICS)
         if self.NSTEPS_SH == 0:
             return None, None, None, None, 0
         T = self.NSTEPS_SH
+        ns, na = self.conf.nb_state, self.conf.nb_action
+        self.control_arr = np.empty((T, na))
+        self.state_arr = np.empty((T + 1, ns))
+        self.ee_pos_arr = np.zeros((T + 1, 3))
+        self.state_arr[0, :] = ICS
+        self.ee_pos_arr[0, :] = self.env.get_end_effector_position(self.state_arr[0, :])
         out = self.rollout_batch(np.asarray(ICS)[None], [T], T, ep=ep, want=("S", "A"))
         if int(out["status"][0].item()) != 0:
             return None, None, None, None, 0
         states = out["S"][0].cpu().numpy()
-        controls = out["A"][0].double().cpu().numpy()
+        controls = out["A"][0].double().cpu().numpy() if "A" in out else np.zeros((T, na))
         return self.init_rand_state, states, controls, self.NSTEPS_SH, 1

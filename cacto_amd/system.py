@@ -40,6 +40,21 @@ def _fill(arr, values):
         arr[i] = float(v)
 
 
+_SHARED = {}
+
+
+def shared_system(conf):
+    """The System of a conf module, created once: the reference constructs `Environment(conf)`,
+    `ReplayBuffer(conf)`, `NN(env, conf)` ... from the same conf (main.py:145-150), and they all
+    address one device copy of it (one `cacto_sys` handle)."""
+    key = id(conf)
+    hit = _SHARED.get(key)
+    if hit is None or hit[0] is not conf:
+        hit = (conf, System(conf))
+        _SHARED[key] = hit
+    return hit[1]
+
+
 class System:
     """Numeric content of a conf module + the device copy the kernels read."""
 

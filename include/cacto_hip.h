@@ -9,6 +9,8 @@
  *                          from NN.compute_actor_grad NeuralNetwork.py:188, :199-204
  *   cacto_env_step         Env.step + get_end_effector_position (float64 rollout semantics)
  *                          environment.py:70-78, :146-156; plot_utils.py:262-264
+ *   cacto_env_jacobians    Env.augmented_derivative environment.py:111-132 (as called by TO.py:181)
+ *   cacto_env_bound_control_cost  Env.bound_control_cost environment.py:158-163
  *   cacto_rollout          RL_AC.create_TO_init loop RL.py:223-231 / PLOT.rollout plot_utils.py:245-279
  *   cacto_rollout_rewards  Env.step reward / get_end_effector_position over recorded trajectories
  *   cacto_ddp_backward     TO.backward_pass TO.py:119-202 (dV/dx Sobolev labels)
@@ -138,6 +140,18 @@ int cacto_env_ee(const cacto_sys* sys, const double* S_d, double* EE_d, int B, v
  * W_d may be NULL (running weights). EE_d [B,3], any output may be NULL. */
 int cacto_env_step(const cacto_sys* sys, const double* S_d, const double* A_d, const double* W_d,
                    double* S_next_d, double* R_d, double* EE_d, int B, void* stream);
+
+/* Env.augmented_derivative(s, a) (environment.py:111-132; SI :221-233, Car :420-435, CarPark
+ * :567-582) for B float64 rows S_d [B,ns], A_d [B,na]: Fx_d [B,nx,nx] = I + dt*[[0,I],[ddq_dq,ddq_dv]]
+ * (closed forms for SI / car / car_park / the prismatic DI pair; hyper-dual RNEA for revolute chains,
+ * computeABADerivatives) and Fu_d [B,nx,na] = dt*[0; M^-1] (not normalised), nx = ns-1. Called by the
+ * host TO backward pass (TO.py:181); cacto_ddp_backward evaluates the same device code inline. */
+int cacto_env_jacobians(const cacto_sys* sys, const double* S_d, const double* A_d, int B, double* Fx_d,
+                        double* Fu_d, void* stream);
+
+/* Env.bound_control_cost(a) (environment.py:158-163) for B float64 action rows A_d [B,na]:
+ * out_d[b] = sum_i a_i^2 + w_b*(a_i/u_max_i)^10, accumulated in action order. */
+int cacto_env_bound_control_cost(const cacto_sys* sys, const double* A_d, double* out_d, int B, void* stream);
 
 /* ---------------------------------------------------------------- networks --------------- */
 
@@ -323,6 +337,10 @@ int cacto_per_init(double* sum_tree_d, double* min_tree_d, int64_t capacity, voi
 /* Set leaves [start, start+n) (mod ring_size) to `value` and refresh ancestors (replay_buffer.py:133-135). */
 int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
                         int64_t start, int64_t n, double value, void* stream);
+/* The same with the value max_priority_d[0] ** alpha read on the device (what ReplayBuffer.add sets new
+ * leaves to, replay_buffer.py:133-135), so adding episodes needs no host read of max_priority. */
+int cacto_per_set_range_max(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
+                            int64_t start, int64_t n, const double* max_priority_d, double alpha, void* stream);
 /* Stratified proportional sampling (replay_buffer.py:139-188). uniforms_d [B] = random.random()
  * draws. Outputs idx_d [B] int32, is_w_d [B] float32 (IS weights), and exp_counter_d (float64
  * [ring]) incremented once per distinct index. */

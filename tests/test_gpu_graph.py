@@ -94,14 +94,20 @@ def test_graph_replay_equals_eager_updates_with_per():
         assert torch.equal(getattr(ebuf, name), getattr(gbuf, name)), name
 
 
-@pytest.mark.parametrize("system,B", [("double_integrator", 128), ("double_integrator", 1000), ("manipulator", 64)])
-def test_pipelined_updates_equal_sequential(system, B):
-    """cacto_update_n overlaps critic(t+1) with actor(t) on two streams; the result is the same bits."""
+@pytest.mark.parametrize("system,B,K,MC", [("double_integrator", 128, 7, 0), ("double_integrator", 1000, 7, 0),
+                                         ("manipulator", 64, 7, 0), ("double_integrator", 128, 1, 0),
+                                         ("double_integrator", 128, 2, 0), ("double_integrator", 128, 8, 0),
+                                         ("double_integrator", 128, 8, 1), ("double_integrator", 256, 3, 1)])
+def test_pipelined_updates_equal_sequential(system, B, K, MC):
+    """cacto_update_n overlaps critic(t+1) with actor(t) on two streams; the result is the same bits.
+    Odd K ends with the critic in the workspace copy (copied back), even K in the caller's buffer;
+    K = 1, 2 finish before the first two-updates-old wait; MC = 1 has no soft target update."""
     conf = load_conf(system)
+    conf.MC = MC
     env = make_env(conf)
     ns = conf.nb_state
     rng = np.random.default_rng(11)
-    N, K = 4096, 7
+    N = 4096
     S = np.column_stack([rng.uniform(-3, 3, (N, ns - 1)), rng.uniform(0, 4.9, N)])
     rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.01, rng.normal(size=(N, ns)) * 0.3,
                            (rng.uniform(size=(N, 1)) < 0.1).astype(float), (rng.uniform(size=(N, 1)) < 0.1)

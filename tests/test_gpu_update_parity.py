@@ -1,0 +1,263 @@
+"""Update-path parity at the settings the BASELINE configs run with, against the float64 oracle
+(oracle/nn.py: Keras-Adam, Sobolev critic loss; oracle/buffer.py: PER):
+
+  * IS-weighted critic loss (PrioritizedReplayBuffer weights, NeuralNetwork.py:167-173 with the
+    weights of replay_buffer.py:159-188) — configs[3];
+  * the manipulator's PiecewiseConstantDecay learning rate across its first boundary
+    (RL.py:80-85, conf_manipulator.py:51-72) — configs[2];
+  * a K-step learn_and_update loop with PER on car_park (sample -> update with IS weights ->
+    priority update -> target update, RL.py:120-143, replay_buffer.py:139-218), pipelined
+    (`cacto_update_n_per`), against the oracle's sequential loop — configs[3];
+  * one update per system at the BASELINE full batch (DI 4096, manipulator 8192, car_park 4096,
+    UR5 2048) against the oracle's gradients and Keras-Adam step.
+
+Tolerances (float32 MFMA chains vs float64 oracle): gradients rel-L2 < 2e-4 per tensor; weights
+after n Adam steps |dw| < 5e-6 * n (Adam normalises each step to ~lr, so a rounding-level
+gradient difference moves a weight by at most a small fraction of lr per step).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_weights
+from oracle import buffer as obuf
+from oracle import env as oenv
+from oracle import nn as onn
+from cacto_amd.confs import load_conf
+
+pytestmark = pytest.mark.gpu
+
+GRAD_TOL = 2e-4
+STEP_TOL = 5e-6
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def _setup(system, tag=None, w_S=1e-2, conf=None):
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.rl import RL_AC
+    conf = conf or load_conf(system)
+    env = make_env(conf)
+    nn = NN(env, conf, w_S=w_S, seed=3)
+    rl = RL_AC(env, nn, conf)
+    rl.setup_model(weights=load_weights(tag) if tag else None)
+    return conf, env, oenv.make_env(conf), rl
+
+
+def _states(conf, n, rng):
+    lo = np.array(conf.x_init_min, dtype=float)
+    hi = np.array(conf.x_init_max, dtype=float)
+    S = rng.uniform(lo, hi, size=(n, conf.nb_state))
+    flat = np.where(hi[:-1] - lo[:-1] < 1e-12)[0]
+    S[:, flat] = rng.uniform(-0.5, 0.5, size=(n, len(flat)))
+    return S
+
+
+def _rows(conf, n, rng):
+    ns = conf.nb_state
+    S, Sn = _states(conf, n, rng), _states(conf, n, rng)
+    R = rng.normal(size=(n, 1)) * 0.5
+    dVdx = rng.normal(size=(n, ns)) * 0.3
+    d = (rng.uniform(size=(n, 1)) < 0.3).astype(float)
+    term = (rng.uniform(size=(n, 1)) < 0.2).astype(float)
+    return np.concatenate([S, R, Sn, dVdx, d, term], axis=1)
+
+
+def _split(conf, rows):
+    """replay_buffer.py:52-61 column split; the reference converts the sample to float32."""
+    ns = conf.nb_state
+    r = rows.astype(np.float32).astype(np.float64)
+    return (r[:, :ns], r[:, ns:ns + 1], r[:, ns + 1:2 * ns + 1], r[:, 2 * ns + 1:3 * ns + 1],
+            r[:, 3 * ns + 1:3 * ns + 2], rows[:, 3 * ns + 2:3 * ns + 3])
+
+
+def _oracle_update(conf, oe, nets, opt, rows, w, w_S):
+    """RL_AC.update + update_target (RL.py:101-118) in float64."""
+    crit, tgt, act = nets
+    oc, oa = opt
+    norm = conf.state_norm_arr.astype(np.float64)
+    s, R, sn, dv, d, term = _split(conf, rows)
+    gc, y, V = onn.compute_critic_grad(crit, tgt, s, sn, R, dv, d, w, w_S, norm, MC=bool(conf.MC))[:3]
+    crit = oc.apply(crit, gc)
+    ga = onn.compute_actor_grad(oe, act, crit, s.astype(np.float32), term, norm)
+    act = oa.apply(act, ga)
+    if not conf.MC:
+        tgt = onn.soft_update(tgt, crit, conf.UPDATE_RATE)
+    return (crit, tgt, act), gc, ga, y, V
+
+
+def _weights(rl):
+    return (rl.critic_model.get_weights(), rl.target_critic.get_weights(), rl.actor_model.get_weights())
+
+
+def _assert_weights(rl, nets, n_steps, tol=STEP_TOL):
+    for name, got, ref in zip(("critic", "target", "actor"), _weights(rl), nets):
+        for i, (a, b) in enumerate(zip(got, ref)):
+            err = np.abs(a - b).max()
+            assert err < tol * n_steps, (name, i, err)
+
+
+# ------------------------------------------------------------------ (a) IS-weighted critic loss
+@pytest.mark.parametrize("system,tag,w_S,B", [("double_integrator", "di_seed0_0", 1e-2, 128),
+                                              ("car_park", None, 0.0, 64),
+                                              ("manipulator", None, 1e-2, 64),
+                                              ("ur5", None, 1e-2, 64)])
+def test_critic_grad_is_weights(system, tag, w_S, B):
+    """sample_weight = PER IS weights (NeuralNetwork.py:167-173): non-unit, spread over [0.2, 1]."""
+    conf, env, oe, rl = _setup(system, tag, w_S)
+    rng = np.random.default_rng(21)
+    rows = _rows(conf, B, rng)
+    w = rng.uniform(0.2, 1.0, size=B).astype(np.float32)
+    rows_d = torch.as_tensor(rows, device="cuda")
+    idx_d = torch.arange(B, dtype=torch.int32, device="cuda")
+    g = rl.critic_grad_rows(rows_d, idx_d, torch.as_tensor(w, device="cuda"))[0]
+    s, R, sn, dv, d, _ = _split(conf, rows)
+    ref = onn.compute_critic_grad(rl.critic_model.get_weights(), rl.target_critic.get_weights(), s, sn, R, dv, d,
+                                  w.astype(np.float64).reshape(B, 1), w_S, conf.state_norm_arr.astype(np.float64))
+    for i, (a, b) in enumerate(zip(g, ref[0])):
+        assert rel_l2(a.cpu().numpy(), b) < GRAD_TOL, (i, rel_l2(a.cpu().numpy(), b))
+    # the weights must matter: the unit-weight gradient is far from the weighted one
+    g1 = rl.critic_grad_rows(rows_d, idx_d)[0]
+    assert rel_l2(g1[0].cpu().numpy(), ref[0][0]) > 10 * GRAD_TOL
+
+
+def test_update_rows_is_weights_sequence():
+    """Five fused cacto_update steps with IS weights == the oracle's weighted sequence."""
+    conf, env, oe, rl = _setup("car_park", None, 0.0)
+    rng = np.random.default_rng(22)
+    N, B, K = 1024, 64, 5
+    rows = _rows(conf, N, rng)
+    storage = torch.as_tensor(rows, device="cuda")
+    nets = _weights(rl)
+    opt = (onn.KerasAdam(conf.CRITIC_LEARNING_RATE), onn.KerasAdam(conf.ACTOR_LEARNING_RATE))
+    for k in range(K):
+        idx = rng.integers(0, N, size=B)
+        w = rng.uniform(0.1, 1.0, size=B).astype(np.float32)
+        rl.update_rows(storage, torch.as_tensor(idx.astype(np.int32), device="cuda"), torch.as_tensor(w, device="cuda"))
+        nets = _oracle_update(conf, oe, nets, opt, rows[idx], w.astype(np.float64).reshape(B, 1), 0.0)[0]
+    torch.cuda.synchronize()
+    _assert_weights(rl, nets, K)
+
+
+# ------------------------------------------------------------------ (b) PER learn_and_update loop
+def test_per_loop_car_park_matches_oracle():
+    """configs[3]: K = 6 pipelined PER updates (cacto_update_n_per) == the oracle's sequential
+    sample -> IS-weighted update -> priority update -> target update loop. Indices are compared
+    through exp_counter (incremented once per distinct sampled index), leaves to f32 rounding."""
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    conf, env, oe, rl = _setup("car_park", None, 0.0)
+    conf.prioritized_replay_alpha = 0.6            # bench/BASELINE build choice (reference ships 0)
+    per = PrioritizedReplayBuffer(conf, rl.sys)
+    o = obuf.PrioritizedReplayBuffer(conf.REPLAY_SIZE, conf.nb_state, 0.6, conf.prioritized_replay_beta,
+                                     conf.prioritized_replay_eps, conf.fresh_factor, conf.BATCH_SIZE)
+    rng = np.random.default_rng(23)
+    n_rows, K, B = 4000, 6, conf.BATCH_SIZE
+    rows = _rows(conf, n_rows, rng)
+    per.add_rows(rows)
+    o.add_rows(rows)
+    nets = _weights(rl)
+    U = rng.uniform(size=(K, B))
+    rl.update_rows_n_per(per, torch.as_tensor(U, device="cuda"))
+    opt = (onn.KerasAdam(conf.CRITIC_LEARNING_RATE), onn.KerasAdam(conf.ACTOR_LEARNING_RATE))
+    for k in range(K):
+        idx = o.sample_proportional(U[k])
+        w = o.sample_weights(idx).reshape(B, 1)
+        nets, _, _, y, V = _oracle_update(conf, oe, nets, opt, rows[idx], w, 0.0)
+        o.update_priorities(idx, y.astype(np.float32), V.astype(np.float32))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(per.exp_counter[:n_rows].cpu().numpy(), o.exp_counter[:n_rows])
+    cap = per.cap
+    st = per.sum_tree.cpu().numpy()
+    np.testing.assert_allclose(st[cap:cap + n_rows], o.it_sum.value[cap:cap + n_rows], rtol=2e-5)
+    np.testing.assert_allclose(per.min_tree.cpu().numpy()[1], o.it_min.value[1], rtol=2e-5)
+    np.testing.assert_allclose(float(per.max_priority.item()), o.max_priority, rtol=2e-5)
+    assert rl.steps.cpu().tolist() == [K, K]
+    _assert_weights(rl, nets, K)
+
+
+# ------------------------------------------------------------------ (c) LR schedule boundary
+def test_manipulator_lr_schedule_crosses_boundary():
+    """configs[2]: PiecewiseConstantDecay(boundaries=[200, 300, 400, 500]*REPLAY_SIZE/B, values
+    lr*[1, 1/2, 1/4, 1/8, 1/16]). The optimizer iterations are seeded just below the first
+    boundary (204,800) so the 5 steps use lr, lr, lr, lr/2, lr/2 (iterations 204,798..204,802;
+    the schedule reads `iterations` before the increment)."""
+    conf, env, oe, rl = _setup("manipulator", None, 0.0)
+    assert conf.LR_SCHEDULE and conf.boundaries_schedule_LR_C[0] == 204800
+    start = 204798
+    rl.steps.fill_(start)
+    rng = np.random.default_rng(24)
+    N, B, K = 1024, conf.BATCH_SIZE, 5
+    rows = _rows(conf, N, rng)
+    storage = torch.as_tensor(rows, device="cuda")
+    idx_all = rng.integers(0, N, size=(K, B))
+    nets = _weights(rl)
+    oc = onn.KerasAdam((conf.boundaries_schedule_LR_C, conf.values_schedule_LR_C))
+    oa = onn.KerasAdam((conf.boundaries_schedule_LR_A, conf.values_schedule_LR_A))
+    oc.iterations = oa.iterations = start
+    lrs = []
+    for k in range(K):
+        lrs.append(oc.current_lr())
+        rl.update_rows(storage, torch.as_tensor(idx_all[k].astype(np.int32), device="cuda"))
+        nets = _oracle_update(conf, oe, nets, (oc, oa), rows[idx_all[k]], np.ones((B, 1)), 0.0)[0]
+    assert lrs == [conf.CRITIC_LEARNING_RATE] * 3 + [conf.CRITIC_LEARNING_RATE / 2] * 2
+    torch.cuda.synchronize()
+    assert rl.steps.cpu().tolist() == [start + K, start + K]
+    _assert_weights(rl, nets, K)
+    # without the schedule the result is measurably different (the halved steps matter)
+    conf_flat = load_conf("manipulator")
+    conf_flat.LR_SCHEDULE = 0
+    _, _, _, rl2 = _setup("manipulator", None, 0.0, conf=conf_flat)
+    rl2.steps.fill_(start)
+    for k in range(K):
+        rl2.update_rows(storage, torch.as_tensor(idx_all[k].astype(np.int32), device="cuda"))
+    d = np.abs(rl2.actor_model.get_weights()[0] - rl.actor_model.get_weights()[0]).max()
+    assert d > 50 * STEP_TOL, d
+
+
+# ------------------------------------------------------------------ (d) full-size updates
+@pytest.mark.parametrize("system,B,w_S", [("double_integrator", 4096, 1e-2), ("manipulator", 8192, 0.0),
+                                          ("car_park", 4096, 0.0), ("ur5", 2048, 1e-2)])
+def test_fullsize_update_matches_oracle(system, B, w_S):
+    """One learn_and_update iteration at the BASELINE batch: critic and actor gradients at rel-L2
+    < 2e-4 of the oracle's, then the fused cacto_update step's weights against the oracle's Adam
+    step (minibatch sampled from a full 65,536-row buffer)."""
+    tag = "di_seed0_0" if system == "double_integrator" else None
+    conf, env, oe, rl = _setup(system, tag, w_S)
+    rng = np.random.default_rng(25)
+    N = conf.REPLAY_SIZE
+    rows = _rows(conf, N, rng)
+    storage = torch.as_tensor(rows, device="cuda")
+    idx = rng.integers(0, N, size=B)
+    idx_d = torch.as_tensor(idx.astype(np.int32), device="cuda")
+    nets = _weights(rl)
+    opt = (onn.KerasAdam(conf.CRITIC_LEARNING_RATE), onn.KerasAdam(conf.ACTOR_LEARNING_RATE))
+    ref_nets, gc, _, _, _ = _oracle_update(conf, oe, nets, opt, rows[idx], np.ones((B, 1)), w_S)
+    rl.update_rows(storage, idx_d)
+    torch.cuda.synchronize()
+    assert rl.steps.cpu().tolist() == [1, 1]
+    _assert_weights(rl, ref_nets, 1)
+    # the gradients themselves, on a second learner (the gradient calls advance its counters): the
+    # critic's at the initial weights, then the actor's against the UPDATED critic (RL.py:104-109),
+    # i.e. with the oracle's updated critic rounded to f32 loaded into the device critic
+    _, _, _, rl_g = _setup(system, tag, w_S)
+    g = rl_g.critic_grad_rows(storage, idx_d, want_vt=False)[0]
+    for i, (a, b) in enumerate(zip(g, gc)):
+        assert rel_l2(a.cpu().numpy(), b) < GRAD_TOL, ("critic", i, rel_l2(a.cpu().numpy(), b))
+    rl_g.critic_model.set_weights([np.asarray(p, dtype=np.float32) for p in ref_nets[0]])
+    ga_dev = rl_g.actor_grad_rows(storage, idx_d)
+    s, _, _, _, _, term = _split(conf, rows[idx])
+    ga = onn.compute_actor_grad(oe, nets[2], rl_g.critic_model.get_weights(), s.astype(np.float32), term,
+                                conf.state_norm_arr.astype(np.float64))
+    for i, (a, b) in enumerate(zip(ga_dev, ga)):
+        assert rel_l2(a.cpu().numpy(), b) < GRAD_TOL, ("actor", i, rel_l2(a.cpu().numpy(), b))

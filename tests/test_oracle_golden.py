@@ -141,3 +141,17 @@ def test_weight_fixtures_shapes_and_identities():
         assert not b.any()
     for k, fan_in in zip(w["critic"][0:8:2], [5, 64, 64, 128]):
         assert np.abs(k).max() <= np.sqrt(6.0 / fan_in) + 1e-6
+
+
+@pytest.mark.parametrize("system", ["single_integrator", "double_integrator"])
+def test_product_env_reset_bit_exact(ref_vectors, system):
+    """cacto_amd.environment.Env.reset itself (host CPython `random`, environment.py:46-55) against
+    the reference's own draws after random.seed(0). reset touches only self.conf, so it runs here
+    without the device handle the rest of Env needs."""
+    import types
+    from cacto_amd.environment import Env
+    conf = load_conf(system)
+    env = types.SimpleNamespace(conf=conf)
+    random.seed(0)
+    got = np.asarray([Env.reset(env) for _ in range(200)])
+    np.testing.assert_array_equal(got, ref_vectors[system[:1] + "i_reset"])
