@@ -449,34 +449,60 @@ __global__ void __launch_bounds__(64) k_ddp_derivs(const SysDevice* __restrict__
 // Env.augmented_derivative (environment.py:111-132; SI :221-233, Car :420-435, CarPark :567-582) for
 // B independent (state, action) rows: the discrete-time Jacobians Fx [nx, nx], Fu [nx, na] that the
 // DDP pass consumes (the same device code), for host-side callers such as TO.backward_pass
-// (TO.py:181). One thread per row.
+// (TO.py:181). Closed-form systems: one thread per row. Revolute chains go through the split DDP
+// pass's derivative kernel (k_ddp_derivs: each row as a one-step episode, records extracted by
+// k_jac_extract), so their hyper-dual RNEA runs in exactly one kernel.
 template <int NJ>
 __global__ void __launch_bounds__(64) k_env_jacobians(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
                                                       const double* __restrict__ U, int B, double* __restrict__ Fx,
                                                       double* __restrict__ Fu) {
   constexpr int N = DdpDims<NJ>::N, M = DdpDims<NJ>::M, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const SysDevice& sd = *sdp;
-  double x[N], u[M], A[N * N], Bm[N * M];
+  if constexpr (NJ <= 2) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const SysDevice& sd = *sdp;
+    double x[N], A[N * N], Bm[N * M];
 #pragma unroll
-  for (int k = 0; k < N; ++k) x[k] = S[(size_t)b * ns + k];
+    for (int k = 0; k < N; ++k) x[k] = S[(size_t)b * ns + k];
+    if constexpr (NJ > 0) {
+      double Mm[M * M], Minv[M * M];
+      chain_mass<NJ>(sd, x, Mm);
+      small_inverse<M>(Mm, Minv);
+      ddp_jacobians<NJ>(sd, x, Minv, A, Bm);
+    } else {
+      ddp_jacobians<NJ>(sd, x, nullptr, A, Bm);
+    }
 #pragma unroll
-  for (int k = 0; k < M; ++k) u[k] = U[(size_t)b * na + k];
-  if constexpr (NJ > 2) {
-    ddp_chain_jacobians<NJ>(sd, x, u, A, Bm);
-  } else if constexpr (NJ > 0) {
-    double Mm[M * M], Minv[M * M];
-    chain_mass<NJ>(sd, x, Mm);
-    small_inverse<M>(Mm, Minv);
-    ddp_jacobians<NJ>(sd, x, Minv, A, Bm);
-  } else {
-    ddp_jacobians<NJ>(sd, x, nullptr, A, Bm);
+    for (int k = 0; k < N * N; ++k) Fx[(size_t)b * N * N + k] = A[k];
+#pragma unroll
+    for (int k = 0; k < N * M; ++k) Fu[(size_t)b * N * M + k] = Bm[k];
   }
-#pragma unroll
-  for (int k = 0; k < N * N; ++k) Fx[(size_t)b * N * N + k] = A[k];
-#pragma unroll
-  for (int k = 0; k < N * M; ++k) Fu[(size_t)b * N * M + k] = Bm[k];
+}
+
+// Rows -> one-step episodes for k_ddp_derivs: S2 [B, 2, ns] (the state twice), nsteps = 1.
+template <int NJ>
+__global__ void k_jac_prep(const double* __restrict__ S, int B, double* __restrict__ S2, int32_t* __restrict__ n1) {
+  constexpr int ns = Dims<NJ>::NS;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= B * 2 * ns) return;
+  const int b = k / (2 * ns), c = k % ns;
+  S2[k] = S[(size_t)b * ns + c];
+  if (k < B) n1[k] = 1;
+}
+
+// Step-0 A, B records ([t][k][e] layout of DdpRec) -> Fx [B, N, N], Fu [B, N, M].
+template <int NJ>
+__global__ void k_jac_extract(const double* __restrict__ ws, int B, double* __restrict__ Fx, double* __restrict__ Fu) {
+  using RC = DdpRec<NJ>;
+  constexpr int N = RC::N, M = RC::M;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= B * (N * N + N * M)) return;
+  const int b = k % B, r = k / B;
+  const double v = ws[(size_t)(RC::A + r) * B + b];
+  if (r < N * N)
+    Fx[(size_t)b * N * N + r] = v;
+  else
+    Fu[(size_t)b * N * M + (r - N * N)] = v;
 }
 
 // The fused pass for the closed-form systems (SI, car, DI): one thread per episode computes each
@@ -842,7 +868,25 @@ struct LaunchJac {
         set_error("cacto_env_jacobians: 2-joint chains are instantiated for the prismatic pair (double integrator)");
         return CACTO_EUNSUPPORTED;
       }
-      hipLaunchKernelGGL(k_env_jacobians<NJ>, dim3(ceil_div(B, 64)), dim3(64), 0, st, sys->dev, S, U, B, Fx, Fu);
+      if constexpr (NJ > 2) {
+        using RC = DdpRec<NJ>;
+        constexpr int ns = Dims<NJ>::NS;
+        const size_t rec = (size_t)2 * RC::R * B, s2 = (size_t)2 * B * ns;
+        double* ws = nullptr;
+        const int rc = ddp_workspace(const_cast<cacto_sys*>(sys), (rec + s2 + B) * sizeof(double), &ws);
+        if (rc != CACTO_OK) return rc;
+        double* S2 = ws + rec;
+        int32_t* n1 = reinterpret_cast<int32_t*>(S2 + s2);
+        hipLaunchKernelGGL(k_jac_prep<NJ>, dim3(ceil_div(B * 2 * ns, 256)), dim3(256), 0, st, S, B, S2, n1);
+        CACTO_CHECK_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_ddp_derivs<NJ>, dim3(ceil_div(B, 64), 2), dim3(64), 0, st, sys->dev, S2, (int64_t)2, U,
+                           (int64_t)1, n1, B, ws);
+        CACTO_CHECK_HIP(hipGetLastError());
+        constexpr int per = RC::N * RC::N + RC::N * RC::M;
+        hipLaunchKernelGGL(k_jac_extract<NJ>, dim3(ceil_div(B * per, 256)), dim3(256), 0, st, ws, B, Fx, Fu);
+      } else {
+        hipLaunchKernelGGL(k_env_jacobians<NJ>, dim3(ceil_div(B, 64)), dim3(64), 0, st, sys->dev, S, U, B, Fx, Fu);
+      }
       CACTO_CHECK_HIP(hipGetLastError());
       return CACTO_OK;
     }

@@ -1,0 +1,186 @@
+"""The HIP data-parallel update on the GPU (the ordering it keeps is RL.py:104-109):
+two spawned ranks, both on cuda:0, exchanging over gloo (the driver's multi-GPU runs use RCCL, one
+rank per GPU; the exchange code path — RL_AC.set_data_parallel + update_rows, the all-reduce of
+the critic gradient before its Adam step and of the actor gradient after it — is the same).
+
+  * RL_AC.update_rows with set_data_parallel(2), each rank on its half of the global minibatch,
+    equals a single-rank update_rows at the global batch (the split only reassociates the sum over
+    samples: float32 rounding of the gradient, so weights within Adam's 5e-6/step), and the two
+    replicas end bit-identical.
+  * PrioritizedReplayBuffer.sample_device with two replay shards: indices bit-exact against the
+    oracle's per-shard sampler, IS weights against oracle.sample_weights_global over the union of
+    the shards (the all-gathered (sum, min, rows) of both ranks).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+K, B_LOCAL, WORLD = 4, 64, 2
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rows(n, seed):
+    from cacto_amd.confs import load_conf
+    conf = load_conf("double_integrator")
+    rng = np.random.default_rng(seed)
+    ns = conf.nb_state
+    S = np.column_stack([rng.uniform(-15, 15, (n, ns - 1)), rng.uniform(0, 9.9, n)])
+    Sn = np.column_stack([rng.uniform(-15, 15, (n, ns - 1)), rng.uniform(0, 9.9, n)])
+    return np.concatenate([S, rng.normal(size=(n, 1)) * 0.5, Sn, rng.normal(size=(n, ns)) * 0.3,
+                           (rng.uniform(size=(n, 1)) < 0.3).astype(float),
+                           (rng.uniform(size=(n, 1)) < 0.2).astype(float)], axis=1)
+
+
+def _learner(world):
+    from conftest import load_weights
+    from cacto_amd.confs import load_conf
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.rl import RL_AC
+    conf = load_conf("double_integrator")
+    env = make_env(conf)
+    rl = RL_AC(env, NN(env, conf, w_S=1e-2, seed=3), conf)
+    rl.setup_model(weights=load_weights("di_seed0_0"))
+    if world > 1:
+        rl.set_data_parallel(world)
+    return rl
+
+
+def _state(rl):
+    return [t.cpu().numpy().copy() for t in (rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf,
+                                             rl.actor_m, rl.actor_v, rl.critic_m, rl.critic_v)]
+
+
+def _init(rank, port):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=WORLD)
+    return dist
+
+
+def _update_worker(rank, port, rows, idx, q):
+    dist = _init(rank, port)
+    try:
+        rl = _learner(WORLD)
+        storage = torch.as_tensor(rows, device="cuda")
+        for k in range(K):
+            loc = idx[k, rank * B_LOCAL:(rank + 1) * B_LOCAL].astype(np.int32)
+            rl.update_rows(storage, torch.as_tensor(loc, device="cuda"))
+        torch.cuda.synchronize()
+        q.put((rank, _state(rl), rl.steps.cpu().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _per_worker(rank, port, q):
+    dist = _init(rank, port)
+    try:
+        from cacto_amd.confs import load_conf
+        from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+        conf = load_conf("double_integrator", fresh=True)
+        conf.prioritized_replay_alpha = 0.6
+        conf.BATCH_SIZE = B_LOCAL
+        buf = PrioritizedReplayBuffer(conf)
+        buf.set_data_parallel(WORLD)
+        n_rows, leaves, u = _per_shard(rank)
+        buf.add_rows(_rows(n_rows, 50 + rank))
+        buf.set_leaves(np.arange(n_rows), leaves)
+        idx, w = buf.sample_device(torch.as_tensor(u, device="cuda"))
+        torch.cuda.synchronize()
+        q.put((rank, idx.cpu().numpy(), w.cpu().numpy(), buf.exp_counter[:n_rows].cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _per_shard(rank):
+    rng = np.random.default_rng(200 + rank)
+    n_rows = 700 + 500 * rank                                # shards of different fill
+    return n_rows, rng.uniform(0.05, 3.0, size=n_rows) ** 0.6, rng.uniform(size=B_LOCAL)
+
+
+def _spawn(target, args_of_rank):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, port) + args_of_rank(r) + (q,)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        res = {}
+        for _ in procs:
+            item = q.get(timeout=240)
+            res[item[0]] = item[1:]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    return res
+
+
+def test_dp_update_on_gpu_equals_single_rank():
+    rng = np.random.default_rng(61)
+    N = 4096
+    rows = _rows(N, 60)
+    idx = rng.integers(0, N, size=(K, WORLD * B_LOCAL))
+    res = _spawn(_update_worker, lambda r: (rows, idx))
+    s0, s1 = res[0][0], res[1][0]
+    for a, b in zip(s0, s1):
+        assert np.array_equal(a, b)                          # replicas stay bit-identical
+    assert res[0][1] == [K, K]
+    single = _learner(1)
+    storage = torch.as_tensor(rows, device="cuda")
+    for k in range(K):
+        single.update_rows(storage, torch.as_tensor(idx[k].astype(np.int32), device="cuda"))
+    torch.cuda.synchronize()
+    ref = _state(single)
+    for name, a, b in zip(("actor", "critic", "target"), s0[:3], ref[:3]):
+        P = single.actor_model.P if name == "actor" else single.critic_model.P
+        err = np.abs(a[:P] - b[:P]).max()
+        assert err < 5e-6 * K, (name, err)
+    # the exchange mattered: a rank's update on its half alone is measurably different
+    alone = _learner(1)
+    for k in range(K):
+        alone.update_rows(storage, torch.as_tensor(idx[k, :B_LOCAL].astype(np.int32), device="cuda"))
+    P = alone.critic_model.P
+    assert np.abs(alone.critic_model.buf.cpu().numpy()[:P] - s0[1][:P]).max() > 20 * 5e-6 * K
+
+
+def test_dp_per_shards_on_gpu_match_oracle():
+    from oracle import buffer as obuf
+    res = _spawn(_per_worker, lambda r: ())
+    shards = []
+    for r in range(WORLD):
+        n_rows, leaves, u = _per_shard(r)
+        o = obuf.PrioritizedReplayBuffer(65536, 5, 0.6, 0.6, 1e-2, 0.95, B_LOCAL)
+        for i, v in enumerate(leaves):
+            o.it_sum[i] = float(v)
+            o.it_min[i] = float(v)
+        o.next_idx = n_rows
+        shards.append((o, u))
+    stats = np.stack([o.shard_stats() for o, _ in shards])
+    for r, (o, u) in enumerate(shards):
+        idx, w, cnt = res[r]
+        oidx = o.sample_proportional(u)
+        np.testing.assert_array_equal(idx, oidx)
+        ow = o.sample_weights_global(oidx, stats)
+        np.testing.assert_allclose(w, ow.astype(np.float32), rtol=1e-6)
+        np.testing.assert_array_equal(cnt, o.exp_counter[:len(cnt)])

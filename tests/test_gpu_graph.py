@@ -31,7 +31,7 @@ def _state(rl):
 
 
 def test_graph_replay_equals_eager_updates():
-    conf = load_conf("double_integrator")
+    conf = load_conf("double_integrator", fresh=True)
     env = make_env(conf)
     ns = conf.nb_state
     rng = np.random.default_rng(5)
@@ -61,7 +61,7 @@ def test_graph_replay_equals_eager_updates_with_per():
     """learn_and_update with PER (RL.py:122-137): sample -> update -> priority update, replayed as one
     graph, leaves the weights, the sum / min trees and the experience counters as the eager loop."""
     from cacto_amd.replay_buffer import PrioritizedReplayBuffer
-    conf = load_conf("double_integrator")
+    conf = load_conf("double_integrator", fresh=True)
     conf.prioritized_replay_alpha = 0.6
     env = make_env(conf)
     ns = conf.nb_state
@@ -102,7 +102,7 @@ def test_pipelined_updates_equal_sequential(system, B, K, MC):
     """cacto_update_n overlaps critic(t+1) with actor(t) on two streams; the result is the same bits.
     Odd K ends with the critic in the workspace copy (copied back), even K in the caller's buffer;
     K = 1, 2 finish before the first two-updates-old wait; MC = 1 has no soft target update."""
-    conf = load_conf(system)
+    conf = load_conf(system, fresh=True)
     conf.MC = MC
     env = make_env(conf)
     ns = conf.nb_state
@@ -134,7 +134,7 @@ def test_pipelined_per_updates_equal_sequential():
     """cacto_update_n_per: sample -> update -> priority update per step, pipelined, equals the
     sequential PER loop bit for bit (weights, moments, counters, trees, experience counters)."""
     from cacto_amd.replay_buffer import PrioritizedReplayBuffer
-    conf = load_conf("car_park")
+    conf = load_conf("car_park", fresh=True)
     conf.prioritized_replay_alpha = 0.6
     env = make_env(conf)
     ns = conf.nb_state

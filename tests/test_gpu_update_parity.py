@@ -156,7 +156,7 @@ def test_per_loop_car_park_matches_oracle():
     sample -> IS-weighted update -> priority update -> target update loop. Indices are compared
     through exp_counter (incremented once per distinct sampled index), leaves to f32 rounding."""
     from cacto_amd.replay_buffer import PrioritizedReplayBuffer
-    conf, env, oe, rl = _setup("car_park", None, 0.0)
+    conf, env, oe, rl = _setup("car_park", None, 0.0, conf=load_conf("car_park", fresh=True))
     conf.prioritized_replay_alpha = 0.6            # bench/BASELINE build choice (reference ships 0)
     per = PrioritizedReplayBuffer(conf, rl.sys)
     o = obuf.PrioritizedReplayBuffer(conf.REPLAY_SIZE, conf.nb_state, 0.6, conf.prioritized_replay_beta,
@@ -177,11 +177,14 @@ def test_per_loop_car_park_matches_oracle():
         o.update_priorities(idx, y.astype(np.float32), V.astype(np.float32))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(per.exp_counter[:n_rows].cpu().numpy(), o.exp_counter[:n_rows])
+    # leaves (|y - V| + eps)^alpha: y and V are float32 network values (abs error ~F32_TOL x their
+    # scale, ~1e-5 here), and d leaf / d|y - V| <= alpha * eps^(alpha - 1) = 3.8, so leaves agree to
+    # an absolute 1e-4 (relative only where |y - V| is not itself at rounding level)
     cap = per.cap
     st = per.sum_tree.cpu().numpy()
-    np.testing.assert_allclose(st[cap:cap + n_rows], o.it_sum.value[cap:cap + n_rows], rtol=2e-5)
-    np.testing.assert_allclose(per.min_tree.cpu().numpy()[1], o.it_min.value[1], rtol=2e-5)
-    np.testing.assert_allclose(float(per.max_priority.item()), o.max_priority, rtol=2e-5)
+    np.testing.assert_allclose(st[cap:cap + n_rows], o.it_sum.value[cap:cap + n_rows], rtol=2e-5, atol=1e-4)
+    np.testing.assert_allclose(per.min_tree.cpu().numpy()[1], o.it_min.value[1], rtol=2e-5, atol=1e-4)
+    np.testing.assert_allclose(float(per.max_priority.item()), o.max_priority, rtol=2e-5, atol=1e-4)
     assert rl.steps.cpu().tolist() == [K, K]
     _assert_weights(rl, nets, K)
 
@@ -215,7 +218,7 @@ def test_manipulator_lr_schedule_crosses_boundary():
     assert rl.steps.cpu().tolist() == [start + K, start + K]
     _assert_weights(rl, nets, K)
     # without the schedule the result is measurably different (the halved steps matter)
-    conf_flat = load_conf("manipulator")
+    conf_flat = load_conf("manipulator", fresh=True)
     conf_flat.LR_SCHEDULE = 0
     _, _, _, rl2 = _setup("manipulator", None, 0.0, conf=conf_flat)
     rl2.steps.fill_(start)

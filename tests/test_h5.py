@@ -125,7 +125,7 @@ def test_rl_save_and_recover_h5(tmp_path):
     from cacto_amd.environment import make_env
     from cacto_amd.neural_network import NN
     from cacto_amd.rl import RL_AC
-    conf = load_conf("double_integrator")
+    conf = load_conf("double_integrator", fresh=True)
     env = make_env(conf)
     z = np.load(os.path.join(GOLD, "di_seed0_final.npz"))
     w = {k: [z["%s_%d" % (k, i)] for i in range(6 if k == "actor" else 10)] for k in ("actor", "critic", "target")}
