@@ -45,11 +45,11 @@ def fc_flops(ns):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--system", default="double_integrator")
     p.add_argument("--rollouts", type=int, default=4096)
-    p.add_argument("--update-steps", type=int, default=200)
+    p.add_argument("--update-steps", type=int, default=1000)
     p.add_argument("--batches", default="128,4096")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -57,6 +57,8 @@ def parse():
                    help="replay the update loop as one HIP graph (RL_AC.capture_updates) instead of launching "
                         "it eagerly; measured equal on MI355X (the update is bound by its kernels, not launches)")
     p.add_argument("--extra-systems", default="manipulator,car_park,ur5")
+    p.add_argument("--no-config0", action="store_true",
+                   help="skip BASELINE configs[0] (single integrator, one main.py training iteration, GPU vs CPU)")
     p.add_argument("--no-diagnostics", action="store_true",
                    help="skip the rollout variants (profiling runs: every k_rollout dispatch is a full rollout)")
     return p.parse_args()
@@ -201,9 +203,28 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     kern_ms = sum(e[0].elapsed_time(e[2]) for e in evs) / K
     seq_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / K
     steps_per_call = int(nsteps.sum())
+    # the timed region in 5 consecutive segments (HIP events at their boundaries): per-segment rate
+    # and the median of the 5, beside the whole-region value
+    seg = segments([(e[0], e[2]) for e in evs], steps_per_call)
     return dict(out=out, S0=S0, nsteps=nsteps, T=T, wall=wall, kernel_ms=kern_ms, seq_kernel_ms=seq_ms,
+                seq_kernel_ms_median=float(np.median([e[0].elapsed_time(e[1]) for e in evs])),
                 rewards_kernel_ms=kern_ms - seq_ms, steps_per_call=steps_per_call,
-                total_steps=sum_over_ranks(steps_per_call * K, world))
+                total_steps=sum_over_ranks(steps_per_call * K, world), segments=seg)
+
+
+def segments(pairs, units_per_item, n=5):
+    """Split K timed items (each a (start, end) HIP-event pair, back to back on one stream) into n
+    consecutive segments: units/s of each segment (start of its first item -> end of its last)."""
+    K = len(pairs)
+    if K < n:
+        return None
+    rates = []
+    for j in range(n):
+        lo, hi = j * K // n, (j + 1) * K // n
+        ms = pairs[lo][0].elapsed_time(pairs[hi - 1][1])
+        rates.append(units_per_item * (hi - lo) / (ms * 1e-3))
+    return dict(n=n, items_per_segment=K // n, rates=rates, median=float(np.median(rates)),
+                spread=float((max(rates) - min(rates)) / np.median(rates)))
 
 
 def rollout_diagnostics(rl, conf, roll, K=5):
@@ -333,18 +354,31 @@ def update_phase(rl, buf, B, K, W, world, seed):
         for i in range(W):
             rl.update_rows(buf.storage, idx[i])
     graph = rl.capture_updates(buf.storage, idx[W:]) if world == 1 and USE_GRAPH else None
+    cuts = [W + j * K // 5 for j in range(6)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev[0].record()
     if graph is not None:
         graph.replay()
     else:
-        rl.update_rows_n(buf.storage, idx[W:])      # K updates, critic(t+1) overlapping actor(t)
+        # K updates, critic(t+1) overlapping actor(t), as 5 consecutive calls (segments for the median)
+        for j in range(5):
+            rl.update_rows_n(buf.storage, idx[cuts[j]:cuts[j + 1]])
+            ev[j + 1].record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
-    return wall
+    seg = None if graph is not None else update_segments(ev, cuts)
+    return wall, seg
+
+
+def update_segments(ev, cuts):
+    rates = [(cuts[j + 1] - cuts[j]) / (ev[j].elapsed_time(ev[j + 1]) * 1e-3) for j in range(5)]
+    return dict(n=5, rates=rates, median=float(np.median(rates)),
+                spread=float((max(rates) - min(rates)) / np.median(rates)))
 
 
 # BASELINE.json configs[2..4] (per GPU): rollouts, minibatches, Sobolev weight, PER.
@@ -378,20 +412,27 @@ def per_update_phase(rl, buf, B, K, W, world, seed):
         for i in range(W):
             step(i)
     graph = rl.capture_updates(None, None, per_buffer=buf, uniforms=U[W:]) if world == 1 and USE_GRAPH else None
+    cuts = [W + j * K // 5 for j in range(6)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev[0].record()
     if graph is not None:
         graph.replay()
-    elif pipelined:
-        rl.update_rows_n_per(buf, U[W:])        # K updates: sample -> update -> priorities, pipelined
     else:
-        for i in range(K):
-            step(W + i)
+        for j in range(5):
+            if pipelined:
+                rl.update_rows_n_per(buf, U[cuts[j]:cuts[j + 1]])   # sample -> update -> priorities, pipelined
+            else:
+                for i in range(cuts[j], cuts[j + 1]):
+                    step(i)
+            ev[j + 1].record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
-    return max_over_ranks(t1 - t0, world)
+    seg = None if graph is not None else update_segments(ev, cuts)
+    return max_over_ranks(t1 - t0, world), seg
 
 
 def extra_system(name, args, world, rank):
@@ -407,16 +448,22 @@ def extra_system(name, args, world, rank):
     if cfg["per"] and world > 1:
         buf.set_data_parallel(world)        # IS weights over the union of the ranks' shards
     ups = {}
+    ns, na = conf.nb_state, conf.nb_action
     for B in cfg["batches"]:
         if cfg["per"]:
             conf.BATCH_SIZE = B
-            wall = per_update_phase(rl, buf, B, args.update_steps, 3, world, seed=300 + rank)
+            wall, seg = per_update_phase(rl, buf, B, args.update_steps, 3, world, seed=300 + rank)
         else:
-            wall = update_phase(rl, buf, B, args.update_steps, 3, world, seed=200 + rank)
+            wall, seg = update_phase(rl, buf, B, args.update_steps, 3, world, seed=200 + rank)
+        flop = B * world * ((9 if cfg["w_S"] else 6) * fc_flops(ns) + 3 * fa_flops(ns, na))
         ups["B=%d" % B] = dict(value=args.update_steps / wall, unit="critic-updates/s", global_batch=B * world,
-                               ms_per_update=1e3 * wall / args.update_steps)
+                               ms_per_update=1e3 * wall / args.update_steps, segments=seg,
+                               tflops=flop * args.update_steps / wall / 1e12,
+                               mfma_frac=flop * args.update_steps / wall / (FP32_MFMA_PEAK * world))
     return dict(config=cfg["config"], env_steps_per_s=r["total_steps"] / r["wall"], rollouts_per_gpu=cfg["R"],
-                rollout_kernel_ms=r["kernel_ms"], env_steps_per_launch=r["steps_per_call"],
+                rollout_kernel_ms=r["kernel_ms"], env_steps_per_launch=r["steps_per_call"], segments=r["segments"],
+                rollout_mfma_frac=r["steps_per_call"] * fa_flops(ns, na) / (r["seq_kernel_ms"] * 1e-3) /
+                FP32_MFMA_PEAK,
                 w_S=cfg["w_S"], per=cfg["per"], critic_updates=ups, ddp_labels=ddp)
 
 
@@ -490,6 +537,80 @@ def cpu_baseline_update(conf, rl, buf, B, seconds):
                 sample="%d updates at B=%d in %.1f s (oracle/nn.py, numpy float64)" % (n, B, dt))
 
 
+def host_info():
+    """The host the CPU baselines ran on: CPU model, the cores this process may use, BLAS threads."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    blas = None
+    try:
+        from threadpoolctl import threadpool_info
+        blas = [dict(api=i.get("internal_api"), threads=i.get("num_threads")) for i in threadpool_info()]
+    except Exception:
+        pass
+    return dict(cpu_model=model, cores_available=len(os.sched_getaffinity(0)), blas=blas,
+                omp_num_threads=os.environ.get("OMP_NUM_THREADS"))
+
+
+def config0(args, rank, cpu_updates):
+    """BASELINE configs[0]: single_integrator, seed 0, w_S = 0 — one main.py training iteration
+    (main.py:216-243, ep = 0: EP_UPDATE = 200 episodes with zero warm-start controls, RL_Solve,
+    buffer.add, learn_and_update of UPDATE_LOOPS[0] = 1000 updates at B = 128), from the reference's
+    SI seed-0 initial weights. GPU: the package's path (one rollout launch, device labels and
+    RL_Solve + ring add, pipelined update loop), timed whole. CPU (rank 0): oracle/cpu_ref.py with
+    Pool(2) as main.py:219-225 runs it — episodes in full, `cpu_updates` updates measured and
+    projected to 1000. TO_Solve (CasADi) is absent on both sides: the warm start stands in for it."""
+    from cacto_amd.confs import load_conf
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.replay_buffer import ReplayBuffer
+    from cacto_amd.rl import RL_AC
+    conf = load_conf("single_integrator", fresh=True)
+    conf.NNs_path = None
+    env = make_env(conf)
+    rl = RL_AC(env, NN(env, conf, w_S=0.0), conf)
+    z = np.load(os.path.join(ROOT, "tests", "golden", "weights", "si_seed0_0.npz"))
+    w = {k: [z["%s_%d" % (k, i)] for i in range(6 if k == "actor" else 10)] for k in ("actor", "critic")}
+    res = {}
+    for rep in range(2):            # the first pass warms the kernels / allocations up
+        rl.setup_model(weights=w)
+        random.seed(0)
+        np.random.seed(0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        S0 = np.array([env.reset() for _ in range(conf.EP_UPDATE)])
+        n = np.array([conf.NSTEPS - int(s[-1] / conf.dt) for s in S0])
+        keep = n > 0
+        S0, n = S0[keep], n[keep]
+        T = int(n.max())
+        out = rl.rollout_batch(S0, n, T, ep=0, weights=conf.cost_weights_running)
+        roll = dict(out=out, nsteps=n)
+        R_term = terminal_rewards(env, conf, roll)
+        buf = ReplayBuffer(conf)
+        buf.add_episodes(out["S"], out["R"], n, R_term=R_term)      # w_S = 0: no labels needed
+        counter = rl.learn_and_update(0, buf, 0)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        res = dict(iteration_s=t1 - t0, episodes=int(len(n)), env_steps=int(n.sum()), updates=int(counter),
+                   batch=conf.BATCH_SIZE)
+    out = {"config": "configs[0]: single_integrator, seed 0, w-S 0, nb-cpus 2 — one main.py iteration "
+                     "(200 episodes + 1000 updates at B=128)", "gpu": res}
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle import cpu_ref
+        c = cpu_ref.training_iteration("single_integrator", w, seed=0, nb_cpus=2, ep=0, update_sample=cpu_updates)
+        c.update(kind="port", cores=2, sample="episodes in full on Pool(2); %d of the %d updates measured, "
+                                               "projected" % (c["updates_measured"], c["update_loops"]))
+        out["cpu"] = c
+        out["speedup_vs_cpu"] = c["projected_iteration_s"] / res["iteration_s"]
+    return out
+
+
 USE_GRAPH = False
 
 
@@ -514,11 +635,11 @@ def main():
     updates = {}
     for B in [int(b) for b in args.batches.split(",") if b]:
         K = args.update_steps
-        wall = update_phase(rl, buf, B, K, max(3, args.warmup), world, seed=100 + rank)
+        wall, seg = update_phase(rl, buf, B, K, max(3, args.warmup), world, seed=100 + rank)
         flop = B * world * (9 * fc_flops(ns) + 3 * fa_flops(ns, na))
         updates["B=%d" % B] = dict(value=K / wall, unit="critic-updates/s", global_batch=B * world,
                                    ms_per_update=1e3 * wall / K, tflops=flop * K / wall / 1e12,
-                                   mfma_frac=flop * K / wall / (FP32_MFMA_PEAK * world))
+                                   mfma_frac=flop * K / wall / (FP32_MFMA_PEAK * world), segments=seg)
     extra = {}
     for sysname in [s for s in args.extra_systems.split(",") if s and s != args.system]:
         extra[sysname] = extra_system(sysname, args, world, rank)
@@ -528,6 +649,9 @@ def main():
         cpu["update"] = cpu_baseline_update(conf, rl, buf, 128, args.cpu_seconds / 2)
         if args.system == "double_integrator":
             cpu["vectorized"] = cpu_baseline_rollout_vectorized(conf, rl, roll, args.cpu_seconds / 2)
+    c0 = None if args.no_config0 else config0(args, rank, max(20, int(args.cpu_seconds * 20)))
+    if cpu is not None:
+        cpu["host"] = host_info()
     traffic, traffic_src = pmc_traffic()
     if rank == 0:
         line = {
@@ -549,6 +673,7 @@ def main():
                        "system": args.system, "rollouts_per_gpu": args.rollouts,
                        "env_steps_per_rollout_batch": roll["steps_per_call"], "T_max": roll["T"],
                        "parallelism": "dp%d" % world},
+            "segments": roll["segments"],
             "roofline": {"kernel": "k_rollout", "bound": "mfma", "achieved": achieved / 1e12,
                          "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
@@ -561,6 +686,7 @@ def main():
             "rollout_diagnostics": diag,
             "cpu_baseline": cpu,
             "extra_systems": extra,
+            "config0": c0,
         }
         print(json.dumps(line))
     if world > 1:

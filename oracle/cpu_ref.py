@@ -1,0 +1,94 @@
+"""Oracle: one main.py training iteration on the host CPU (test infrastructure / CPU baseline only —
+see oracle/__init__). BASELINE.json configs[0]: single_integrator, seed 0, w_S = 0, nb_cpus = 2.
+
+Restates main.py:216-243 for one `ep`:
+  * EP_UPDATE initial states (Env.reset, environment.py:46-55) from `random.seed(seed)`;
+  * compute_sample per state in a `multiprocessing.Pool(nb_cpus)` (main.py:219-225): the
+    create_TO_init warm-start rollout (RL.py:197-233, `oracle.rollout.to_init_rollout`) and
+    RL_Solve's n-step targets (RL.py:145-189, `oracle.buffer.rl_solve`); TO_Solve (CasADi + ipopt)
+    is absent, so the warm start stands in for the TO solution and the step cost is -reward of it
+    (Env.step, environment.py:70-78);
+  * buffer.add of the episodes (main.py:240; oracle.buffer.ReplayBuffer);
+  * learn_and_update: UPDATE_LOOPS[ep] updates at BATCH_SIZE (RL.py:120-143; oracle.nn, float64).
+`bench.py` times the episodes in full and a bounded number of updates (projected to
+UPDATE_LOOPS[ep]) so the default bench stays within minutes.
+"""
+import random
+import time
+
+import numpy as np
+
+from . import buffer as obuf
+from . import env as oenv
+from . import nn as onn
+from . import rollout as oroll
+
+
+def _sample(args):
+    """main.py:174-195 compute_sample (warm start in place of TO_Solve)."""
+    conf_name, actor, s0, ep = args
+    from cacto_amd.confs import load_conf
+    conf = load_conf(conf_name)
+    oe = oenv.make_env(conf)
+    r = oroll.to_init_rollout(oe, actor, s0, ep)
+    if r is None:
+        return None
+    S, U, T = r
+    w_run, w_term = conf.cost_weights_running, conf.cost_weights_terminal
+    cost = np.empty(T + 1)
+    for i in range(T):
+        cost[i] = -oe.reward(w_run, S[i], U[i])
+    cost[T] = -oe.reward(w_term, S[T])
+    partial, total, s_next, done, term = obuf.rl_solve(S, cost, conf.nsteps_TD_N, MC=bool(conf.MC))
+    dVdx = np.zeros_like(S)                   # w_S = 0: the labels never enter the loss
+    return S, partial, s_next, dVdx, done, term
+
+
+def _warm(i):
+    from cacto_amd.confs import load_conf  # noqa: F401
+    return i
+
+
+def training_iteration(conf_name, weights, seed=0, nb_cpus=2, ep=0, update_sample=None, w_S=0.0):
+    """Returns a dict of timings: episodes (pool), buffer add, updates (measured count) and the
+    projection of the iteration's UPDATE_LOOPS[ep] updates."""
+    from multiprocessing import get_context
+    from cacto_amd.confs import load_conf
+    conf = load_conf(conf_name)
+    oe = oenv.make_env(conf)
+    rng = random.Random(seed)
+    ics = [oe.reset(rng) for _ in range(conf.EP_UPDATE)]
+    with get_context("spawn").Pool(nb_cpus) as pool:
+        t_s = time.perf_counter()
+        pool.map(_warm, range(nb_cpus))          # worker start-up (spawn + imports) kept out
+        t0 = time.perf_counter()
+        tmp = pool.map(_sample, [(conf_name, weights["actor"], s, ep) for s in ics])
+        t1 = time.perf_counter()
+    t_pool = t0 - t_s
+    tmp = [x for x in tmp if x is not None]
+    buf = obuf.ReplayBuffer(conf.REPLAY_SIZE, conf.nb_state)
+    buf.add_rows(buf.concatenate(*zip(*tmp)))
+    t2 = time.perf_counter()
+    n_up = int(conf.UPDATE_LOOPS[ep])
+    n_meas = n_up if update_sample is None else min(update_sample, n_up)
+    crit, tgt, act = weights["critic"], weights.get("target", weights["critic"]), weights["actor"]
+    oc, oa = onn.KerasAdam(conf.CRITIC_LEARNING_RATE), onn.KerasAdam(conf.ACTOR_LEARNING_RATE)
+    norm = conf.state_norm_arr.astype(np.float64)
+    ns, B = conf.nb_state, conf.BATCH_SIZE
+    nrng = np.random.RandomState(seed)
+    for _ in range(n_meas):
+        idx = nrng.randint(0, buf.max_idx(), size=B)
+        r = buf.storage[idx].astype(np.float32).astype(np.float64)
+        gc = onn.compute_critic_grad(crit, tgt, r[:, :ns], r[:, ns + 1:2 * ns + 1], r[:, ns:ns + 1],
+                                     r[:, 2 * ns + 1:3 * ns + 1], r[:, 3 * ns + 1:3 * ns + 2], np.ones((B, 1)), w_S,
+                                     norm)[0]
+        crit = oc.apply(crit, gc)
+        ga = onn.compute_actor_grad(oe, act, crit, r[:, :ns].astype(np.float32), buf.storage[idx, 3 * ns + 2:], norm)
+        act = oa.apply(act, ga)
+        tgt = onn.soft_update(tgt, crit, conf.UPDATE_RATE)
+    t3 = time.perf_counter()
+    per_update = (t3 - t2) / max(n_meas, 1)
+    return dict(episodes=len(tmp), env_steps=int(sum(len(x[0]) - 1 for x in tmp)), pool_start_s=t_pool,
+                episodes_s=t1 - t0, buffer_add_s=t2 - t1, updates_measured=n_meas, updates_s=t3 - t2,
+                update_loops=n_up, ms_per_update=1e3 * per_update,
+                projected_iteration_s=(t2 - t0) + per_update * n_up)
