@@ -642,6 +642,183 @@ __global__ void __launch_bounds__(256) k_reduce(const float* __restrict__ slab, 
   }
 }
 
+// ---------------------------------------------------------------- fused weight gradient + Adam (small batches)
+// For batches whose weight-gradient rows fit 64-row chunks (rows <= 1024), k_wgrad + k_adam run as
+// one launch: one wave per 16 x 16 weight tile or 16-wide bias tile of a layer, over ALL rows,
+// then the Adam step (+ packed refresh, + soft update) on the tile's parameters straight from the
+// accumulators. No slab round trip and one launch instead of two. The sums are formed in exactly
+// the order of k_wgrad (per chunk: the four 16-row wave spans, each a 4-MFMA chain from zero,
+// reduced ((p0 + p1) + p2) + p3; bias: 64-row groups, then shuffles over g) followed by k_adam's
+// chunk order, so results are bit-identical to the split path.
+struct AdamNet {
+  WgArgs wg;  // panels, rows, 64-row chunking (as k_wgrad)
+  NetTopo t;
+  const float* src;  // weights the step starts from (== nb for an in-place step)
+  float* nb;
+  float4* pk;
+  float* m;
+  float* v;
+  float* target;  // soft update (critic) or nullptr
+  float4* tpk;
+  AdamArgs ad;
+  int items;                    // weight tiles + bias tiles, all layers
+  int ioff[MAX_LAYERS + 1];     // first item of layer l: KT*OT weight tiles then OT bias tiles
+};
+
+struct AdamScalars {
+  float alpha, c1, c2, eps, tau, omt;
+};
+
+__device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int32_t* step) {
+  const int it = step[a.which];  // = Keras iterations + 1
+  const int iters = it - 1;
+  double lr = a.lr[4];
+  for (int k = 0; k < 4; ++k)
+    if ((double)iters <= a.bounds[k]) {
+      lr = a.lr[k];
+      break;
+    }
+  const float tf = (float)it;
+  const float b1p = powf((float)a.beta1, tf), b2p = powf((float)a.beta2, tf);
+  AdamScalars s;
+  s.alpha = fdiv(fmul((float)lr, __fsqrt_rn(fsub(1.f, b2p))), fsub(1.f, b1p));
+  s.c1 = (float)(1.0 - a.beta1);
+  s.c2 = (float)(1.0 - a.beta2);
+  s.eps = (float)a.eps;
+  s.tau = (float)a.tau;
+  s.omt = (float)(1.0 - a.tau);
+  return s;
+}
+
+// k_adam's per-parameter arithmetic (same ops, same order)
+__device__ __forceinline__ void adam_apply(const AdamNet& N, const AdamScalars& s, int p, float g, float mm, float vv,
+                                           float th0, float tg0) {
+  mm = fadd(mm, fmul(fsub(g, mm), s.c1));
+  vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
+  const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
+  N.m[p] = mm;
+  N.v[p] = vv;
+  N.nb[p] = th;
+  write_packed(N.pk, N.t, p, th);
+  if (N.target) {
+    const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
+    N.target[p] = tg;
+    write_packed(N.tpk, N.t, p, tg);
+  }
+}
+
+__device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, const int32_t* __restrict__ step,
+                                                int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  int l = 0;
+  while (item >= N.ioff[l + 1]) ++l;
+  const int rem = item - N.ioff[l];
+  const WgLayer& Ly = N.wg.l[l];
+  const WgArgs& a = N.wg;
+  const AdamScalars s = adam_scalars(N.ad, step);
+  if (rem < Ly.IT * Ly.OT) {
+    const int it = rem / Ly.OT, ot = rem - it * Ly.OT;
+    const int oc = 16 * ot + c;
+    // Adam operands of the lane's 4 parameters, in flight during the GEMM
+    int p[4];
+    float mm[4], vv[4], th[4], tg[4];
+    bool ok[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ii = 16 * it + 4 * g + q;
+      ok[q] = ii < Ly.in && oc < Ly.out;
+      p[q] = ok[q] ? Ly.woff + ii * Ly.out + oc : 0;
+      mm[q] = N.m[p[q]];
+      vv[q] = N.v[p[q]];
+      th[q] = N.src[p[q]];
+      tg[q] = N.target ? N.target[p[q]] : 0.f;
+    }
+    const float* ap = Ly.LT + (size_t)(16 * it + c) * a.ld + 4 * g;
+    const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
+    floatx4 gs = {0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < a.nch; ++ch) {
+      const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+      float4 A[4], Bv[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int r = min(lo + 16 * w, hi - 16);  // clamped (branch-free); unused past hi
+        A[w] = *reinterpret_cast<const float4*>(ap + r);
+        Bv[w] = *reinterpret_cast<const float4*>(bp + r);
+      }
+      floatx4 part[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (lo + 16 * w < hi) {
+          acc = mfma4(A[w].x, Bv[w].x, acc);
+          acc = mfma4(A[w].y, Bv[w].y, acc);
+          acc = mfma4(A[w].z, Bv[w].z, acc);
+          acc = mfma4(A[w].w, Bv[w].w, acc);
+        }
+        part[w] = acc;
+      }
+      floatx4 s4 = part[0];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        s4[0] += part[w][0];
+        s4[1] += part[w][1];
+        s4[2] += part[w][2];
+        s4[3] += part[w][3];
+      }
+      if (ch == 0) {
+        gs = s4;
+      } else {
+        gs[0] += s4[0];
+        gs[1] += s4[1];
+        gs[2] += s4[2];
+        gs[3] += s4[3];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (ok[q]) adam_apply(N, s, p[q], gs[q], mm[q], vv[q], th[q], tg[q]);
+  } else {
+    const int ot = rem - Ly.IT * Ly.OT;
+    const int oc = 16 * ot + c;
+    const bool ok = g == 0 && oc < Ly.out;
+    const int pp = ok ? Ly.boff + oc : 0;
+    const float mm = N.m[pp], vv = N.v[pp], th = N.src[pp], tg = N.target ? N.target[pp] : 0.f;
+    const float* bp = Ly.RT + (size_t)(16 * min(ot, Ly.OT - 1) + c) * a.ld + 4 * g;
+    float gsum = 0.f;
+    for (int ch = 0; ch < a.nch; ++ch) {
+      const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+      float sb = 0.f;
+      int r = max(lo, a.bias_r0);
+      for (; r + 64 <= hi; r += 64) {
+        float4 v4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v4[k] = *reinterpret_cast<const float4*>(bp + r + 16 * k);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sb += (v4[k].x + v4[k].y) + (v4[k].z + v4[k].w);
+      }
+      for (; r < hi; r += 16) {
+        const float4 v4 = *reinterpret_cast<const float4*>(bp + r);
+        sb += (v4.x + v4.y) + (v4.z + v4.w);
+      }
+      sb += __shfl_xor(sb, 16);
+      sb += __shfl_xor(sb, 32);
+      gsum = ch == 0 ? sb : gsum + sb;
+    }
+    if (ok) adam_apply(N, s, pp, gsum, mm, vv, th, tg);
+  }
+}
+
+// one or two networks (the union update runs the critic of update t and the actor of t - 1)
+__global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, int nnet, const int32_t* step) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + wave;
+  if (item < n0.items) {
+    wgrad_adam_item(n0, item, step, lane);
+  } else if (nnet > 1 && item - n0.items < n1.items) {
+    wgrad_adam_item(n1, item - n0.items, step, lane);
+  }
+}
+
 }  // namespace cacto
 
 #ifdef CACTO_STAMPS
@@ -783,9 +960,9 @@ int check_nets(const cacto_nets* n) {
   return CACTO_OK;
 }
 
-int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
-                                  const double* storage, const int32_t* idx, const float* isw, int B, float* y,
-                                  float* V, float* Vt, const Workspace& w, hipStream_t st, int* nch_out) {
+int launch_critic_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                        const double* storage, const int32_t* idx, const float* isw, int B, float* y, float* V,
+                        float* Vt, const Workspace& w, hipStream_t st) {
   NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
   NetView Tg = cacto_make_view(sys, CACTO_NET_CRITIC, nets->target_d);
   const ChainScalars cs = chain_scalars(cfg, B);
@@ -795,6 +972,14 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
   hipLaunchKernelGGL(k_critic_grad, dim3(w.Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, cs, storage, idx, isw,
                      B, w.crit, yb, Vb, Vtb, nets->step_d);
   CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                  const double* storage, const int32_t* idx, const float* isw, int B, float* y,
+                                  float* V, float* Vt, const Workspace& w, hipStream_t st, int* nch_out) {
+  if (int e = launch_critic_chain(sys, nets, cfg, storage, idx, isw, B, y, V, Vt, w, st)) return e;
+  const ChainScalars cs = chain_scalars(cfg, B);
   const bool sob = cs.w_S != 0.f;
   WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
   hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
@@ -837,6 +1022,79 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
                      adam_args(cfg, which, soft && which == CACTO_NET_CRITIC), nets->target_d, tpk);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
+}
+
+// The fused weight-gradient + Adam launch serves batches whose gradient rows (critic: 2 Bp with the
+// Sobolev half, actor: Bp) all fall in 64-row chunks; larger batches keep k_wgrad's split-K slabs
+// (many workgroups per tile) and k_adam. A function of B only, so every update path of one batch
+// size takes the same kernels (bit-identical results).
+inline bool fused_adam(int Bp) { return 2 * Bp <= 1024; }
+
+AdamNet adam_net(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, int which, const GradBufs& gb,
+                 int r_begin, int r_end, int bias_r0, int soft, const float* src, float* nb) {
+  AdamNet n{};
+  const NetTopo& t = topo(sys, which);
+  n.wg = wg_args(t, gb, r_begin, r_end, bias_r0);
+  n.t = t;
+  n.nb = nb;
+  n.src = src ? src : nb;
+  n.pk = reinterpret_cast<float4*>(nb + flat_span(t));
+  n.m = which == CACTO_NET_CRITIC ? nets->critic_m_d : nets->actor_m_d;
+  n.v = which == CACTO_NET_CRITIC ? nets->critic_v_d : nets->actor_v_d;
+  const bool sft = soft && which == CACTO_NET_CRITIC;
+  n.target = sft ? nets->target_d : nullptr;
+  n.tpk = sft ? reinterpret_cast<float4*>(nets->target_d + flat_span(t)) : nullptr;
+  n.ad = adam_args(cfg, which, sft);
+  int items = 0;
+  for (int l = 0; l < t.L; ++l) {
+    n.ioff[l] = items;
+    items += t.KT[l] * t.OT[l] + t.OT[l];
+  }
+  n.ioff[t.L] = items;
+  for (int l = t.L + 1; l <= MAX_LAYERS; ++l) n.ioff[l] = items;
+  n.items = items;
+  return n;
+}
+
+AdamNet critic_adam_net(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
+                        int soft, const float* src, float* nb) {
+  const bool sob = cfg->w_S != 0.0;
+  return adam_net(sys, nets, cfg, CACTO_NET_CRITIC, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, soft, src, nb);
+}
+
+AdamNet actor_adam_net(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w) {
+  return adam_net(sys, nets, cfg, CACTO_NET_ACTOR, w.act, 0, w.Bp, 0, 0, nullptr, nets->actor_d);
+}
+
+int launch_wgrad_adam(const AdamNet& n0, const AdamNet* n1, const int32_t* step, hipStream_t st) {
+  const int items = n0.items + (n1 ? n1->items : 0);
+  hipLaunchKernelGGL(k_wgrad_adam, dim3(ceil_div(items, 4)), dim3(256), 0, st, n0, n1 ? *n1 : n0, n1 ? 2 : 1, step);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+// critic step after its chain: GEMM + Adam (+ soft update) from src into nb
+int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
+                     hipStream_t st, const float* src, float* nb) {
+  const int soft = cfg->MC ? 0 : 1;
+  if (fused_adam(w.Bp)) return launch_wgrad_adam(critic_adam_net(sys, nets, cfg, w, soft, src, nb), nullptr,
+                                                 nets->step_d, st);
+  const bool sob = cfg->w_S != 0.0;
+  WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
+  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
+  CACTO_CHECK_HIP(hipGetLastError());
+  cacto_nets dst = *nets;
+  dst.critic_d = nb;
+  return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, a.nch, soft, st, src);
+}
+
+int actor_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
+                    hipStream_t st) {
+  if (fused_adam(w.Bp)) return launch_wgrad_adam(actor_adam_net(sys, nets, cfg, w), nullptr, nets->step_d, st);
+  WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
+  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, a.nch, 0, st);
 }
 
 }  // namespace
@@ -912,12 +1170,10 @@ extern "C" int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const 
   CHECK_WS(workspace_d, workspace_bytes, B);
   const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
   hipStream_t st = as_stream(stream);
-  int nch = 0;
-  if (int e = launch_critic_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, is_w_d, B, y_d, V_d, Vt_d, w, st, &nch))
-    return e;
-  if (int e = launch_adam(sys, nets, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st)) return e;
-  if (int e = launch_actor_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, B, w, st, &nch)) return e;
-  return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, nch, 0, st);
+  if (int e = launch_critic_chain(sys, nets, cfg, storage_d, idx_d, is_w_d, B, y_d, V_d, Vt_d, w, st)) return e;
+  if (int e = critic_step_tail(sys, nets, cfg, w, st, nullptr, nets->critic_d)) return e;
+  if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx_d, B, w, st)) return e;
+  return actor_step_tail(sys, nets, cfg, w, st);
 }
 
 // K consecutive updates (learn_and_update's loop with its minibatches drawn up front, RL.py:120-143)
@@ -974,11 +1230,8 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
     cacto_nets cur = *nets, nxt = *nets;
     cur.critic_d = buf[t & 1];
     nxt.critic_d = buf[(t + 1) & 1];
-    int nch = 0;
-    if (int e = launch_critic_chain_and_wgrad(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st, &nch))
-      return e;
-    if (int e = launch_adam(sys, &nxt, cfg, CACTO_NET_CRITIC, w.slab, nch, cfg->MC ? 0 : 1, st, cur.critic_d))
-      return e;
+    if (int e = launch_critic_chain(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
+    if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d)) return e;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
     if (per) {
       if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
@@ -988,10 +1241,7 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
     CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t & 1], side));
-    WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
-    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, side, a, w.slab_a);
-    CACTO_CHECK_HIP(hipGetLastError());
-    if (int e = launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, a.nch, 0, side)) return e;
+    if (int e = actor_step_tail(sys, nets, cfg, w, side)) return e;
   }
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, side));
   CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));

@@ -165,3 +165,41 @@ def test_pipelined_per_updates_equal_sequential():
         assert torch.equal(a, b)
     for name in ("sum_tree", "min_tree", "exp_counter", "max_priority"):
         assert torch.equal(getattr(sbuf, name), getattr(pbuf, name)), name
+
+
+@pytest.mark.parametrize("system,B,w_S,MC", [("double_integrator", 128, 1e-2, 0), ("double_integrator", 200, 1e-2, 1),
+                                            ("double_integrator", 512, 1e-2, 0), ("manipulator", 64, 0.0, 0),
+                                            ("car_park", 96, 0.0, 1)])
+def test_fused_gemm_adam_equals_split_path(system, B, w_S, MC):
+    """Small batches (gradient rows <= 1024) run the weight-gradient GEMM and Adam as one launch
+    (k_wgrad_adam); its sums are formed in k_wgrad's order, so an update equals the split path
+    (cacto_critic_grad -> slabs -> reduce, cacto_adam_step; the same for the actor) bit for bit."""
+    from cacto_amd.rl import ACTOR, CRITIC
+    conf = load_conf(system, fresh=True)
+    conf.MC = MC
+    env = make_env(conf)
+    ns = conf.nb_state
+    rng = np.random.default_rng(17)
+    N = 3000
+    S = np.column_stack([rng.uniform(-3, 3, (N, ns - 1)), rng.uniform(0, 4.9, N)])
+    rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.01, rng.normal(size=(N, ns)) * 0.3,
+                           (rng.uniform(size=(N, 1)) < 0.1).astype(float), (rng.uniform(size=(N, 1)) < 0.1)
+                           .astype(float)], axis=1)
+    storage = torch.as_tensor(rows, device="cuda")
+    idx = torch.as_tensor(rng.integers(0, N, size=(3, B)).astype(np.int32), device="cuda")
+    wts = torch.as_tensor(rng.uniform(0.2, 1.0, size=(3, B)).astype(np.float32), device="cuda")
+
+    def learner():
+        rl = RL_AC(env, NN(env, conf, w_S=w_S, seed=4), conf)
+        rl.setup_model()
+        return rl
+    fused, split = learner(), learner()
+    for k in range(3):
+        fused.update_rows(storage, idx[k], wts[k])
+        gc = split.critic_grad_flat(storage, idx[k], wts[k])
+        split.apply_gradients(CRITIC, gc, soft_update=not MC)
+        ga = split.actor_grad_flat(storage, idx[k])
+        split.apply_gradients(ACTOR, ga)
+    torch.cuda.synchronize()
+    for a, b in zip(_state(fused), _state(split)):
+        assert torch.equal(a, b)

@@ -1,13 +1,26 @@
-# Round profile set (see profiles/README.md): kernel trace of the default bench, then FETCH_SIZE and
-# WRITE_SIZE of k_rollout in separate passes. Usage: bash tools/prof_round.sh r01
+# Round profile set (see profiles/README.md). Usage: bash tools/prof_round.sh r02
+#  1. kernel trace of the default bench (every system), and of the DI update loop at B = 128 and at
+#     B = 4096 in runs of their own (so per-batch learner kernel times are readable);
+#  2. PMC passes, one counter group per run (TCC slot limits): FETCH_SIZE, WRITE_SIZE of the
+#     rollout; MFMA busy cycles / MFMA MOPS / GRBM_GUI_ACTIVE of the rollout and learner kernels.
 set -e
 export TMPDIR=/tmp
 R=$1
 D=gpurun_out/prof_$R
 mkdir -p $D
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/trace -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-diagnostics > $D/bench_under_rocprof.json 2> $D/trace.err
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_rollout -d $D/fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-diagnostics --extra-systems "" --batches 128 --update-steps 5 > $D/fetch.json 2> $D/fetch.err
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_rollout -d $D/write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-diagnostics --extra-systems "" --batches 128 --update-steps 5 > $D/write.json 2> $D/write.err
+SMALL="--no-cpu-baseline --no-diagnostics --no-config0"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/trace -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 200 $SMALL > $D/bench_under_rocprof.json 2> $D/trace.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/b128 -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 1000 --batches 128 --extra-systems "" $SMALL > $D/b128.json 2> $D/b128.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/b4096 -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 1000 --batches 4096 --extra-systems "" $SMALL > $D/b4096.json 2> $D/b4096.err
+PMCARGS="--steps 3 --warmup 1 --extra-systems= --update-steps 20 $SMALL"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_rollout -d $D/fetch -o run -- python3 bench.py $PMCARGS --batches 128 > $D/fetch.json 2> $D/fetch.err
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_rollout -d $D/write -o run -- python3 bench.py $PMCARGS --batches 128 > $D/write.json 2> $D/write.err
 python3 tools/prof_summary.py stats $D/trace/run_results.db > $D/kernel_stats.csv
+python3 tools/prof_summary.py stats $D/b128/run_results.db > $D/kernel_stats_di_b128.csv
+python3 tools/prof_summary.py stats $D/b4096/run_results.db > $D/kernel_stats_di_b4096.csv
 python3 tools/prof_summary.py pmc $D/fetch/run_results.db > $D/pmc_fetch.csv
 python3 tools/prof_summary.py pmc $D/write/run_results.db > $D/pmc_write.csv
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_rollout|k_critic_grad|k_actor_grad|k_wgrad" -d $D/mfma128 -o run -- python3 bench.py $PMCARGS --batches 128 > $D/mfma128.json 2> $D/mfma128.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_rollout|k_critic_grad|k_actor_grad|k_wgrad" -d $D/mfma4096 -o run -- python3 bench.py $PMCARGS --batches 4096 > $D/mfma4096.json 2> $D/mfma4096.err
+python3 tools/prof_summary.py pmc $D/mfma128/run_results.db > $D/pmc_mfma_b128.csv
+python3 tools/prof_summary.py pmc $D/mfma4096/run_results.db > $D/pmc_mfma_b4096.csv
