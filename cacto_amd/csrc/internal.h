@@ -1,6 +1,8 @@
 // Host-side handle layout shared by the translation units of libcacto_hip.so.
 #pragma once
 
+#include <mutex>
+
 #include "env.h"
 #include "mlp.h"
 
@@ -12,6 +14,7 @@ struct cacto_sys {
   size_t ddp_ws_bytes = 0;
   hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its two events
   hipEvent_t ev_critic = nullptr, ev_actor[2] = {nullptr, nullptr};
+  std::mutex pipe_mu;  // one two-stream pipeline at a time per handle (they share side / events)
 };
 
 namespace cacto {

@@ -68,30 +68,38 @@ __device__ __forceinline__ float clog_backward(float x, float g) {
 }
 
 // ---------------------------------------------------------------- critic chain (a11)
-__global__ void __launch_bounds__(CACTO_THREADS)
-    k_critic_grad(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, ChainScalars cs,
-                  const double* __restrict__ storage, const int32_t* __restrict__ idx, const float* __restrict__ isw,
-                  int B, GradBufs gb, float* __restrict__ y_out, float* __restrict__ V_out, float* __restrict__ Vt_out,
-                  int32_t* __restrict__ step) {
-  __shared__ float4 X0[64], XT[64], G0[64];
-  __shared__ float4 Cs[24 * 64];  // cos z_l
-  __shared__ float4 Hs[24 * 64];  // h_l = sin z_l
-  __shared__ float4 G[16 * 64];
-  __shared__ float4 ZB[24 * 64];
-  __shared__ float4 GB[16 * 64];
-  __shared__ float4 red[4 * 64];
-  __shared__ float st[256], stn[256], dvdx[256];
-  __shared__ float Rs[16], ds[16], ws[16], Vn[16], V[16], y[16], Vb[16], Vt2[16];
+struct CriticLds {
+  float4 X0[64], XT[64], G0[64];
+  float4 Cs[24 * 64];  // cos z_l
+  float4 Hs[24 * 64];  // h_l = sin z_l
+  float4 G[16 * 64];
+  float4 ZB[24 * 64];
+  float4 GB[16 * 64];
+  float4 red[4 * 64];
+  float st[256], stn[256], dvdx[256];
+  float Rs[16], ds[16], ws[16], Vn[16], V[16], y[16], Vb[16], Vt2[16];
+};
+
+// one 16-sample tile of the critic chain (workgroup-wide; S in LDS)
+__device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const SysDevice* __restrict__ sdp,
+                                             const NetView& C, const NetView& Tg, const ChainScalars& cs,
+                                             const double* __restrict__ storage, const int32_t* __restrict__ idx,
+                                             const float* __restrict__ isw, int B, const GradBufs& gb,
+                                             float* __restrict__ y_out, float* __restrict__ V_out,
+                                             float* __restrict__ Vt_out, int32_t* __restrict__ step) {
+  float4 *X0 = S.X0, *XT = S.XT, *G0 = S.G0, *Cs = S.Cs, *Hs = S.Hs, *G = S.G, *ZB = S.ZB, *GB = S.GB, *red = S.red;
+  float *st = S.st, *stn = S.stn, *dvdx = S.dvdx, *Rs = S.Rs, *ds = S.ds, *ws = S.ws, *Vn = S.Vn, *V = S.V, *y = S.y,
+        *Vb = S.Vb, *Vt2 = S.Vt2;
   CSTAMP_DECL;
   CSTAMP(0);
   const cacto_sys_params& p = sdp->p;
   const Lane L;
-  const int ns = p.nb_state, cols = 3 * ns + 3, s0 = blockIdx.x * CACTO_TILE;
+  const int ns = p.nb_state, cols = 3 * ns + 3, s0 = tile * CACTO_TILE;
   const int ld = gb.ld, Bp = gb.Bp;
   const bool sob = cs.w_S != 0.f;
   const int zoff[4] = {0, 4, 8, 16};
   const int goff[4] = {0, 0, 4, 8};
-  if (blockIdx.x == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
+  if (tile == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
 
   float4 w5[2];  // W5[:, 0] at this lane's rows of layer-3 out tiles wave, wave + 4
 #pragma unroll
@@ -283,30 +291,46 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   CSTAMP_FLUSH;
 }
 
-// ---------------------------------------------------------------- actor chain (a12)
-template <int NJ>
 __global__ void __launch_bounds__(CACTO_THREADS)
-    k_actor_grad(const SysDevice* __restrict__ sdp, NetView Ac, NetView C, ChainScalars cs,
-                 const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
-                 int32_t* __restrict__ step) {
-  __shared__ float4 X0[64], XS[64], G0[64], ZB3[64];
-  __shared__ float4 ZA[32 * 64];  // actor z1, z2
-  __shared__ float4 H[32 * 64];   // actor h ping-pong; later critic H (16) + actor zbar2 (16)
-  __shared__ float4 ZC[24 * 64];  // critic cos z at s'
-  __shared__ float4 red[4 * 64];
-  __shared__ float st[256], stn[256];
-  __shared__ float A[16 * CACTO_MAX_ACTION];
-  __shared__ float Fu[16 * CACTO_MAX_STATE * CACTO_MAX_ACTION];
-  __shared__ float dra[16 * CACTO_MAX_ACTION];
-  __shared__ float Vn[16];
-  __shared__ double term_s[16];
+    k_critic_grad(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, ChainScalars cs,
+                  const double* __restrict__ storage, const int32_t* __restrict__ idx, const float* __restrict__ isw,
+                  int B, GradBufs gb, float* __restrict__ y_out, float* __restrict__ V_out, float* __restrict__ Vt_out,
+                  int32_t* __restrict__ step) {
+  __shared__ CriticLds S;
+  critic_chain(S, blockIdx.x, sdp, C, Tg, cs, storage, idx, isw, B, gb, y_out, V_out, Vt_out, step);
+}
+
+// ---------------------------------------------------------------- actor chain (a12)
+struct ActorLds {
+  float4 X0[64], XS[64], G0[64], ZB3[64];
+  float4 ZA[32 * 64];  // actor z1, z2
+  float4 H[32 * 64];   // actor h ping-pong; later critic H (16) + actor zbar2 (16)
+  float4 ZC[24 * 64];  // critic cos z at s'
+  float4 red[4 * 64];
+  float st[256], stn[256];
+  float A[16 * CACTO_MAX_ACTION];
+  float Fu[16 * CACTO_MAX_STATE * CACTO_MAX_ACTION];
+  float dra[16 * CACTO_MAX_ACTION];
+  float Vn[16];
+  double term_s[16];
+};
+
+// one 16-sample tile of the actor chain (workgroup-wide; S in LDS)
+template <int NJ>
+__device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const SysDevice* __restrict__ sdp,
+                                            const NetView& Ac, const NetView& C, const ChainScalars& cs,
+                                            const double* __restrict__ storage, const int32_t* __restrict__ idx, int B,
+                                            const GradBufs& gb, int32_t* __restrict__ step) {
+  float4 *X0 = S.X0, *XS = S.XS, *G0 = S.G0, *ZB3 = S.ZB3, *ZA = S.ZA, *H = S.H, *ZC = S.ZC, *red = S.red;
+  float *st = S.st, *stn = S.stn, *A = S.A, *Fu = S.Fu, *dra = S.dra, *Vn = S.Vn;
+  double* term_s = S.term_s;
   CSTAMP(0);
   const SysDevice& sd = *sdp;
   const cacto_sys_params& p = sd.p;
   const Lane L;
-  const int ns = p.nb_state, na = p.nb_action, cols = 3 * ns + 3, s0 = blockIdx.x * CACTO_TILE;
+  const int ns = p.nb_state, na = p.nb_action, cols = 3 * ns + 3, s0 = tile * CACTO_TILE;
   const int ld = gb.ld;
-  if (blockIdx.x == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
+  if (tile == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
   {
     const int c = L.tid >> 4, f = L.tid & 15;
     const bool valid = s0 + c < B;
@@ -420,6 +444,36 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   CSTAMP(9);
   __syncthreads();
   CSTAMP_FLUSH;
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(CACTO_THREADS)
+    k_actor_grad(const SysDevice* __restrict__ sdp, NetView Ac, NetView C, ChainScalars cs,
+                 const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
+                 int32_t* __restrict__ step) {
+  __shared__ ActorLds S;
+  actor_chain<NJ>(S, blockIdx.x, sdp, Ac, C, cs, storage, idx, B, gb, step);
+}
+
+// The critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the
+// rest) in one launch: neither reads what the other writes (the actor reads the critic C_t that
+// both chains take; panels and counters are separate), so the single-stream small-batch pipeline
+// issues the two as one grid. LDS is the larger of the two layouts, not their sum.
+template <int NJ>
+__global__ void __launch_bounds__(CACTO_THREADS)
+    k_chain_pair(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, NetView Ac, ChainScalars cs,
+                 const double* __restrict__ storage, const int32_t* __restrict__ idx_c, const float* __restrict__ isw,
+                 const int32_t* __restrict__ idx_a, int B, int nct, GradBufs gbc, GradBufs gba,
+                 float* __restrict__ y_out, float* __restrict__ V_out, int32_t* __restrict__ step) {
+  constexpr size_t bytes = sizeof(CriticLds) > sizeof(ActorLds) ? sizeof(CriticLds) : sizeof(ActorLds);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[bytes];
+  if ((int)blockIdx.x < nct) {
+    critic_chain(*reinterpret_cast<CriticLds*>(smem), blockIdx.x, sdp, C, Tg, cs, storage, idx_c, isw, B, gbc, y_out,
+                 V_out, nullptr, step);
+  } else {
+    actor_chain<NJ>(*reinterpret_cast<ActorLds*>(smem), blockIdx.x - nct, sdp, Ac, C, cs, storage, idx_a, B, gba,
+                    step);
+  }
 }
 
 // ---------------------------------------------------------------- weight-gradient GEMM
@@ -845,6 +899,18 @@ struct LaunchActorChain {
   }
 };
 
+template <int NJ>
+struct LaunchChainPair {
+  static int run(const cacto_sys* sys, NetView C, NetView Tg, NetView Ac, ChainScalars cs, const double* storage,
+                 const int32_t* idx_c, const float* isw, const int32_t* idx_a, int B, int nct, GradBufs gbc,
+                 GradBufs gba, float* y, float* V, int32_t* step, hipStream_t st) {
+    hipLaunchKernelGGL(k_chain_pair<NJ>, dim3(2 * nct), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, Ac, cs, storage,
+                       idx_c, isw, idx_a, B, nct, gbc, gba, y, V, step);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
+};
+
 // Rows per weight-gradient chunk (one slab each): small batches use short chunks so the grid
 // still fills the chip; large ones long chunks so Adam sums few slabs.
 inline int wg_chunk(int rows) { return rows <= 1024 ? 64 : rows <= 4096 ? 128 : 256; }
@@ -1176,6 +1242,65 @@ extern "C" int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const 
   return actor_step_tail(sys, nets, cfg, w, st);
 }
 
+// Data-parallel form of the paired schedule (update_pipeline_pair): per step, the gradients of the
+// critic step of update t and of the actor step of update t - 1 (either may be absent) go to one
+// flat buffer [critic P | actor P], the caller all-reduces it once (RCCL), then both Adam steps.
+extern "C" int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                       const double* storage_d, const int32_t* idx_c_d, const float* is_w_d,
+                                       const int32_t* idx_a_d, int B, float* grad_d, float* y_d, float* V_d,
+                                       void* workspace_d, size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && grad_d && B > 0 && (idx_c_d || idx_a_d),
+                "cacto_update_pair_grads: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  hipStream_t st = as_stream(stream);
+  float* yb = y_d ? y_d : w.scal;
+  float* Vb = V_d ? V_d : w.scal + w.Bp;
+  if (idx_c_d && idx_a_d) {
+    const NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
+    const NetView Tg = cacto_make_view(sys, CACTO_NET_CRITIC, nets->target_d);
+    const NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
+    if (int e = dispatch_nj<LaunchChainPair>(sys->host.p, sys, C, Tg, Ac, chain_scalars(cfg, B), storage_d, idx_c_d,
+                                             is_w_d, idx_a_d, B, w.Bp / 16, w.crit, w.act, yb, Vb, nets->step_d, st))
+      return e;
+  } else if (idx_c_d) {
+    if (int e = launch_critic_chain(sys, nets, cfg, storage_d, idx_c_d, is_w_d, B, yb, Vb, nullptr, w, st)) return e;
+  } else {
+    if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx_a_d, B, w, st)) return e;
+  }
+  const int Pc = sys->critic.params, Pa = sys->actor.params;
+  if (idx_c_d) {
+    const bool sob = cfg->w_S != 0.0;
+    WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
+    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
+    CACTO_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pc + 255) / 256, 1024)), dim3(256), 0, st, w.slab, a.nch, Pc, grad_d);
+    CACTO_CHECK_HIP(hipGetLastError());
+  }
+  if (idx_a_d) {
+    WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
+    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
+    CACTO_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, a.nch, Pa,
+                       grad_d + Pc);
+    CACTO_CHECK_HIP(hipGetLastError());
+  }
+  return CACTO_OK;
+}
+
+extern "C" int cacto_update_pair_apply(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                       const float* grad_d, int critic, int actor, int soft_update, void* stream) {
+  CACTO_REQUIRE(sys && cfg && grad_d && (critic || actor), "cacto_update_pair_apply: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  hipStream_t st = as_stream(stream);
+  if (critic)
+    if (int e = launch_adam(sys, nets, cfg, CACTO_NET_CRITIC, grad_d, 1, soft_update, st)) return e;
+  if (actor)
+    if (int e = launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, grad_d + sys->critic.params, 1, 0, st)) return e;
+  return CACTO_OK;
+}
+
 // K consecutive updates (learn_and_update's loop with its minibatches drawn up front, RL.py:120-143)
 // as a two-stream pipeline. The critic step of update t+1 reads only the critic, the target and the
 // rows — never the actor — so it runs while the actor step of update t is still going:
@@ -1196,22 +1321,114 @@ struct PerArgs {
   double *exp_counter, *max_priority;
 };
 
+// Small batches (fused_adam): one stream, K + 1 steps. Step t runs the critic chain of update t
+// and the actor chain of update t - 1 as one grid (k_chain_pair), then both GEMM + Adam steps as
+// one k_wgrad_adam launch:
+//   critic(t) reads C_t, T_t (Adam of step t - 1 wrote them); actor(t-1) reads A_{t-1} and C_t —
+//   exactly what RL.py:104-109 gives it (the critic after its own update t - 1);
+//   Adam: C_t -> C_{t+1} (+ soft T), A_{t-1} -> A_t.
+// Every kernel sees the inputs of the sequential loop, so results are bit-identical, with no
+// cross-stream events and three launches per update (five with PER).
+int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                         const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
+                         const Workspace& w, hipStream_t st) {
+  float* const y = w.scal;
+  float* const V = w.scal + w.Bp;
+  const int nct = w.Bp / 16;
+  const int soft = cfg->MC ? 0 : 1;
+  const ChainScalars cs = chain_scalars(cfg, B);
+  const NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
+  const NetView Tg = cacto_make_view(sys, CACTO_NET_CRITIC, nets->target_d);
+  const NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
+  const AdamNet cn = critic_adam_net(sys, nets, cfg, w, soft, nullptr, nets->critic_d);
+  const AdamNet an = actor_adam_net(sys, nets, cfg, w);
+  const int32_t* idx_prev = nullptr;
+  for (int t = 0; t <= K; ++t) {
+    const int32_t* idx = nullptr;
+    const float* isw = nullptr;
+    if (t < K) {
+      idx = idx_d ? idx_d + (size_t)t * B : nullptr;
+      if (per) {
+        int32_t* pi = w.pidx + (size_t)(t & 1) * w.Bp;
+        if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                     per->uniforms + (size_t)t * B, B, pi, w.pisw, per->exp_counter, st))
+          return e;
+        idx = pi;
+        isw = w.pisw;
+      }
+    }
+    if (t < K && t > 0) {
+      if (int e = dispatch_nj<LaunchChainPair>(sys->host.p, sys, C, Tg, Ac, cs, storage_d, idx, isw, idx_prev, B, nct,
+                                               w.crit, w.act, y, V, nets->step_d, st))
+        return e;
+      if (int e = launch_wgrad_adam(cn, &an, nets->step_d, st)) return e;
+    } else if (t < K) {
+      if (int e = launch_critic_chain(sys, nets, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
+      if (int e = launch_wgrad_adam(cn, nullptr, nets->step_d, st)) return e;
+    } else {
+      if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx_prev, B, w, st)) return e;
+      if (int e = launch_wgrad_adam(an, nullptr, nets->step_d, st)) return e;
+    }
+    if (per && t < K) {
+      if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
+                                   per->eps, per->alpha, per->max_priority, B, st))
+        return e;
+    }
+    idx_prev = idx;
+  }
+  return CACTO_OK;
+}
+
+// The side stream and its events, created once per handle and published only when all exist.
+int ensure_side_stream(cacto_sys* ms) {
+  if (ms->side) return CACTO_OK;
+  hipStream_t side = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  hipError_t e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+  if (e != hipSuccess) {
+    for (hipEvent_t x : ev)
+      if (x) (void)hipEventDestroy(x);
+    if (side) (void)hipStreamDestroy(side);
+    return hip_fail(e, "cacto_update_n: side stream / events");
+  }
+  ms->ev_critic = ev[0];
+  ms->ev_actor[0] = ev[1];
+  ms->ev_actor[1] = ev[2];
+  ms->side = side;
+  return CACTO_OK;
+}
+
+int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                         const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
+                         const Workspace& w, hipStream_t st, int* cbuf);
+
 int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const double* storage_d,
                     const int32_t* idx_d, const PerArgs* per, int K, int B, const Workspace& w, hipStream_t st) {
   cacto_sys* ms = const_cast<cacto_sys*>(sys);
-  if (!ms->side) {
-    CACTO_CHECK_HIP(hipStreamCreateWithFlags(&ms->side, hipStreamNonBlocking));
-    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_critic, hipEventDisableTiming));
-    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_actor[0], hipEventDisableTiming));
-    CACTO_CHECK_HIP(hipEventCreateWithFlags(&ms->ev_actor[1], hipEventDisableTiming));
-  }
-  hipStream_t side = ms->side;
+  std::lock_guard<std::mutex> lock(ms->pipe_mu);
+  if (int e = ensure_side_stream(ms)) return e;
   const NetTopo& tc = sys->critic;
   const size_t nb_bytes = ((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256) * sizeof(float);
-  float* const buf[2] = {nets->critic_d, w.cshadow};
   CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));  // everything the caller queued before
-  CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+  CACTO_CHECK_HIP(hipStreamWaitEvent(ms->side, ms->ev_critic, 0));
+  // cbuf: the buffer (0 caller's, 1 workspace) holding the newest critic; on every exit, error or
+  // not, the side stream joins the caller's stream and the newest critic lands in the caller's buffer
+  int cbuf = 0;
+  const int err = update_pipeline_body(sys, nets, cfg, storage_d, idx_d, per, K, B, w, st, &cbuf);
+  CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, ms->side));
+  CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
+  if (cbuf) CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow, nb_bytes, hipMemcpyDeviceToDevice, st));
+  return err;
+}
+
+int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                         const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
+                         const Workspace& w, hipStream_t st, int* cbuf) {
+  cacto_sys* ms = const_cast<cacto_sys*>(sys);
+  hipStream_t side = ms->side;
+  float* const buf[2] = {nets->critic_d, w.cshadow};
   float* const y = w.scal;
   float* const V = w.scal + w.Bp;
   for (int t = 0; t < K; ++t) {
@@ -1232,6 +1449,7 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
     nxt.critic_d = buf[(t + 1) & 1];
     if (int e = launch_critic_chain(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
     if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d)) return e;
+    *cbuf = (t + 1) & 1;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
     if (per) {
       if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
@@ -1243,9 +1461,6 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t & 1], side));
     if (int e = actor_step_tail(sys, nets, cfg, w, side)) return e;
   }
-  CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, side));
-  CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
-  if (K & 1) CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow, nb_bytes, hipMemcpyDeviceToDevice, st));
   return CACTO_OK;
 }
 }  // namespace
@@ -1258,6 +1473,7 @@ extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, cons
   CHECK_WS(workspace_d, workspace_bytes, B);
   if (K == 0) return CACTO_OK;
   const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  if (fused_adam(w.Bp)) return update_pipeline_pair(sys, nets, cfg, storage_d, idx_d, nullptr, K, B, w, as_stream(stream));
   return update_pipeline(sys, nets, cfg, storage_d, idx_d, nullptr, K, B, w, as_stream(stream));
 }
 
@@ -1278,5 +1494,7 @@ extern "C" int cacto_update_n_per(const cacto_sys* sys, const cacto_nets* nets, 
   const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
   const PerArgs per{sum_tree_d, min_tree_d, capacity, max_idx, beta, fresh_factor, eps, alpha, uniforms_d,
                     exp_counter_d, max_priority_d};
+  // with PER the sampling and the priority update sit between consecutive critic steps on one
+  // stream, so the two-stream pipeline (actor steps beside them) is the faster schedule here
   return update_pipeline(sys, nets, cfg, storage_d, nullptr, &per, K, B, w, as_stream(stream));
 }

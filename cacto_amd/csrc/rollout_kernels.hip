@@ -577,6 +577,9 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   if (use_actor) ro_load_actor<NG, ns, na, REGK, LDSK>(N, L, R, Sh.W);
   const float* W2g = N.flat + N.t.woff[1];
   for (int e = L.tid; e < NG * 64; e += CACTO_THREADS) Sh.W.x0[e] = 0.f;
+  // slot states too: a slot that is never filled still feeds its (unused) actor input row, which
+  // then reads zeros rather than stale LDS
+  for (int e = L.tid; e < SL * ns; e += CACTO_THREADS) Sh.sS[e] = 0.0;
   if (L.tid < SL) Sh.sact[L.tid] = 0;
   __syncthreads();
   int head = 0;  // queue position (wave 0, uniform)

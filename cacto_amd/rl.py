@@ -34,6 +34,24 @@ def dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update):
     apply("actor", ga, False)
 
 
+def dp_pipeline(K, grads, all_reduce, apply):
+    """K data-parallel updates (RL.py:101-118 each) with ONE gradient exchange per update.
+
+    Step t = 0..K computes, into one flat buffer, the gradient of the critic step of update t
+    (c = t, absent at t = K) and of the actor step of update t - 1 (a = t - 1, absent at t = 0),
+    all-reduces it once, then applies both Adam steps. The critic step of update t never reads the
+    actor, and the actor step of update t - 1 sees the critic after its update t - 1 — the ordering
+    RL.py:104-109 prescribes — so the K updates equal the sequential loop. Gradients are normalised by
+    the GLOBAL batch, so the exchange is a plain sum. grads(c, a) -> tensor, apply(c, a, g).
+    """
+    for t in range(K + 1):
+        c = t if t < K else None
+        a = t - 1 if t > 0 else None
+        g = grads(c, a)
+        all_reduce(g)
+        apply(c, a, g)
+
+
 class Adam:
     """tf.keras.optimizers.Adam surface (RL.py:79-88) over the device Keras-2.11 Adam step
     (`cacto_adam_step`, with the learner's PiecewiseConstantDecay schedule when LR_SCHEDULE)."""
@@ -205,9 +223,7 @@ class RL_AC:
         results bit-identical to K update_rows calls. Single rank (the data-parallel update
         all-reduces between the two steps)."""
         if self.dp_world > 1:
-            for k in range(idx_steps.shape[0]):
-                self.update_rows(storage, idx_steps[k])
-            return
+            return self._update_rows_n_dp(storage, idx_steps)
         K, B = int(idx_steps.shape[0]), int(idx_steps.shape[1])
         ws = self.workspace(B)
         cfg = self._cfg_for(B)
@@ -261,13 +277,47 @@ class RL_AC:
         return g
 
     def _update_rows_dp(self, storage, idx, is_w=None, y=None, V=None, Vt=None):
+        if Vt is not None:      # the extra V_tgt(s) output: the two-exchange form
+            import torch.distributed as dist
+            dp_update_step(lambda: self.critic_grad_flat(storage, idx, is_w, y, V, Vt),
+                           lambda: self.actor_grad_flat(storage, idx),
+                           lambda which, g, soft: self.apply_gradients(CRITIC if which == "critic" else ACTOR, g,
+                                                                       soft_update=soft),
+                           lambda t: dist.all_reduce(t, group=self.dp_group),
+                           soft_update=not self.conf.MC)
+            return
+        self._update_rows_n_dp(storage, idx.reshape(1, -1), is_w, y, V)
+
+    def _update_rows_n_dp(self, storage, idx_steps, is_w=None, y=None, V=None):
+        """K data-parallel updates through dp_pipeline: per step one C-ABI call for the paired
+        gradients (critic of update t, actor of update t-1) into one buffer, one RCCL all-reduce of
+        it on the current stream, one call for the Adam steps. is_w / y / V only with K = 1 (PER)."""
         import torch.distributed as dist
-        dp_update_step(lambda: self.critic_grad_flat(storage, idx, is_w, y, V, Vt),
-                       lambda: self.actor_grad_flat(storage, idx),
-                       lambda which, g, soft: self.apply_gradients(CRITIC if which == "critic" else ACTOR, g,
-                                                                   soft_update=soft),
-                       lambda t: dist.all_reduce(t, group=self.dp_group),
-                       soft_update=not self.conf.MC)
+        K, B = int(idx_steps.shape[0]), int(idx_steps.shape[1])
+        ws = self.workspace(B)
+        cfg = self._cfg_for(B)
+        Pc, Pa = self.critic_model.P, self.actor_model.P
+        g = self._dp_grad_buf(Pc + Pa)
+        idx_steps = idx_steps.contiguous()
+
+        def grads(c, a):
+            ic = idx_steps[c] if c is not None else None
+            ia = idx_steps[a] if a is not None else None
+            L.lib().call("cacto_update_pair_grads", self.sys.handle, C.byref(self.nets), C.byref(cfg),
+                         dptr(storage, torch.float64), dptr(ic, torch.int32), dptr(is_w if c is not None else None),
+                         dptr(ia, torch.int32), B, dptr(g), dptr(y if c is not None else None),
+                         dptr(V if c is not None else None), dptr(ws), ws.numel() * 4, stream())
+            return g[:Pc] if a is None else (g[Pc:] if c is None else g)
+
+        def apply(c, a, _):
+            L.lib().call("cacto_update_pair_apply", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(g),
+                         int(c is not None), int(a is not None), int(not self.conf.MC), stream())
+        dp_pipeline(K, grads, lambda t: dist.all_reduce(t, group=self.dp_group), apply)
+
+    def _dp_grad_buf(self, n):
+        if getattr(self, "_dp_g", None) is None or self._dp_g.numel() < n:
+            self._dp_g = torch.empty(n, dtype=torch.float32, device=DEVICE)
+        return self._dp_g
 
     def update(self, state_batch, state_next_rollout_batch, partial_reward_to_go_batch, dVdx_batch, d_batch,
                term_batch, weights_batch, batch_size=None):

@@ -235,10 +235,12 @@ int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_updat
                  void* stream);
 
 /* K consecutive updates on minibatch indices idx_d [K][B] (learn_and_update's loop with its
- * minibatches drawn up front, RL.py:120-143; no IS weights). Bit-identical to K cacto_update calls;
- * internally the critic step of update t+1 overlaps the actor step of update t on a second stream
- * owned by the system handle (the critic step never reads the actor), joined back into `stream`
- * before the call returns. */
+ * minibatches drawn up front, RL.py:120-143; no IS weights). Bit-identical to K cacto_update calls.
+ * The critic step of update t+1 overlaps the actor step of update t (the critic step never reads
+ * the actor): for batches of at most 512 the two chains run as one grid on `stream` (three launches
+ * per update); larger batches use a second stream owned by the system handle, joined back into
+ * `stream` before the call returns (also on error). Calls on one handle are serialised internally
+ * (a mutex), so two host threads may call it, but their updates are not interleaved. */
 int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                    const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
                    size_t workspace_bytes, void* stream);
@@ -251,6 +253,21 @@ int cacto_update_n_per(const cacto_sys* sys, const cacto_nets* nets, const cacto
                        int64_t max_idx, double beta, const double* uniforms_d, double* exp_counter_d,
                        double fresh_factor, double eps, double alpha, double* max_priority_d, int K, int B,
                        void* workspace_d, size_t workspace_bytes, void* stream);
+
+/* Data-parallel K-update loop (RL.py:101-118 per update, replaces the two blocking all-reduces of
+ * learn_and_update's DP form with one per update). The host runs K + 1 steps; step t computes the
+ * gradient of the critic step of update t (idx_c_d != NULL, with is_w_d / y_d / V_d as in
+ * cacto_update) and of the actor step of update t - 1 (idx_a_d != NULL) into
+ * grad_d [critic params | actor params] (each scaled by 1/cfg->B_global, so the exchange is a plain
+ * sum), the caller all-reduces the present part(s) of grad_d once, then cacto_update_pair_apply runs
+ * the Adam steps (critic with the soft target update when soft_update). The actor gradient of
+ * update t - 1 is taken against the critic after its update t - 1, as in the sequential loop. */
+int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                            const double* storage_d, const int32_t* idx_c_d, const float* is_w_d,
+                            const int32_t* idx_a_d, int B, float* grad_d, float* y_d, float* V_d,
+                            void* workspace_d, size_t workspace_bytes, void* stream);
+int cacto_update_pair_apply(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                            const float* grad_d, int critic, int actor, int soft_update, void* stream);
 
 /* ---------------------------------------------------------------- rollouts --------------- */
 

@@ -47,10 +47,13 @@ def _unflat(t, like):
     return out
 
 
-def _run_update(rows, world, all_reduce, n_steps=2):
-    """n_steps data-parallel updates on `rows` (this rank's shard), returning final weights."""
+def _run_update(rows, world, all_reduce, n_steps=3, pipelined=True):
+    """n_steps data-parallel updates on `rows` (this rank's shard), returning final weights.
+    pipelined: RL_AC's schedule (cacto_amd.rl.dp_pipeline: one exchange per update, the critic step
+    of update t beside the actor step of update t-1); else one update after the other
+    (dp_update_step, RL.py:104-109 literally)."""
     from cacto_amd.confs import load_conf
-    from cacto_amd.rl import dp_update_step
+    from cacto_amd.rl import dp_pipeline, dp_update_step
     conf = load_conf("double_integrator")
     oe = oenv.make_env(conf)
     w = load_weights("di_seed0_0")
@@ -78,8 +81,22 @@ def _run_update(rows, world, all_reduce, n_steps=2):
         if soft:
             st["target"] = onn.soft_update(st["target"], st["critic"], conf.UPDATE_RATE)
 
-    for _ in range(n_steps):
-        dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update=True)
+    if not pipelined:
+        for _ in range(n_steps):
+            dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update=True)
+        return {k: _flat(v).numpy() for k, v in st.items()}
+    nc = _flat(st["critic"]).numel()
+
+    def grads(c, a):
+        parts = ([critic_grad()] if c is not None else []) + ([actor_grad()] if a is not None else [])
+        return torch.cat(parts)
+
+    def apply_pair(c, a, g):
+        if c is not None:
+            apply("critic", g[:nc], True)
+        if a is not None:
+            apply("actor", g[nc:] if c is not None else g, False)
+    dp_pipeline(n_steps, grads, all_reduce, apply_pair)
     return {k: _flat(v).numpy() for k, v in st.items()}
 
 
@@ -104,7 +121,7 @@ def _free_port():
 def test_dp_update_equals_single_process():
     from cacto_amd.confs import load_conf
     rows = _rows(load_conf("double_integrator"), np.random.default_rng(7))
-    ref = _run_update(rows, 1, lambda t: None)
+    ref = _run_update(rows, 1, lambda t: None, pipelined=False)   # the sequential reference order
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

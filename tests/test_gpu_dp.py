@@ -83,7 +83,12 @@ def _update_worker(rank, port, rows, idx, q):
             loc = idx[k, rank * B_LOCAL:(rank + 1) * B_LOCAL].astype(np.int32)
             rl.update_rows(storage, torch.as_tensor(loc, device="cuda"))
         torch.cuda.synchronize()
-        q.put((rank, _state(rl), rl.steps.cpu().tolist()))
+        # the K updates again as one pipelined call (one exchange per update: critic of t with actor of t-1)
+        rp = _learner(WORLD)
+        loc = np.ascontiguousarray(idx[:, rank * B_LOCAL:(rank + 1) * B_LOCAL].astype(np.int32))
+        rp.update_rows_n(storage, torch.as_tensor(loc, device="cuda"))
+        torch.cuda.synchronize()
+        q.put((rank, _state(rl), rl.steps.cpu().tolist(), _state(rp), rp.steps.cpu().tolist()))
     finally:
         dist.destroy_process_group()
 
@@ -146,6 +151,10 @@ def test_dp_update_on_gpu_equals_single_rank():
     for a, b in zip(s0, s1):
         assert np.array_equal(a, b)                          # replicas stay bit-identical
     assert res[0][1] == [K, K]
+    for r in range(WORLD):                                   # pipelined DP loop == K single DP updates
+        assert res[r][3] == [K, K]
+        for a, b in zip(res[r][0], res[r][2]):
+            assert np.array_equal(a, b)
     single = _learner(1)
     storage = torch.as_tensor(rows, device="cuda")
     for k in range(K):
