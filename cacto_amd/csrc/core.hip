@@ -92,6 +92,11 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
     }
     s->actor = make_topo(CACTO_NET_ACTOR, p.nb_state, p.nb_action);
     s->critic = make_topo(CACTO_NET_CRITIC, p.nb_state, p.nb_action);
+    if (int rc = cacto_const_dyn_init(s)) {
+      (void)hipFree(s->dev);
+      delete s;
+      return rc;
+    }
     *out = s;
     return CACTO_OK;
   } catch (const std::exception& ex) {

@@ -14,6 +14,12 @@ struct SysDevice {
   cacto_sys_params p;
   double joints[CACTO_MAX_JOINTS * CACTO_JOINT_COLS];
   double inv_norm[CACTO_MAX_STATE];  // 1.0 / state_norm (the reference's 1/state_norm_arr, f64)
+  // prismatic-only chains (p.const_dyn): the Cholesky factor of M, the bias forces h and the
+  // derivative Fu [ns][na] (row-normalised), computed once on the device at system creation
+  // (k_const_dyn_init) by the same code the per-sample path runs — M and h do not depend on (q, v)
+  double cd_L[CACTO_MAX_JOINTS * CACTO_MAX_JOINTS];
+  double cd_h[CACTO_MAX_JOINTS];
+  double cd_Fu[CACTO_MAX_STATE * CACTO_MAX_ACTION];
 };
 
 // ------------------------------------------------------------------ small 3-vector algebra
@@ -536,6 +542,40 @@ __device__ inline void env_simulate_const(const SysDevice& sd, const ConstDyn<NJ
     }
     out[2 * NJ] = s[2 * NJ] + dt;
   }
+}
+
+// env_simulate_derivative for a prismatic-only chain from the factor / Fu tabled in SysDevice:
+// the same operations on the same values as the per-sample path (chain_terms -> cholesky ->
+// chol_solve), minus the recomputation of the q-independent M and h.
+template <int NJ>
+__device__ inline bool env_simulate_derivative_const(const SysDevice& sd, const double* s, const double* a, bool f32in,
+                                                     double* out, double* Fu) {
+  if constexpr (NJ > 0) {
+    constexpr int NS = 2 * NJ + 1, NA = NJ;
+    const double dt = sd.p.dt;
+    double L[NJ * NJ], dv[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) L[k] = sd.cd_L[k];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) dv[i] = a[i] - sd.cd_h[i];
+    chol_solve<NJ>(L, dv);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      const double v = s[NJ + i];
+      if (f32in) {
+        const float vdt = __fmul_rn((float)v, (float)dt);
+        out[i] = s[i] + (double)vdt;
+        out[NJ + i] = (double)(float)(v + dv[i] * dt);
+      } else {
+        out[i] = s[i] + v * dt;
+        out[NJ + i] = v + dv[i] * dt;
+      }
+    }
+    out[2 * NJ] = s[2 * NJ] + dt;
+#pragma unroll
+    for (int k = 0; k < NS * NA; ++k) Fu[k] = sd.cd_Fu[k];
+  }
+  return true;
 }
 
 // Env.derivative (environment.py:93-109 / SI :209-219): Fu[ns, na] row-major, rows scaled by

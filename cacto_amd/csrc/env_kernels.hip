@@ -194,6 +194,31 @@ __global__ void k_buffer_gather(const double* __restrict__ storage, int ns, cons
   }
 }
 
+// The tabled constants of a prismatic-only chain (SysDevice::cd_*), one thread, at system creation:
+// chain_terms / cholesky / the per-sample derivative path evaluated once (at q = v = 0; M and h do
+// not depend on them for such chains, which the rollout's per-episode factor relies on as well).
+template <int NJ>
+__global__ void k_const_dyn_init(SysDevice* sd) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if constexpr (NJ > 0) {
+    constexpr int NS = 2 * NJ + 1, NA = NJ;
+    double s[NS], a[NA], out[NS], Fu[NS * NA], M[NJ * NJ], h[NJ];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) s[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) a[i] = 0.0;
+    chain_terms<NJ>(*sd, s, s + NJ, M, h);
+    cholesky<NJ>(M);
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) sd->cd_L[k] = M[k];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) sd->cd_h[i] = h[i];
+    env_simulate_derivative<NJ>(*sd, s, a, false, out, Fu);
+#pragma unroll
+    for (int k = 0; k < NS * NA; ++k) sd->cd_Fu[k] = Fu[k];
+  }
+}
+
 }  // namespace cacto
 
 using namespace cacto;
@@ -311,4 +336,21 @@ extern "C" int cacto_buffer_gather(const cacto_sys* sys, const double* storage_d
                      idx_d, B, S_d, R_d, S_next_d, dVdx_d, d_d, term_d);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
+}
+
+namespace {
+template <int NJ>
+struct LaunchConstDyn {
+  static int run(cacto_sys* sys) {
+    hipLaunchKernelGGL(k_const_dyn_init<NJ>, dim3(1), dim3(64), 0, 0, sys->dev);
+    CACTO_CHECK_HIP(hipGetLastError());
+    CACTO_CHECK_HIP(hipDeviceSynchronize());
+    return CACTO_OK;
+  }
+};
+}  // namespace
+
+int cacto_const_dyn_init(cacto_sys* sys) {
+  if (!sys->host.p.const_dyn) return CACTO_OK;
+  return dispatch_nj<LaunchConstDyn>(sys->host.p, sys);
 }

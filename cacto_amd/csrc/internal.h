@@ -24,3 +24,4 @@ inline int64_t flat_span(const NetTopo& t) { return ((int64_t)t.params + 63) / 6
 }  // namespace cacto
 
 cacto::NetView cacto_make_view(const cacto_sys* sys, int net, const float* netbuf);
+int cacto_const_dyn_init(cacto_sys* sys);  // SysDevice::cd_* of a prismatic-only chain (env_kernels.hip)

@@ -364,7 +364,12 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
       af[i] = A[c * na + i];
       a[i] = (double)af[i];
     }
-    env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
+    if constexpr (NJ > 0 && NJ <= 3) {
+      if (p.const_dyn) env_simulate_derivative_const<NJ>(sd, s, a, true, sn, F);
+      else env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
+    } else {
+      env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
+    }
 #pragma unroll
     for (int f = 0; f < 16; ++f) stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
 #pragma unroll
