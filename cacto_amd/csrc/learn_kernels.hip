@@ -101,6 +101,10 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
   const int goff[4] = {0, 0, 4, 8};
   if (tile == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
 
+  // the target network's fragments for the first pass, in flight during the row gathers
+  CriticFwdFrags TF;
+  TF.load<true>(Tg, L);
+  TF.load_last(Tg, L);
   float4 w5[2];  // W5[:, 0] at this lane's rows of layer-3 out tiles wave, wave + 4
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -136,12 +140,12 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
   CSTAMP(1);
 
   // y = R + (1 - d) * V_tgt(s_next)   (NeuralNetwork.py:153-158)
-  if (!cs.MC) critic_forward_tile(Tg, XT, nullptr, nullptr, Hs, red, Vn, L, [](int, int, float4) {});
+  if (!cs.MC) critic_forward_tile_f(TF, Tg, XT, nullptr, nullptr, Hs, red, Vn, L, [](int, int, float4) {});
   __syncthreads();
   CSTAMP(2);
   if (L.tid < 16) y[L.tid] = cs.MC ? Rs[L.tid] : fadd(Rs[L.tid], fmul(fsub(1.f, ds[L.tid]), Vn[L.tid]));
   if (cs.want_vt) {  // the extra V_tgt(s) of NeuralNetwork.py:178
-    critic_forward_tile(Tg, X0, nullptr, nullptr, Hs, red, Vt2, L, [](int, int, float4) {});
+    critic_forward_tile_f(TF, Tg, X0, nullptr, nullptr, Hs, red, Vt2, L, [](int, int, float4) {});
     __syncthreads();
   }
 
@@ -162,25 +166,22 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
     __syncthreads();
     CSTAMP(4);
     SF.load<false>(C, L);
-    // Sobolev loss gradient w.r.t. dV/ds, then w.r.t. G_0 (NeuralNetwork.py:167-170)
-    if (L.wave == 0) {
-      const float4 g4 = G0[L.lane];
-      const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-      float gb0[4];
-      const float gsq = fdiv(fmul(fdiv(1.f, (float)cs.B_global), ws[L.c]), (float)(ns - 1));
-      for (int r = 0; r < 4; ++r) {
-        const int f = 4 * L.g + r;
-        gb0[r] = 0.f;
-        if (f < ns - 1) {
-          const float dvds = nrm.backward(r, gv[r]);
-          const float yp = clog(dvds), yt = clog(dvdx[L.c * 16 + f]);
-          const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
-          gb0[r] = nrm.backward(r, clog_backward(dvds, gyp));
-        }
+    // Sobolev loss gradient w.r.t. dV/ds, then w.r.t. G_0 (NeuralNetwork.py:167-170): one
+    // (sample c, feature f) element per thread (the same ops as per lane and feature)
+    {
+      const int c = L.tid >> 4, f = L.tid & 15;
+      float gb0 = 0.f;
+      if (f < ns - 1) {
+        const float nf = (float)p.state_norm[f];
+        auto nback = [&](float g) { return !p.normalize ? g : fdiv(g, nf); };  // f < ns - 1: not the time column
+        const float gsq = fdiv(fmul(fdiv(1.f, (float)cs.B_global), ws[c]), (float)(ns - 1));
+        const float dvds = nback(reinterpret_cast<const float*>(G0)[((f >> 2) * 16 + c) * 4 + (f & 3)]);
+        const float yp = clog(dvds), yt = clog(dvdx[c * 16 + f]);
+        const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
+        gb0 = nback(clog_backward(dvds, gyp));
       }
-      const float4 v = make_float4(gb0[0], gb0[1], gb0[2], gb0[3]);
-      GB[L.lane] = v;
-      store_panel(gb.LT[0], ld, s0 + L.c, 0, L.g, v);
+      reinterpret_cast<float*>(GB)[((f >> 2) * 16 + c) * 4 + (f & 3)] = gb0;
+      gb.LT[0][(size_t)f * ld + s0 + c] = gb0;  // the panel row of feature f (store_panel's layout)
     }
     __syncthreads();
     CSTAMP(5);
@@ -307,7 +308,7 @@ struct ActorLds {
   float4 H[32 * 64];   // actor h ping-pong; later critic H (16) + actor zbar2 (16)
   float4 ZC[24 * 64];  // critic cos z at s'
   float4 red[4 * 64];
-  float st[256], stn[256];
+  float st[256], stn[256], gn[256];
   float A[16 * CACTO_MAX_ACTION];
   float Fu[16 * CACTO_MAX_STATE * CACTO_MAX_ACTION];
   float dra[16 * CACTO_MAX_ACTION];
@@ -322,7 +323,7 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
                                             const double* __restrict__ storage, const int32_t* __restrict__ idx, int B,
                                             const GradBufs& gb, int32_t* __restrict__ step) {
   float4 *X0 = S.X0, *XS = S.XS, *G0 = S.G0, *ZB3 = S.ZB3, *ZA = S.ZA, *H = S.H, *ZC = S.ZC, *red = S.red;
-  float *st = S.st, *stn = S.stn, *A = S.A, *Fu = S.Fu, *dra = S.dra, *Vn = S.Vn;
+  float *st = S.st, *stn = S.stn, *gn = S.gn, *A = S.A, *Fu = S.Fu, *dra = S.dra, *Vn = S.Vn;
   double* term_s = S.term_s;
   CSTAMP(0);
   const SysDevice& sd = *sdp;
@@ -404,6 +405,11 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   __syncthreads();
   CSTAMP(6);
   // dQ/da = dV/ds' Fu + dr/da ; abar = -dQ/da / B  (NeuralNetwork.py:206-231)
+  {  // d normalize / d s of every (sample, state) element at once, one per thread
+    const int c = L.tid >> 4, i = L.tid & 15;
+    if (i < ns) gn[c * 16 + i] = normalize_backward(p, i, reinterpret_cast<const float*>(G0)[((i >> 2) * 16 + c) * 4 + (i & 3)]);
+  }
+  __syncthreads();
   if (L.wave == 0) {
     const int c = L.c;
     float abar[4];
@@ -413,9 +419,7 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
       if (j < na && s0 + c < B) {
         float q = 0.f;
         for (int i = 0; i < ns; ++i) {
-          const float4 gt = G0[tile_lane(i) + c];
-          const float gi = normalize_backward(p, i, get4(gt, i & 3));
-          const float t = fmul(gi, Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + i * na + j]);
+          const float t = fmul(gn[c * 16 + i], Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + i * na + j]);
           q = (i == 0) ? t : fadd(q, t);
         }
         q = fadd(q, dra[c * na + j]);
@@ -626,6 +630,14 @@ struct AdamArgs {
   int soft;
 };
 
+// write_packed for a weight W_l[i][o] whose layer and indices are known (no search, no division)
+__device__ __forceinline__ void write_packed_w(float4* pk4, const NetTopo& t, int l, int i, int o, float val) {
+  float* pk = reinterpret_cast<float*>(pk4);
+  pk[((size_t)(t.pkoff[l] + (o >> 4) * t.KT[l] + (i >> 4)) * 64 + ((i & 15) >> 2) * 16 + (o & 15)) * 4 + (i & 3)] = val;
+  pk[((size_t)(t.blocks + t.pkoff[l] + (i >> 4) * t.OT[l] + (o >> 4)) * 64 + ((o & 15) >> 2) * 16 + (i & 15)) * 4 +
+     (o & 3)] = val;
+}
+
 __device__ __forceinline__ void write_packed(float4* pk4, const NetTopo& t, int p, float val) {
   float* pk = reinterpret_cast<float*>(pk4);
   int l = t.L - 1;
@@ -749,20 +761,21 @@ __device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int
   return s;
 }
 
-// k_adam's per-parameter arithmetic (same ops, same order)
+// k_adam's per-parameter arithmetic (same ops, same order); l >= 0: a weight W_l[i][o] (direct
+// packed writes), l < 0: a bias (not packed)
 __device__ __forceinline__ void adam_apply(const AdamNet& N, const AdamScalars& s, int p, float g, float mm, float vv,
-                                           float th0, float tg0) {
+                                           float th0, float tg0, int l, int i, int o) {
   mm = fadd(mm, fmul(fsub(g, mm), s.c1));
   vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
   const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
   N.m[p] = mm;
   N.v[p] = vv;
   N.nb[p] = th;
-  write_packed(N.pk, N.t, p, th);
+  if (l >= 0) write_packed_w(N.pk, N.t, l, i, o, th);
   if (N.target) {
     const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
     N.target[p] = tg;
-    write_packed(N.tpk, N.t, p, tg);
+    if (l >= 0) write_packed_w(N.tpk, N.t, l, i, o, tg);
   }
 }
 
@@ -774,7 +787,7 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
   const int rem = item - N.ioff[l];
   const WgLayer& Ly = N.wg.l[l];
   const WgArgs& a = N.wg;
-  const AdamScalars s = adam_scalars(N.ad, step);
+  CSTAMP(1);
   if (rem < Ly.IT * Ly.OT) {
     const int it = rem / Ly.OT, ot = rem - it * Ly.OT;
     const int oc = 16 * ot + c;
@@ -794,48 +807,74 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
     }
     const float* ap = Ly.LT + (size_t)(16 * it + c) * a.ld + 4 * g;
     const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
+#ifdef CACTO_STAMPS
+    {  // diagnostic: latency of a first touch of this tile's panel rows (chunk 0), then the real loop
+      float4 t0 = *reinterpret_cast<const float4*>(ap + a.r_begin);
+      float4 t1 = *reinterpret_cast<const float4*>(bp + a.r_begin);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (t0.x == 12345.f && t1.y == 54321.f) N.m[0] = 0.f;
+    }
+    CSTAMP(5);
+#endif
+    // chunks in batches of CB: all their panel loads are in flight together (one latency per batch)
+    constexpr int CB = 4;
     floatx4 gs = {0.f, 0.f, 0.f, 0.f};
-    for (int ch = 0; ch < a.nch; ++ch) {
-      const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
-      float4 A[4], Bv[4];
+    for (int cb = 0; cb < a.nch; cb += CB) {
+      float4 A[CB][4], Bv[CB][4];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int r = min(lo + 16 * w, hi - 16);  // clamped (branch-free); unused past hi
-        A[w] = *reinterpret_cast<const float4*>(ap + r);
-        Bv[w] = *reinterpret_cast<const float4*>(bp + r);
-      }
-      floatx4 part[4];
+      for (int j = 0; j < CB; ++j) {
+        const int ch = min(cb + j, a.nch - 1);
+        const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        if (lo + 16 * w < hi) {
-          acc = mfma4(A[w].x, Bv[w].x, acc);
-          acc = mfma4(A[w].y, Bv[w].y, acc);
-          acc = mfma4(A[w].z, Bv[w].z, acc);
-          acc = mfma4(A[w].w, Bv[w].w, acc);
+        for (int w = 0; w < 4; ++w) {
+          const int r = min(lo + 16 * w, hi - 16);  // clamped (branch-free); unused past hi
+          A[j][w] = *reinterpret_cast<const float4*>(ap + r);
+          Bv[j][w] = *reinterpret_cast<const float4*>(bp + r);
         }
-        part[w] = acc;
       }
-      floatx4 s4 = part[0];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        s4[0] += part[w][0];
-        s4[1] += part[w][1];
-        s4[2] += part[w][2];
-        s4[3] += part[w][3];
-      }
-      if (ch == 0) {
-        gs = s4;
-      } else {
-        gs[0] += s4[0];
-        gs[1] += s4[1];
-        gs[2] += s4[2];
-        gs[3] += s4[3];
+      for (int j = 0; j < CB; ++j) {
+        const int ch = cb + j;
+        const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+        floatx4 part[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          if (lo + 16 * w < hi) {
+            acc = mfma4(A[j][w].x, Bv[j][w].x, acc);
+            acc = mfma4(A[j][w].y, Bv[j][w].y, acc);
+            acc = mfma4(A[j][w].z, Bv[j][w].z, acc);
+            acc = mfma4(A[j][w].w, Bv[j][w].w, acc);
+          }
+          part[w] = acc;
+        }
+        floatx4 s4 = part[0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+          s4[0] += part[w][0];
+          s4[1] += part[w][1];
+          s4[2] += part[w][2];
+          s4[3] += part[w][3];
+        }
+        if (ch == 0) {
+          gs = s4;
+        } else if (ch < a.nch) {
+          gs[0] += s4[0];
+          gs[1] += s4[1];
+          gs[2] += s4[2];
+          gs[3] += s4[3];
+        }
       }
     }
+    CSTAMP(2);
+#ifdef CACTO_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: the GEMM's results landed
+#endif
+    CSTAMP(3);
+    const AdamScalars s = adam_scalars(N.ad, step);  // after the loads are in flight
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (ok[q]) adam_apply(N, s, p[q], gs[q], mm[q], vv[q], th[q], tg[q]);
+      if (ok[q]) adam_apply(N, s, p[q], gs[q], mm[q], vv[q], th[q], tg[q], l, 16 * it + 4 * g + q, oc);
   } else {
     const int ot = rem - Ly.IT * Ly.OT;
     const int oc = 16 * ot + c;
@@ -843,39 +882,57 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
     const int pp = ok ? Ly.boff + oc : 0;
     const float mm = N.m[pp], vv = N.v[pp], th = N.src[pp], tg = N.target ? N.target[pp] : 0.f;
     const float* bp = Ly.RT + (size_t)(16 * min(ot, Ly.OT - 1) + c) * a.ld + 4 * g;
+    // per chunk: its (<= 4) 16-row steps from max(lo, bias_r0), summed in row order from 0 — the
+    // sequence k_wgrad's 64-row groups and 16-row tail produce — then the shuffles over g
+    constexpr int CB = 4;
     float gsum = 0.f;
-    for (int ch = 0; ch < a.nch; ++ch) {
-      const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
-      float sb = 0.f;
-      int r = max(lo, a.bias_r0);
-      for (; r + 64 <= hi; r += 64) {
-        float4 v4[4];
+    for (int cb = 0; cb < a.nch; cb += CB) {
+      float4 v4[CB][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v4[k] = *reinterpret_cast<const float4*>(bp + r + 16 * k);
+      for (int j = 0; j < CB; ++j) {
+        const int ch = min(cb + j, a.nch - 1);
+        const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+        const int r0 = max(lo, a.bias_r0);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) sb += (v4[k].x + v4[k].y) + (v4[k].z + v4[k].w);
+        for (int k = 0; k < 4; ++k) v4[j][k] = *reinterpret_cast<const float4*>(bp + max(0, min(r0 + 16 * k, hi - 16)));
       }
-      for (; r < hi; r += 16) {
-        const float4 v4 = *reinterpret_cast<const float4*>(bp + r);
-        sb += (v4.x + v4.y) + (v4.z + v4.w);
+#pragma unroll
+      for (int j = 0; j < CB; ++j) {
+        const int ch = cb + j;
+        const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+        const int r0 = max(lo, a.bias_r0);
+        float sb = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (r0 + 16 * k < hi) sb += (v4[j][k].x + v4[j][k].y) + (v4[j][k].z + v4[j][k].w);
+        sb += __shfl_xor(sb, 16);
+        sb += __shfl_xor(sb, 32);
+        if (ch == 0) gsum = sb;
+        else if (ch < a.nch) gsum = gsum + sb;
       }
-      sb += __shfl_xor(sb, 16);
-      sb += __shfl_xor(sb, 32);
-      gsum = ch == 0 ? sb : gsum + sb;
     }
-    if (ok) adam_apply(N, s, pp, gsum, mm, vv, th, tg);
+    const AdamScalars s = adam_scalars(N.ad, step);
+    if (ok) adam_apply(N, s, pp, gsum, mm, vv, th, tg, -1, 0, 0);
   }
 }
 
 // one or two networks (the union update runs the critic of update t and the actor of t - 1)
 __global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, int nnet, const int32_t* step) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  CSTAMP(0);
+  // the item is wave-uniform: readfirstlane lets the compiler keep the network descriptor in
+  // scalar registers (s_load from the kernel arguments) instead of chasing it through VGPR pointers
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + wave;
   if (item < n0.items) {
     wgrad_adam_item(n0, item, step, lane);
   } else if (nnet > 1 && item - n0.items < n1.items) {
     wgrad_adam_item(n1, item - n0.items, step, lane);
   }
+  CSTAMP(4);
+#ifdef CACTO_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int k_ = 0; k_ < 6; ++k_) g_cstamps[k_] = cacto_stamp_s[k_];
+#endif
 }
 
 }  // namespace cacto

@@ -180,6 +180,12 @@ constexpr int ZOFF[4] = {0, 4, 8, 16};  // critic hidden-layer tile offsets (64,
 // offsets ZOFF); otherwise h tiles alternate in H (2 x 8 tiles). With Cs != nullptr cos(z_l) is
 // kept too (24 tiles), so no later pass re-evaluates a transcendental. hook(l, ot, h4) runs for
 // every hidden out tile (l = 0..3). V[c] (LDS, 16 floats) receives the output for sample c.
+// The pass with its fragments already in registers (a chain kernel issues the loads of its first
+// pass before the row gathers, so their latency overlaps the gathers).
+template <typename Hook>
+__device__ void critic_forward_tile_f(const CriticFwdFrags& F, const NetView& N, const float4* X0, float4* Cs,
+                                      float4* Hs, float4* H, float4* red, float* V, const Lane& L, Hook&& hook);
+
 template <typename Hook>
 __device__ void critic_forward_tile(const NetView& N, const float4* X0, float4* Cs, float4* Hs, float4* H, float4* red,
                                     float* V, const Lane& L, Hook&& hook) {
@@ -191,6 +197,12 @@ __device__ void critic_forward_tile(const NetView& N, const float4* X0, float4* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PSTAMP(28);
 #endif
+  critic_forward_tile_f(F, N, X0, Cs, Hs, H, red, V, L, hook);
+}
+
+template <typename Hook>
+__device__ void critic_forward_tile_f(const CriticFwdFrags& F, const NetView& N, const float4* X0, float4* Cs,
+                                      float4* Hs, float4* H, float4* red, float* V, const Lane& L, Hook&& hook) {
   const float4* in = X0;
   auto epi = [&](int l, float4* out) {
     return [&, l, out](int ot, floatx4 acc) {
