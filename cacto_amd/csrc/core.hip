@@ -92,6 +92,11 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
     }
     s->actor = make_topo(CACTO_NET_ACTOR, p.nb_state, p.nb_action);
     s->critic = make_topo(CACTO_NET_CRITIC, p.nb_state, p.nb_action);
+    if (int rc = cacto_build_wgrad_adam_items(s)) {
+      (void)hipFree(s->dev);
+      delete s;
+      return rc;
+    }
     if (int rc = cacto_const_dyn_init(s)) {
       (void)hipFree(s->dev);
       delete s;
@@ -109,6 +114,8 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   if (!sys) return CACTO_OK;
   (void)hipFree(sys->dev);
   if (sys->ddp_ws) (void)hipFree(sys->ddp_ws);
+  for (int32_t* t : sys->wa_items)
+    if (t) (void)hipFree(t);
   if (sys->side) (void)hipStreamSynchronize(sys->side);
   if (sys->ev_critic) (void)hipEventDestroy(sys->ev_critic);
   for (hipEvent_t e : sys->ev_actor)

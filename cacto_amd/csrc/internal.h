@@ -15,6 +15,10 @@ struct cacto_sys {
   hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its two events
   hipEvent_t ev_critic = nullptr, ev_actor[2] = {nullptr, nullptr};
   std::mutex pipe_mu;  // one two-stream pipeline at a time per handle (they share side / events)
+  // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (net << 15 | item, -1 = none), for
+  // the critic alone, the actor alone and both (built at creation, cacto_build_wgrad_adam_items)
+  int32_t* wa_items[3] = {nullptr, nullptr, nullptr};
+  int wa_stride[3] = {0, 0, 0};
 };
 
 namespace cacto {
@@ -25,3 +29,4 @@ inline int64_t flat_span(const NetTopo& t) { return ((int64_t)t.params + 63) / 6
 
 cacto::NetView cacto_make_view(const cacto_sys* sys, int net, const float* netbuf);
 int cacto_const_dyn_init(cacto_sys* sys);  // SysDevice::cd_* of a prismatic-only chain (env_kernels.hip)
+int cacto_build_wgrad_adam_items(cacto_sys* sys);  // learn_kernels.hip

@@ -10,10 +10,14 @@
 //   actor rows : [0, Bp) = (h_l, zbar_l)
 //   -> k_wgrad: one wave per (layer, 16x16 output tile | bias tile, row chunk) -> slab[chunk][P]
 //   -> k_adam : sum chunks in fixed order (deterministic), Adam, packed copies, soft update.
+#include <algorithm>
+#include <vector>
+
 #include "net_common.h"
 
 #ifdef CACTO_STAMPS
 __device__ unsigned long long g_cstamps[32];
+__device__ unsigned long long g_astamps[32];  // actor chain, tile 0 (also inside the paired kernel)
 #define CSTAMP(k) PSTAMP(k)
 #define CSTAMP_DECL
 #define CSTAMP_FLUSH                                                                     \
@@ -398,7 +402,7 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   float4* HC = H;            // 16 tiles
   float4* ZB2 = H + 16 * 64;  // 16 tiles
   CSTAMP(4);
-  critic_forward_tile(C, XS, ZC, nullptr, HC, red, Vn, L, [](int, int, float4) {});
+  critic_forward_tile<false>(C, XS, ZC, nullptr, HC, red, Vn, L, [](int, int, float4) {});  // V(s') unused
   __syncthreads();
   CSTAMP(5);
   critic_first_backward(C, ZC, HC, nullptr, G0, red, L, [](int, int, int, float4) {});
@@ -453,6 +457,10 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   CSTAMP(9);
   __syncthreads();
   CSTAMP_FLUSH;
+#ifdef CACTO_STAMPS
+  if (tile == 0 && L.tid == 0)
+    for (int k_ = 0; k_ < 32; ++k_) g_astamps[k_] = cacto_stamp_s[k_];
+#endif
 }
 
 template <int NJ>
@@ -916,17 +924,21 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
   }
 }
 
-// one or two networks (the union update runs the critic of update t and the actor of t - 1)
-__global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, int nnet, const int32_t* step) {
+// One or two networks (the paired update runs the critic of update t and the actor of t - 1).
+// Work list: workgroup b runs on XCD b % 8 (the dispatcher's round robin; used for locality only,
+// nothing depends on it) and takes 4 items of that XCD's bin. The bins group the tiles of a layer
+// into blocks of in-tiles x out-tiles, so each XCD's L2 fetches a panel slice once for several
+// tiles instead of every XCD fetching every slice from the memory-side cache.
+__global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, const int32_t* __restrict__ items,
+                                                    int stride, const int32_t* step) {
   CSTAMP(0);
   // the item is wave-uniform: readfirstlane lets the compiler keep the network descriptor in
   // scalar registers (s_load from the kernel arguments) instead of chasing it through VGPR pointers
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int item = blockIdx.x * 4 + wave;
-  if (item < n0.items) {
-    wgrad_adam_item(n0, item, step, lane);
-  } else if (nnet > 1 && item - n0.items < n1.items) {
-    wgrad_adam_item(n1, item - n0.items, step, lane);
+  const int code = __builtin_amdgcn_readfirstlane(items[(blockIdx.x & 7) * stride + (blockIdx.x >> 3) * 4 + wave]);
+  if (code >= 0) {
+    if ((code >> 15) == 0) wgrad_adam_item(n0, code & 0x7fff, step, lane);
+    else wgrad_adam_item(n1, code & 0x7fff, step, lane);
   }
   CSTAMP(4);
 #ifdef CACTO_STAMPS
@@ -941,6 +953,11 @@ __global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, int 
 extern "C" int cacto_debug_critic_stamps(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipDeviceSynchronize());
   CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_cstamps), sizeof(unsigned long long) * 32));
+  return CACTO_OK;
+}
+extern "C" int cacto_debug_actor_stamps(unsigned long long* out_h) {
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_astamps), sizeof(unsigned long long) * 32));
   return CACTO_OK;
 }
 #endif
@@ -1194,9 +1211,12 @@ AdamNet actor_adam_net(const cacto_sys* sys, const cacto_nets* nets, const cacto
   return adam_net(sys, nets, cfg, CACTO_NET_ACTOR, w.act, 0, w.Bp, 0, 0, nullptr, nets->actor_d);
 }
 
-int launch_wgrad_adam(const AdamNet& n0, const AdamNet* n1, const int32_t* step, hipStream_t st) {
-  const int items = n0.items + (n1 ? n1->items : 0);
-  hipLaunchKernelGGL(k_wgrad_adam, dim3(ceil_div(items, 4)), dim3(256), 0, st, n0, n1 ? *n1 : n0, n1 ? 2 : 1, step);
+// mode 0: critic alone (n0), 1: actor alone (n0), 2: critic (n0) and actor (n1)
+int launch_wgrad_adam(const cacto_sys* sys, int mode, const AdamNet& n0, const AdamNet* n1, const int32_t* step,
+                      hipStream_t st) {
+  const int stride = sys->wa_stride[mode];
+  hipLaunchKernelGGL(k_wgrad_adam, dim3(8 * (stride / 4)), dim3(256), 0, st, n0, n1 ? *n1 : n0, sys->wa_items[mode],
+                     stride, step);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }
@@ -1205,7 +1225,7 @@ int launch_wgrad_adam(const AdamNet& n0, const AdamNet* n1, const int32_t* step,
 int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
                      hipStream_t st, const float* src, float* nb) {
   const int soft = cfg->MC ? 0 : 1;
-  if (fused_adam(w.Bp)) return launch_wgrad_adam(critic_adam_net(sys, nets, cfg, w, soft, src, nb), nullptr,
+  if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 0, critic_adam_net(sys, nets, cfg, w, soft, src, nb), nullptr,
                                                  nets->step_d, st);
   const bool sob = cfg->w_S != 0.0;
   WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
@@ -1218,7 +1238,7 @@ int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_u
 
 int actor_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
                     hipStream_t st) {
-  if (fused_adam(w.Bp)) return launch_wgrad_adam(actor_adam_net(sys, nets, cfg, w), nullptr, nets->step_d, st);
+  if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 1, actor_adam_net(sys, nets, cfg, w), nullptr, nets->step_d, st);
   WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
   hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
   CACTO_CHECK_HIP(hipGetLastError());
@@ -1226,6 +1246,55 @@ int actor_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
 }
 
 }  // namespace
+
+// k_wgrad_adam's XCD bins (see the kernel). Per layer the IT x OT weight tiles are cut into bi x bo
+// = 8 blocks (bi chosen so the blocks are as square as the tile grid allows), block k to bin k; a
+// layer's bias tiles go to the bin of their out-tile block. Item numbering is AdamNet's (per layer:
+// IT * OT weight tiles, row-major in (it, ot), then OT bias tiles).
+int cacto_build_wgrad_adam_items(cacto_sys* sys) {
+  std::vector<int32_t> bins[3][8];
+  const NetTopo* nets[2] = {&sys->critic, &sys->actor};
+  for (int mode = 0; mode < 3; ++mode) {
+    for (int n = 0; n < 2; ++n) {
+      if ((mode == 0 && n == 1) || (mode == 1 && n == 0)) continue;
+      const int tag = (mode == 2 && n == 1) ? 1 : 0;  // n1 in the paired launch
+      const NetTopo& t = *nets[n];
+      int base = 0;
+      for (int l = 0; l < t.L; ++l) {
+        const int IT = t.KT[l], OT = t.OT[l];
+        // bi x bo = 8 with the blocks (IT/bi) x (OT/bo) closest to square; both within the grid
+        int bi = 1;
+        double best = 1e30;
+        for (int c = 1; c <= 8; c *= 2) {
+          if (c > IT || 8 / c > OT) continue;
+          const double d = std::abs((double)IT / c - (double)OT / (8 / c));
+          if (d < best) best = d, bi = c;
+        }
+        if (best == 1e30) bi = std::max(1, std::min(IT, 8));  // grid smaller than 8 blocks
+        const int bo = std::max(1, 8 / bi);
+        for (int it = 0; it < IT; ++it)
+          for (int ot = 0; ot < OT; ++ot) {
+            const int bin = ((it * bi) / IT) * bo + std::min(bo - 1, (ot * bo) / OT);
+            bins[mode][bin % 8].push_back((tag << 15) | (base + it * OT + ot));
+          }
+        for (int ot = 0; ot < OT; ++ot) {
+          const int bin = std::min(bo - 1, (ot * bo) / OT);
+          bins[mode][bin % 8].push_back((tag << 15) | (base + IT * OT + ot));
+        }
+        base += IT * OT + OT;
+      }
+    }
+    size_t S = 4;
+    for (auto& b : bins[mode]) S = std::max(S, (b.size() + 3) / 4 * 4);
+    std::vector<int32_t> flat(8 * S, -1);
+    for (int x = 0; x < 8; ++x)
+      for (size_t k = 0; k < bins[mode][x].size(); ++k) flat[x * S + k] = bins[mode][x][k];
+    CACTO_CHECK_HIP(hipMalloc(&sys->wa_items[mode], flat.size() * sizeof(int32_t)));
+    CACTO_CHECK_HIP(hipMemcpy(sys->wa_items[mode], flat.data(), flat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    sys->wa_stride[mode] = (int)S;
+  }
+  return CACTO_OK;
+}
 
 extern "C" size_t cacto_workspace_bytes(const cacto_sys* sys, int B) {
   if (!sys || B <= 0) return 0;
@@ -1423,13 +1492,13 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
       if (int e = dispatch_nj<LaunchChainPair>(sys->host.p, sys, C, Tg, Ac, cs, storage_d, idx, isw, idx_prev, B, nct,
                                                w.crit, w.act, y, V, nets->step_d, st))
         return e;
-      if (int e = launch_wgrad_adam(cn, &an, nets->step_d, st)) return e;
+      if (int e = launch_wgrad_adam(sys, 2, cn, &an, nets->step_d, st)) return e;
     } else if (t < K) {
       if (int e = launch_critic_chain(sys, nets, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
-      if (int e = launch_wgrad_adam(cn, nullptr, nets->step_d, st)) return e;
+      if (int e = launch_wgrad_adam(sys, 0, cn, nullptr, nets->step_d, st)) return e;
     } else {
       if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx_prev, B, w, st)) return e;
-      if (int e = launch_wgrad_adam(an, nullptr, nets->step_d, st)) return e;
+      if (int e = launch_wgrad_adam(sys, 1, an, nullptr, nets->step_d, st)) return e;
     }
     if (per && t < K) {
       if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,

@@ -182,25 +182,26 @@ constexpr int ZOFF[4] = {0, 4, 8, 16};  // critic hidden-layer tile offsets (64,
 // every hidden out tile (l = 0..3). V[c] (LDS, 16 floats) receives the output for sample c.
 // The pass with its fragments already in registers (a chain kernel issues the loads of its first
 // pass before the row gathers, so their latency overlaps the gathers).
-template <typename Hook>
+// WANT_V = false: the pass only for its sin / cos tiles (the actor chain needs dV/ds', not V)
+template <bool WANT_V = true, typename Hook>
 __device__ void critic_forward_tile_f(const CriticFwdFrags& F, const NetView& N, const float4* X0, float4* Cs,
                                       float4* Hs, float4* H, float4* red, float* V, const Lane& L, Hook&& hook);
 
-template <typename Hook>
+template <bool WANT_V = true, typename Hook>
 __device__ void critic_forward_tile(const NetView& N, const float4* X0, float4* Cs, float4* Hs, float4* H, float4* red,
                                     float* V, const Lane& L, Hook&& hook) {
   CriticFwdFrags F;
   PSTAMP(27);
   F.load<true>(N, L);
-  F.load_last(N, L);
+  if (WANT_V) F.load_last(N, L);
 #ifdef CACTO_STAMPS_LOADWAIT
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PSTAMP(28);
 #endif
-  critic_forward_tile_f(F, N, X0, Cs, Hs, H, red, V, L, hook);
+  critic_forward_tile_f<WANT_V>(F, N, X0, Cs, Hs, H, red, V, L, hook);
 }
 
-template <typename Hook>
+template <bool WANT_V, typename Hook>
 __device__ void critic_forward_tile_f(const CriticFwdFrags& F, const NetView& N, const float4* X0, float4* Cs,
                                       float4* Hs, float4* H, float4* red, float* V, const Lane& L, Hook&& hook) {
   const float4* in = X0;
@@ -239,11 +240,13 @@ __device__ void critic_forward_tile_f(const CriticFwdFrags& F, const NetView& N,
   PSTAMP(23);
   __syncthreads();
   PSTAMP(24);
-  F.f4.run(8, out, red, L, N.biasp(4), [&](int, floatx4 acc) {
-    if (L.g == 0) V[L.c] = acc[0];
-  });
-  PSTAMP(25);
-  __syncthreads();
+  if (WANT_V) {
+    F.f4.run(8, out, red, L, N.biasp(4), [&](int, floatx4 acc) {
+      if (L.g == 0) V[L.c] = acc[0];
+    });
+    PSTAMP(25);
+    __syncthreads();
+  }
   PSTAMP(26);
 }
 
@@ -267,6 +270,7 @@ __device__ void actor_forward_tile(const NetView& N, int na, const float4* X0, f
       out[ot * 64 + L.lane] = h4;
       hook(l, ot, z4, h4);
     }, N.biasp(l), N.t.out[l]);
+    PSTAMP(10 + l);
     in = out;
   }
   layer(N.fwd(2), 1, N.t.KT[2], in, red, L, [&](int, floatx4 acc) {

@@ -56,9 +56,33 @@ def actor():
         L.lib().dll.cacto_debug_critic_stamps(st)
         t = np.array(st[:10], dtype=np.float64)
         print("actor B=%d total %.0f cycles: " % (B, t[9] - t[0]) + ", ".join("%s %.0f" % (n, x) for n, x in zip(names, np.diff(t))))
+        if st[10] > st[1] and st[11] > st[10]:
+            print("   actor forward: layer 1 %.0f, layer 2 %.0f, layer 3 %.0f" % (st[10] - st[1], st[11] - st[10], st[2] - st[11]))
+
+
+def pair():
+    """The actor chain inside the paired kernel (cacto_update_n at B <= 512), tile 0."""
+    conf, env, rl = bench.make_learner(sys.argv[2] if len(sys.argv) > 2 else "double_integrator")
+    rows = torch.randn(8192, 3 * conf.nb_state + 3, dtype=torch.float64, device="cuda") * 0.5
+    names = ["load", "actor_fwd", "dynamics", "fill", "critic_fwd", "critic_bwd1", "dQda", "actor_bwd_l2",
+             "actor_bwd_l1"]
+    for B in (64, 128):
+        idx = torch.randint(0, 8192, (3, B), dtype=torch.int32, device="cuda")
+        for _ in range(2):
+            rl.update_rows_n(rows, idx)
+        torch.cuda.synchronize()
+        st = (ctypes.c_ulonglong * 32)()
+        L.lib().dll.cacto_debug_actor_stamps(st)
+        t = np.array(st[:10], dtype=np.float64)
+        print("paired actor B=%d total %.0f cycles: " % (B, t[9] - t[0]) +
+              ", ".join("%s %.0f" % (n, x) for n, x in zip(names, np.diff(t))))
+        print("   actor forward: layer 1 %.0f, layer 2 %.0f, layer 3 %.0f" % (st[10] - st[1], st[11] - st[10], st[2] - st[11]))
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "pair":
+        pair()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "actor":
         actor()
         sys.exit(0)

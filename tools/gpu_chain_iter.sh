@@ -6,4 +6,6 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_graph.py tests/test_gpu_upd
 CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/critic_stamps.py > gpurun_out/stamps.log 2>&1 &&
 CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/critic_stamps.py actor double_integrator >> gpurun_out/stamps.log 2>&1 &&
 CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/critic_stamps.py actor manipulator >> gpurun_out/stamps.log 2>&1 &&
-timeout -k 10 300 python -u bench.py --steps 20 --no-cpu-baseline --no-diagnostics --no-config0 --extra-systems manipulator > gpurun_out/bench_upd.json 2> gpurun_out/bench_upd.err
+timeout -k 10 300 python -u bench.py --steps 20 --no-cpu-baseline --no-diagnostics --no-config0 --extra-systems manipulator > gpurun_out/bench_upd.json 2> gpurun_out/bench_upd.err &&
+CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/critic_stamps.py pair double_integrator >> gpurun_out/stamps.log 2>&1 &&
+CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/critic_stamps.py pair manipulator >> gpurun_out/stamps.log 2>&1
