@@ -20,7 +20,7 @@ python3 tools/prof_summary.py stats $D/b128/run_results.db > $D/kernel_stats_di_
 python3 tools/prof_summary.py stats $D/b4096/run_results.db > $D/kernel_stats_di_b4096.csv
 python3 tools/prof_summary.py pmc $D/fetch/run_results.db > $D/pmc_fetch.csv
 python3 tools/prof_summary.py pmc $D/write/run_results.db > $D/pmc_write.csv
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_rollout|k_critic_grad|k_actor_grad|k_wgrad" -d $D/mfma128 -o run -- python3 bench.py $PMCARGS --batches 128 > $D/mfma128.json 2> $D/mfma128.err
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_rollout|k_critic_grad|k_actor_grad|k_wgrad" -d $D/mfma4096 -o run -- python3 bench.py $PMCARGS --batches 4096 > $D/mfma4096.json 2> $D/mfma4096.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_rollout|k_critic_grad|k_actor_grad|k_wgrad|k_chain_pair" -d $D/mfma128 -o run -- python3 bench.py $PMCARGS --batches 128 > $D/mfma128.json 2> $D/mfma128.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_rollout|k_critic_grad|k_actor_grad|k_wgrad|k_chain_pair" -d $D/mfma4096 -o run -- python3 bench.py $PMCARGS --batches 4096 > $D/mfma4096.json 2> $D/mfma4096.err
 python3 tools/prof_summary.py pmc $D/mfma128/run_results.db > $D/pmc_mfma_b128.csv
 python3 tools/prof_summary.py pmc $D/mfma4096/run_results.db > $D/pmc_mfma_b4096.csv
