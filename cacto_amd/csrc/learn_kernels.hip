@@ -336,6 +336,8 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   const int ns = p.nb_state, na = p.nb_action, cols = 3 * ns + 3, s0 = tile * CACTO_TILE;
   const int ld = gb.ld;
   if (tile == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
+  Frag1<4> F1;  // actor layer 1 (ns -> 256), in flight during the row gathers
+  F1.load(Ac.fwd(0), Ac.biasp(0), L.wave, L.lane);
   {
     const int c = L.tid >> 4, f = L.tid & 15;
     const bool valid = s0 + c < B;
@@ -353,7 +355,7 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   CSTAMP(1);
   actor_forward_tile(Ac, na, X0, ZA, H, red, A, L, [&](int l, int ot, float4, float4 h4) {
     store_panel(gb.LT[l + 1], ld, s0 + L.c, ot, L.g, h4);
-  });
+  }, &F1);
   __syncthreads();
   CSTAMP(2);
   // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
@@ -413,6 +415,15 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
     const int c = L.tid >> 4, i = L.tid & 15;
     if (i < ns) gn[c * 16 + i] = normalize_backward(p, i, reinterpret_cast<const float*>(G0)[((i >> 2) * 16 + c) * 4 + (i & 3)]);
   }
+  // the two backward layers' first fragments, in flight during the rest of the dQ/da phase (W3^T:
+  // KT = 1, every tile; W2^T: the first tile's 16 blocks); issued after the loads above waited on
+  Frag1<4> B2;
+  FragTile<16> B1;
+  const bool wide = Ac.t.OT[2] == 1 && Ac.t.KT[2] == 4 * CACTO_NWAVES && Ac.t.KT[1] == 16 && Ac.t.OT[1] == 16;
+  if (wide) {
+    B2.load(Ac.bwd(2), nullptr, L.wave, L.lane);
+    B1.load(Ac.bwd(1), L.wave, L.lane);
+  }
   __syncthreads();
   if (L.wave == 0) {
     const int c = L.c;
@@ -437,7 +448,7 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   __syncthreads();
   CSTAMP(7);
   // zbar2 = (abar W3^T) * lrelu'(z2) ; zbar1 = (zbar2 W2^T) * lrelu'(z1)
-  layer(Ac.bwd(2), Ac.t.KT[2], Ac.t.OT[2], ZB3, red, L, [&](int it, floatx4 acc) {
+  auto epi2 = [&](int it, floatx4 acc) {
     const float4 z = ZA[(16 + it) * 64 + L.lane];
     const float zz[4] = {z.x, z.y, z.z, z.w};
     float o[4];
@@ -445,15 +456,25 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
     const float4 v = make_float4(o[0], o[1], o[2], o[3]);
     ZB2[it * 64 + L.lane] = v;
     store_panel(gb.RT[1], ld, s0 + L.c, it, L.g, v);
-  });
-  CSTAMP(8);
-  layer(Ac.bwd(1), Ac.t.KT[1], Ac.t.OT[1], ZB2, red, L, [&](int it, floatx4 acc) {
+  };
+  auto epi1 = [&](int it, floatx4 acc) {
     const float4 z = ZA[it * 64 + L.lane];
     const float zz[4] = {z.x, z.y, z.z, z.w};
     float o[4];
     for (int r = 0; r < 4; ++r) o[r] = zz[r] > 0.f ? acc[r] : fmul(acc[r], 0.3f);
     store_panel(gb.RT[0], ld, s0 + L.c, it, L.g, make_float4(o[0], o[1], o[2], o[3]));
-  });
+  };
+  if (wide) {
+    mm_layer1_pre<4>(B2, ZB3, L.wave, L.lane, epi2, nullptr);
+    __syncthreads();
+    CSTAMP(8);
+    mm_layer_t_pre<16>(B1, Ac.bwd(1), 16, ZB2, L.wave, L.lane, epi1);
+    __syncthreads();
+  } else {
+    layer(Ac.bwd(2), Ac.t.KT[2], Ac.t.OT[2], ZB3, red, L, epi2);
+    CSTAMP(8);
+    layer(Ac.bwd(1), Ac.t.KT[1], Ac.t.OT[1], ZB2, red, L, epi1);
+  }
   CSTAMP(9);
   __syncthreads();
   CSTAMP_FLUSH;

@@ -189,6 +189,78 @@ struct Frags {
   }
 };
 
+// Preloaded fragments (a caller issues them a phase early, so the L2 latency hides behind other
+// work; the in-order vmcnt means they should be issued after any load the intervening phase waits
+// for). Same arithmetic as mm_layer_t.
+//   KT == 1 layers (OT = 4 * NT): every out tile's single fragment block and bias, no loads inside.
+template <int NT>
+struct Frag1 {
+  float4 a[NT], b[NT];
+  __device__ __forceinline__ void load(const float4* __restrict__ A, const float* __restrict__ bias, int wave,
+                                       int lane) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      a[t] = A[(size_t)(wave + CACTO_NWAVES * t) * 64 + lane];
+      b[t] = tile_bias(bias, wave + CACTO_NWAVES * t, lane);
+    }
+  }
+};
+template <int NT, typename Epi>
+__device__ __forceinline__ void mm_layer1_pre(const Frag1<NT>& F, const float4* X, int wave, int lane, Epi&& epi,
+                                              const float* __restrict__ bias) {
+  const float4 x = X[lane];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+    c0 = mfma4(F.a[t].x, x.x, c0);
+    c1 = mfma4(F.a[t].y, x.y, c1);
+    c2 = mfma4(F.a[t].z, x.z, c2);
+    c3 = mfma4(F.a[t].w, x.w, c3);
+    epi(wave + CACTO_NWAVES * t, add_bias((c0 + c1) + (c2 + c3), bias, F.b[t]));
+  }
+}
+//   the first out tile's KT fragment blocks (no bias), for mm_layer_t_pre below
+template <int KT>
+struct FragTile {
+  float4 a[KT];
+  __device__ __forceinline__ void load(const float4* __restrict__ A, int wave, int lane) {
+#pragma unroll
+    for (int k = 0; k < KT; ++k) a[k] = A[((size_t)wave * KT + k) * 64 + lane];
+  }
+};
+// mm_layer_t (no bias) with the first tile's fragments preloaded
+template <int KT, typename Epi>
+__device__ __forceinline__ void mm_layer_t_pre(const FragTile<KT>& F0, const float4* __restrict__ A, int OT,
+                                               const float4* X, int wave, int lane, Epi&& epi) {
+  int ot = wave;
+  if (ot >= OT) return;
+  float4 a[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) a[k] = F0.a[k];
+  while (true) {
+    const int nxt = ot + CACTO_NWAVES;
+    float4 an[KT];
+    if (nxt < OT) {
+#pragma unroll
+      for (int k = 0; k < KT; ++k) an[k] = A[((size_t)nxt * KT + k) * 64 + lane];
+    }
+    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const float4 b = X[k * 64 + lane];
+      c0 = mfma4(a[k].x, b.x, c0);
+      c1 = mfma4(a[k].y, b.y, c1);
+      c2 = mfma4(a[k].z, b.z, c2);
+      c3 = mfma4(a[k].w, b.w, c3);
+    }
+    epi(ot, (c0 + c1) + (c2 + c3));
+    if (nxt >= OT) break;
+    ot = nxt;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) a[k] = an[k];
+  }
+}
+
 template <typename Epi>
 __device__ __forceinline__ void mm_layer(const float4* __restrict__ A, int OT, int KT, const float4* X, int wave,
                                          int lane, Epi&& epi, const float* __restrict__ bias = nullptr) {

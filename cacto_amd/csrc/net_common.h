@@ -252,13 +252,14 @@ __device__ void critic_forward_tile_f(const CriticFwdFrags& F, const NetView& N,
 
 // Actor forward; Z1/Z2 (16 tiles each) kept when non-null, h tiles in H (2 x 16 tiles).
 // A[c * na + f] (LDS) receives the action.
+// F1 (optional): layer 1's fragments preloaded (the 256-wide first layer: KT = 1, OT = 16).
 template <typename Hook>
 __device__ void actor_forward_tile(const NetView& N, int na, const float4* X0, float4* Z, float4* H, float4* red,
-                                   float* A, const Lane& L, Hook&& hook) {
+                                   float* A, const Lane& L, Hook&& hook, const Frag1<4>* F1 = nullptr) {
   const float4* in = X0;
   for (int l = 0; l < 2; ++l) {
     float4* out = H + l * 16 * 64;
-    layer(N.fwd(l), N.t.OT[l], N.t.KT[l], in, red, L, [&](int ot, floatx4 acc) {
+    auto epi = [&](int ot, floatx4 acc) {
       float z[4], h[4];
       for (int r = 0; r < 4; ++r) {
         z[r] = acc[r];  // x W + b
@@ -269,7 +270,13 @@ __device__ void actor_forward_tile(const NetView& N, int na, const float4* X0, f
       if (Z) Z[(l * 16 + ot) * 64 + L.lane] = z4;
       out[ot * 64 + L.lane] = h4;
       hook(l, ot, z4, h4);
-    }, N.biasp(l), N.t.out[l]);
+    };
+    if (l == 0 && F1 && N.t.KT[0] == 1 && N.t.OT[0] == 4 * CACTO_NWAVES) {
+      mm_layer1_pre<4>(*F1, in, L.wave, L.lane, epi, N.biasp(0));
+      __syncthreads();
+    } else {
+      layer(N.fwd(l), N.t.OT[l], N.t.KT[l], in, red, L, epi, N.biasp(l), N.t.out[l]);
+    }
     PSTAMP(10 + l);
     in = out;
   }
