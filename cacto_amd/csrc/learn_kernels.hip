@@ -790,6 +790,14 @@ __device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int
   return s;
 }
 
+// k_adam's per-parameter arithmetic (same ops, same order), values only
+__device__ __forceinline__ void adam_math(const AdamScalars& s, float g, float& mm, float& vv, float& th, float& tg) {
+  mm = fadd(mm, fmul(fsub(g, mm), s.c1));
+  vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
+  th = fsub(th, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
+  tg = fadd(fmul(th, s.tau), fmul(tg, s.omt));
+}
+
 // k_adam's per-parameter arithmetic (same ops, same order); l >= 0: a weight W_l[i][o] (direct
 // packed writes), l < 0: a bias (not packed)
 __device__ __forceinline__ void adam_apply(const AdamNet& N, const AdamScalars& s, int p, float g, float mm, float vv,
@@ -809,7 +817,7 @@ __device__ __forceinline__ void adam_apply(const AdamNet& N, const AdamScalars& 
 }
 
 __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, const int32_t* __restrict__ step,
-                                                int lane) {
+                                                int lane, float* tr) {
   const int g = lane >> 4, c = lane & 15;
   int l = 0;
   while (item >= N.ioff[l + 1]) ++l;
@@ -820,19 +828,36 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
   if (rem < Ly.IT * Ly.OT) {
     const int it = rem / Ly.OT, ot = rem - it * Ly.OT;
     const int oc = 16 * ot + c;
+    // A full 16 x 16 tile runs Adam in the row layout: lane (g, c) owns W[16 it + c][16 ot + 4g + j],
+    // 4 consecutive Keras-flat parameters (float4 loads / stores; the pkT block is this layout and
+    // the pk block the MFMA's C layout, one LDS transpose away). Edge tiles: per element.
+    const bool full = 16 * it + 16 <= Ly.in && 16 * ot + 16 <= Ly.out;
+    const int pT = Ly.woff + (16 * it + c) * Ly.out + 16 * ot + 4 * g;
     // Adam operands of the lane's 4 parameters, in flight during the GEMM
     int p[4];
     float mm[4], vv[4], th[4], tg[4];
     bool ok[4];
+    if (full) {
+      const float4 m4 = *reinterpret_cast<const float4*>(N.m + pT), v4 = *reinterpret_cast<const float4*>(N.v + pT);
+      const float4 t4 = *reinterpret_cast<const float4*>(N.src + pT);
+      const float4 g4 = N.target ? *reinterpret_cast<const float4*>(N.target + pT) : make_float4(0.f, 0.f, 0.f, 0.f);
+      mm[0] = m4.x, mm[1] = m4.y, mm[2] = m4.z, mm[3] = m4.w;
+      vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
+      th[0] = t4.x, th[1] = t4.y, th[2] = t4.z, th[3] = t4.w;
+      tg[0] = g4.x, tg[1] = g4.y, tg[2] = g4.z, tg[3] = g4.w;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ii = 16 * it + 4 * g + q;
-      ok[q] = ii < Ly.in && oc < Ly.out;
-      p[q] = ok[q] ? Ly.woff + ii * Ly.out + oc : 0;
-      mm[q] = N.m[p[q]];
-      vv[q] = N.v[p[q]];
-      th[q] = N.src[p[q]];
-      tg[q] = N.target ? N.target[p[q]] : 0.f;
+      for (int q = 0; q < 4; ++q) ok[q] = true, p[q] = pT + q;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ii = 16 * it + 4 * g + q;
+        ok[q] = ii < Ly.in && oc < Ly.out;
+        p[q] = ok[q] ? Ly.woff + ii * Ly.out + oc : 0;
+        mm[q] = N.m[p[q]];
+        vv[q] = N.v[p[q]];
+        th[q] = N.src[p[q]];
+        tg[q] = N.target ? N.target[p[q]] : 0.f;
+      }
     }
     const float* ap = Ly.LT + (size_t)(16 * it + c) * a.ld + 4 * g;
     const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
@@ -901,9 +926,46 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
 #endif
     CSTAMP(3);
     const AdamScalars s = adam_scalars(N.ad, step);  // after the loads are in flight
+    if (full) {
+      // gradient C layout -> row layout through the wave's LDS scratch (LDS operations of one wave
+      // complete in order; the wave-scope fence keeps the compiler from reordering across lanes)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (ok[q]) adam_apply(N, s, p[q], gs[q], mm[q], vv[q], th[q], tg[q], l, 16 * it + 4 * g + q, oc);
+      for (int q = 0; q < 4; ++q) tr[(4 * g + q) * 16 + c] = gs[q];
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const float4 gT = *reinterpret_cast<const float4*>(tr + c * 16 + 4 * g);
+      const float gv[4] = {gT.x, gT.y, gT.z, gT.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) adam_math(s, gv[j], mm[j], vv[j], th[j], tg[j]);
+      *reinterpret_cast<float4*>(N.m + pT) = make_float4(mm[0], mm[1], mm[2], mm[3]);
+      *reinterpret_cast<float4*>(N.v + pT) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      const float4 th4 = make_float4(th[0], th[1], th[2], th[3]);
+      *reinterpret_cast<float4*>(N.nb + pT) = th4;
+      const NetTopo& t = N.t;
+      const size_t bT = (size_t)(t.blocks + t.pkoff[l] + it * t.OT[l] + ot) * 64 + lane;  // pkT block (it, ot)
+      const size_t bF = (size_t)(t.pkoff[l] + ot * t.KT[l] + it) * 64 + lane;             // pk block (ot, it)
+      N.pk[bT] = th4;
+      auto to_c = [&](const float (&v)[4]) {  // row layout -> C layout (the pk block)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tr[c * 16 + 4 * g + j] = v[j];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = tr[(4 * g + q) * 16 + c];
+        return make_float4(o[0], o[1], o[2], o[3]);
+      };
+      N.pk[bF] = to_c(th);
+      if (N.target) {
+        const float4 tg4 = make_float4(tg[0], tg[1], tg[2], tg[3]);
+        *reinterpret_cast<float4*>(N.target + pT) = tg4;
+        N.tpk[bT] = tg4;
+        N.tpk[bF] = to_c(tg);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (ok[q]) adam_apply(N, s, p[q], gs[q], mm[q], vv[q], th[q], tg[q], l, 16 * it + 4 * g + q, oc);
+    }
   } else {
     const int ot = rem - Ly.IT * Ly.OT;
     const int oc = 16 * ot + c;
@@ -957,9 +1019,10 @@ __global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, cons
   // scalar registers (s_load from the kernel arguments) instead of chasing it through VGPR pointers
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int code = __builtin_amdgcn_readfirstlane(items[(blockIdx.x & 7) * stride + (blockIdx.x >> 3) * 4 + wave]);
+  __shared__ float tr[4][256];  // per wave: one 16 x 16 transpose
   if (code >= 0) {
-    if ((code >> 15) == 0) wgrad_adam_item(n0, code & 0x7fff, step, lane);
-    else wgrad_adam_item(n1, code & 0x7fff, step, lane);
+    if ((code >> 15) == 0) wgrad_adam_item(n0, code & 0x7fff, step, lane, tr[wave]);
+    else wgrad_adam_item(n1, code & 0x7fff, step, lane, tr[wave]);
   }
   CSTAMP(4);
 #ifdef CACTO_STAMPS
