@@ -61,6 +61,8 @@ def parse():
                    help="skip BASELINE configs[0] (single integrator, one main.py training iteration, GPU vs CPU)")
     p.add_argument("--no-diagnostics", action="store_true",
                    help="skip the rollout variants (profiling runs: every k_rollout dispatch is a full rollout)")
+    p.add_argument("--long-steps", type=int, default=1000,
+                   help="rollout batches of the long robustness region reported beside the K-step value")
     return p.parse_args()
 
 
@@ -206,10 +208,32 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     # the timed region in 5 consecutive segments (HIP events at their boundaries): per-segment rate
     # and the median of the 5, beside the whole-region value
     seg = segments([(e[0], e[2]) for e in evs], steps_per_call)
+    # robustness check beside the contract's K-step region (the driver runs K = 20, ~16 ms): a long
+    # region of max(K, LONG_STEPS) rollout batches, as 5 consecutive segments, median reported
+    long_k = max(K, LONG_STEPS) if LONG_STEPS > 0 else 0
+    if long_k < 5:
+        return dict(out=out, S0=S0, nsteps=nsteps, T=T, wall=wall, kernel_ms=kern_ms, seq_kernel_ms=seq_ms,
+                    seq_kernel_ms_median=float(np.median([e[0].elapsed_time(e[1]) for e in evs])),
+                    rewards_kernel_ms=kern_ms - seq_ms, steps_per_call=steps_per_call,
+                    total_steps=sum_over_ranks(steps_per_call * K, world), segments=seg, long_region=None)
+    lev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    cuts = [j * long_k // 5 for j in range(6)]
+    barrier(world)
+    lev[0].record()
+    for j in range(5):
+        for _ in range(cuts[j + 1] - cuts[j]):
+            rl.rollout_batch(None, None, T, inputs=inputs, out=seq)
+            rl.rollout_rewards(out, n_d, T)
+        lev[j + 1].record()
+    torch.cuda.synchronize()
+    rates = [steps_per_call * (cuts[j + 1] - cuts[j]) / (lev[j].elapsed_time(lev[j + 1]) * 1e-3) for j in range(5)]
+    long_region = dict(batches=long_k, seconds=lev[0].elapsed_time(lev[5]) * 1e-3, segment_rates=rates,
+                       median=sum_over_ranks(float(np.median(rates)), world),
+                       spread=float((max(rates) - min(rates)) / np.median(rates)))
     return dict(out=out, S0=S0, nsteps=nsteps, T=T, wall=wall, kernel_ms=kern_ms, seq_kernel_ms=seq_ms,
                 seq_kernel_ms_median=float(np.median([e[0].elapsed_time(e[1]) for e in evs])),
                 rewards_kernel_ms=kern_ms - seq_ms, steps_per_call=steps_per_call,
-                total_steps=sum_over_ranks(steps_per_call * K, world), segments=seg)
+                total_steps=sum_over_ranks(steps_per_call * K, world), segments=seg, long_region=long_region)
 
 
 def segments(pairs, units_per_item, n=5):
@@ -462,6 +486,7 @@ def extra_system(name, args, world, rank):
                                mfma_frac=flop * args.update_steps / wall / (FP32_MFMA_PEAK * world))
     return dict(config=cfg["config"], env_steps_per_s=r["total_steps"] / r["wall"], rollouts_per_gpu=cfg["R"],
                 rollout_kernel_ms=r["kernel_ms"], env_steps_per_launch=r["steps_per_call"], segments=r["segments"],
+                long_region=r["long_region"],
                 rollout_mfma_frac=r["steps_per_call"] * fa_flops(ns, na) / (r["seq_kernel_ms"] * 1e-3) /
                 FP32_MFMA_PEAK,
                 w_S=cfg["w_S"], per=cfg["per"], critic_updates=ups, ddp_labels=ddp)
@@ -612,12 +637,14 @@ def config0(args, rank, cpu_updates):
 
 
 USE_GRAPH = False
+LONG_STEPS = 1000
 
 
 def main():
-    global USE_GRAPH
+    global USE_GRAPH, LONG_STEPS
     args = parse()
     USE_GRAPH = args.graph
+    LONG_STEPS = args.long_steps
     world, rank = init_dist()
     torch.backends.cuda.matmul.allow_tf32 = False
     conf, env, rl = make_learner(args.system)
@@ -674,6 +701,7 @@ def main():
                        "env_steps_per_rollout_batch": roll["steps_per_call"], "T_max": roll["T"],
                        "parallelism": "dp%d" % world},
             "segments": roll["segments"],
+            "long_region": roll["long_region"],
             "roofline": {"kernel": "k_rollout", "bound": "mfma", "achieved": achieved / 1e12,
                          "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

@@ -105,10 +105,8 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
   const int goff[4] = {0, 0, 4, 8};
   if (tile == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
 
-  // the target network's fragments for the first pass, in flight during the row gathers
+  // the target network's fragments for the first pass (loaded during the row gathers, below)
   CriticFwdFrags TF;
-  TF.load<true>(Tg, L);
-  TF.load_last(Tg, L);
   float4 w5[2];  // W5[:, 0] at this lane's rows of layer-3 out tiles wave, wave + 4
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -122,7 +120,12 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
     const int c = L.tid >> 4, f = L.tid & 15;
     const bool valid = s0 + c < B, in = valid && f < ns;
     const int sc = min(s0 + c, B - 1), fc = min(f, ns - 1);
-    const double* rp = storage + (size_t)idx[sc] * cols;
+    const int32_t row = idx[sc];
+    // issued between the index load and the dependent row loads: the wait for the index (in-order
+    // vmcnt) does not cover them, and they have both latencies to land
+    TF.load<true>(Tg, L);
+    TF.load_last(Tg, L);
+    const double* rp = storage + (size_t)row * cols;
     const double x = rp[fc], xn = rp[ns + 1 + fc], xd = rp[2 * ns + 1 + fc];
     const double r = rp[ns], d = rp[3 * ns + 1];
     const float wv = isw ? isw[sc] : 1.f;

@@ -5,6 +5,10 @@ import sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 r = d["roofline"]
 print("DI rollout %.1f M env-steps/s  k_rollout %.3f ms  frac %.3f" % (d["value"] / 1e6, r["kernel_ms"], r["frac"]))
+if d.get("long_region"):
+    lr = d["long_region"]
+    print("  long region: %d batches, %.2f s, median %.1f M/s, spread %.3f" % (lr["batches"], lr["seconds"],
+                                                                             lr["median"] / 1e6, lr["spread"]))
 for k, v in d["critic_updates"].items():
     print("  DI %s: %.0f updates/s (%.1f us) mfma %.3f" % (k, v["value"], v["ms_per_update"] * 1e3, v["mfma_frac"]))
 for s, e in (d.get("extra_systems") or {}).items():

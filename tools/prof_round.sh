@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 R=$1
 D=gpurun_out/prof_$R
 mkdir -p $D
-SMALL="--no-cpu-baseline --no-diagnostics --no-config0"
+SMALL="--no-cpu-baseline --no-diagnostics --no-config0 --long-steps 0"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/trace -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 200 $SMALL > $D/bench_under_rocprof.json 2> $D/trace.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/b128 -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 1000 --batches 128 --extra-systems "" $SMALL > $D/b128.json 2> $D/b128.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/b4096 -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 1000 --batches 4096 --extra-systems "" $SMALL > $D/b4096.json 2> $D/b4096.err
