@@ -164,8 +164,10 @@ class RL_AC:
     dp_group = None
 
     def set_data_parallel(self, world_size, group=None):
-        """Replicated weights, local minibatch per rank, RCCL all-reduce of both gradients (the
-        critic's before its Adam step, then the actor's against the updated critic, RL.py:104-109)."""
+        """Replicated weights, local minibatch per rank, RCCL all-reduce of the gradients: one
+        all-reduce per update of [critic gradient of update t | actor gradient of update t-1]
+        (dp_pipeline), which keeps RL.py:104-109's order (the actor gradient is taken against the
+        critic after its own update)."""
         self.dp_world = int(world_size)
         self.dp_group = group
 

@@ -93,6 +93,23 @@ def _update_worker(rank, port, rows, idx, q):
         dist.destroy_process_group()
 
 
+def _isw_worker(rank, port, rows, idx, wts, q):
+    dist = _init(rank, port)
+    try:
+        rl = _learner(WORLD)
+        storage = torch.as_tensor(rows, device="cuda")
+        y = torch.empty(B_LOCAL, dtype=torch.float32, device="cuda")
+        V = torch.empty_like(y)
+        for k in range(K):
+            sl = slice(rank * B_LOCAL, (rank + 1) * B_LOCAL)
+            rl.update_rows(storage, torch.as_tensor(idx[k, sl].astype(np.int32), device="cuda"),
+                           torch.as_tensor(wts[k, sl], device="cuda"), y, V)
+        torch.cuda.synchronize()
+        q.put((rank, _state(rl), y.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
 def _per_worker(rank, port, q):
     dist = _init(rank, port)
     try:
@@ -193,3 +210,35 @@ def test_dp_per_shards_on_gpu_match_oracle():
         ow = o.sample_weights_global(oidx, stats)
         np.testing.assert_allclose(w, ow.astype(np.float32), rtol=1e-6)
         np.testing.assert_array_equal(cnt, o.exp_counter[:len(cnt)])
+
+
+def test_dp_update_with_is_weights_on_gpu():
+    """The data-parallel update with per-sample IS weights (the PER path of learn_and_update,
+    replay_buffer.py:159-188 weights into NeuralNetwork.py:167-173): equals a single-rank weighted
+    update at the global batch, replicas bit-identical, and each rank's y / V outputs are its own
+    samples' (the priority update reads them)."""
+    rng = np.random.default_rng(71)
+    N = 4096
+    rows = _rows(N, 70)
+    idx = rng.integers(0, N, size=(K, WORLD * B_LOCAL))
+    wts = rng.uniform(0.2, 1.0, size=(K, WORLD * B_LOCAL)).astype(np.float32)
+    res = _spawn(_isw_worker, lambda r: (rows, idx, wts))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert np.array_equal(a, b)
+    single = _learner(1)
+    storage = torch.as_tensor(rows, device="cuda")
+    y = torch.empty(WORLD * B_LOCAL, dtype=torch.float32, device="cuda")
+    V = torch.empty_like(y)
+    for k in range(K):
+        single.update_rows(storage, torch.as_tensor(idx[k].astype(np.int32), device="cuda"),
+                           torch.as_tensor(wts[k], device="cuda"), y, V)
+    torch.cuda.synchronize()
+    ref = _state(single)
+    for name, a, b in zip(("actor", "critic", "target"), res[0][0][:3], ref[:3]):
+        P = single.actor_model.P if name == "actor" else single.critic_model.P
+        assert np.abs(a[:P] - b[:P]).max() < 5e-6 * K, name
+    # y of the last update: rank r's half of the global batch (y depends only on the target critic
+    # and the rows, identical on every rank and in the single-rank run up to the target's rounding)
+    yg = y.cpu().numpy()
+    for r in range(WORLD):
+        np.testing.assert_allclose(res[r][1], yg[r * B_LOCAL:(r + 1) * B_LOCAL], rtol=1e-5, atol=1e-5)

@@ -97,11 +97,15 @@ def test_graph_replay_equals_eager_updates_with_per():
 @pytest.mark.parametrize("system,B,K,MC", [("double_integrator", 128, 7, 0), ("double_integrator", 1000, 7, 0),
                                          ("manipulator", 64, 7, 0), ("double_integrator", 128, 1, 0),
                                          ("double_integrator", 128, 2, 0), ("double_integrator", 128, 8, 0),
-                                         ("double_integrator", 128, 8, 1), ("double_integrator", 256, 3, 1)])
+                                         ("double_integrator", 128, 8, 1), ("double_integrator", 256, 3, 1),
+                                         ("car_park", 200, 5, 0), ("double_integrator", 512, 3, 0),
+                                         ("double_integrator", 520, 2, 0), ("ur5", 48, 3, 0)])
 def test_pipelined_updates_equal_sequential(system, B, K, MC):
-    """cacto_update_n overlaps critic(t+1) with actor(t) on two streams; the result is the same bits.
-    Odd K ends with the critic in the workspace copy (copied back), even K in the caller's buffer;
-    K = 1, 2 finish before the first two-updates-old wait; MC = 1 has no soft target update."""
+    """cacto_update_n overlaps critic(t+1) with actor(t): for B <= 512 as one paired grid per step on
+    one stream, above on two streams; either way the result is the same bits. Two streams: odd K
+    ends with the critic in the workspace copy (copied back), even K in the caller's buffer; K = 1, 2
+    finish before the first two-updates-old wait. MC = 1 has no soft target update. B = 200 and 48
+    leave a partial last tile; 512 / 520 sit either side of the paired / two-stream threshold."""
     conf = load_conf(system, fresh=True)
     conf.MC = MC
     env = make_env(conf)
@@ -116,7 +120,7 @@ def test_pipelined_updates_equal_sequential(system, B, K, MC):
     idx = torch.as_tensor(rng.integers(0, N, size=(K, B)).astype(np.int32), device="cuda")
 
     def learner():
-        rl = RL_AC(env, NN(env, conf, w_S=1e-2 if system == "double_integrator" else 0.0, seed=3), conf)
+        rl = RL_AC(env, NN(env, conf, w_S=1e-2 if system in ("double_integrator", "ur5") else 0.0, seed=3), conf)
         rl.setup_model()
         return rl
     seq = learner()
