@@ -59,7 +59,7 @@ __device__ __forceinline__ floatx4 mfma_bc(float x, float w, floatx4 c) {
 template <int NJ, int NG>
 struct RoSplit {
   static constexpr int REGK = NJ <= 2 ? 192 : NJ == 3 ? (NG == 4 ? 160 : 128) : NG == 4 ? 48 : 64;
-  static constexpr int LDSK = NJ <= 2 ? 64 : NJ == 3 ? (NG == 4 ? 96 : 128) : NG == 4 ? 80 : 64;
+  static constexpr int LDSK = NJ <= 2 ? 64 : NJ == 3 ? (NG == 4 ? 96 : 128) : NG == 4 ? 80 : 112;
   static_assert(REGK % 16 == 0 && LDSK % 16 == 0 && REGK + LDSK <= 256, "row split");
 };
 
