@@ -608,8 +608,12 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
       if constexpr (NJ > 0) {
         if (L.wave == 0 && active) {
           ro_chain_nle<NJ, SL>(sd, Sh.ch, c, Sh.sS + c * ns, Sh.sS + c * ns + NJ, Sh.hS + c);
+          RSTAMP(9);
         } else if (L.wave == 3 && active) {
           ro_chain_mass<NJ, SL>(sd, Sh.ch, c, Sh.MS + c);
+#ifdef CACTO_STAMPS
+          if (blockIdx.x == 0 && L.lane == 0 && it == 20) g_rstamps[10] = __builtin_amdgcn_s_memtime();
+#endif
         }
       }
       __syncthreads();
