@@ -240,14 +240,12 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
 // Chain dynamics workspace of the rollout, structure of arrays [joint][component][slot] (slot
 // fastest: the slot lanes of a wave read consecutive doubles). The joint placements X(q_i) of every
 // (slot, joint) are computed in parallel by all threads; the RNEA and CRBA recursions then read
-// them (and park their per-joint forces / composite inertias) here instead of holding NJ of each
-// in registers — a 6-joint chain in float64 would otherwise not fit beside the actor.
+// them (and the RNEA parks its per-joint forces) here instead of holding NJ of each in registers — a 6-joint chain in float64 would otherwise not fit beside the actor.
 template <int NJ, int SL>
 struct RoChain {
   static constexpr int J = NJ > 0 ? NJ : 1;
   double X[J * 12 * SL];   // SE3: R (9, row-major), p (3)
   double f[J * 6 * SL];    // RNEA forces: l (3), a (3)
-  double Ic[J * 10 * SL];  // CRBA composite inertias: m, h (3), Io (6)
 };
 
 template <int SL>
@@ -275,22 +273,6 @@ template <int SL>
 __device__ __forceinline__ SV sv_ld(const double* b) {
   return SV{v3(b[0], b[SL], b[2 * SL]), v3(b[3 * SL], b[4 * SL], b[5 * SL])};
 }
-template <int SL>
-__device__ __forceinline__ void inertia_st(double* b, const Inertia& I) {
-  b[0] = I.m;
-  b[SL] = I.h.x, b[2 * SL] = I.h.y, b[3 * SL] = I.h.z;
-  b[4 * SL] = I.Io.xx, b[5 * SL] = I.Io.xy, b[6 * SL] = I.Io.xz;
-  b[7 * SL] = I.Io.yy, b[8 * SL] = I.Io.yz, b[9 * SL] = I.Io.zz;
-}
-template <int SL>
-__device__ __forceinline__ Inertia inertia_ld(const double* b) {
-  Inertia I;
-  I.m = b[0];
-  I.h = v3(b[SL], b[2 * SL], b[3 * SL]);
-  I.Io = S3{b[4 * SL], b[5 * SL], b[6 * SL], b[7 * SL], b[8 * SL], b[9 * SL]};
-  return I;
-}
-
 // X(q_i) of every active (slot, joint): item e -> slot e % SL, joint e / SL, spread over the waves.
 template <int NJ, int SL>
 __device__ __forceinline__ void ro_placements(const SysDevice& sd, RoChain<NJ, SL>& C, const double* sS,
@@ -349,32 +331,46 @@ __device__ __forceinline__ void ro_chain_nle(const SysDevice& sd, RoChain<NJ, SL
   }
 }
 
-// chain_mass (env.h) from the workspace placements; M written to Mout[k * SL] (k = row-major
-// index). Same operations in the same order.
+// chain_mass (env.h) from the workspace placements, split by columns over waves 1-3: column i of
+// M needs the composite inertia Ic_i = I_i + X_{i+1}^* Ic_{i+1} (tip to base) and then i force
+// transports toward the base. Wave 3 takes columns {0, 1} (the whole composite chain), wave 2 the
+// lower half of the rest, wave 1 the upper half; each wave runs the composite chain from the tip
+// down to its lowest column itself (a few act_inertia recomputed instead of a cross-wave wait).
+// Every element is computed by the same operations in the same order as chain_mass, so M is
+// bit-identical; row-major M written to Mout[k * SL], each element by exactly one wave.
+template <int NJ>
+struct RoMassCols {
+  static constexpr int rest = NJ > 2 ? NJ - 2 : 0, up = (rest + 1) / 2;
+  __device__ static int lo(int w) { return w == 3 ? 0 : (w == 2 ? 2 : 2 + up); }
+  __device__ static int hi(int w) { return w == 3 ? (NJ > 1 ? 1 : 0) : (w == 2 ? 1 + up : NJ - 1); }
+};
+
 template <int NJ, int SL>
-__device__ __forceinline__ void ro_chain_mass(const SysDevice& sd, RoChain<NJ, SL>& C, int c, double* Mout) {
-  Inertia acc = JointView{sd.joints + (NJ - 1) * CACTO_JOINT_COLS}.inertia();
-  inertia_st<SL>(C.Ic + (NJ - 1) * 10 * SL + c, acc);
-#pragma unroll RO_JU
-  for (int i = NJ - 1; i > 0; --i) {
+__device__ __forceinline__ void ro_mass_column(const SysDevice& sd, RoChain<NJ, SL>& C, int c, int i,
+                                               const Inertia& Ic, double* Mout) {
+  JointView j{sd.joints + i * CACTO_JOINT_COLS};
+  SV F = inertia_mul(Ic, joint_S(j));
+  Mout[(i * NJ + i) * SL] = sdot(joint_S(j), F);
+  for (int k = i; k > 0; --k) {
+    F = act_force(se3_ld<SL>(C.X + k * 12 * SL + c), F);
+    JointView jp{sd.joints + (k - 1) * CACTO_JOINT_COLS};
+    const double mij = sdot(joint_S(jp), F);
+    Mout[(i * NJ + (k - 1)) * SL] = mij;
+    Mout[((k - 1) * NJ + i) * SL] = mij;
+  }
+}
+
+template <int NJ, int SL>
+__device__ __forceinline__ void ro_chain_mass_cols(const SysDevice& sd, RoChain<NJ, SL>& C, int c, double* Mout,
+                                                   int lo, int hi) {
+  if (lo > hi) return;
+  Inertia acc = JointView{sd.joints + (NJ - 1) * CACTO_JOINT_COLS}.inertia();  // Ic_{NJ-1}
+  for (int i = NJ - 1;; --i) {
+    if (i <= hi) ro_mass_column<NJ, SL>(sd, C, c, i, acc, Mout);
+    if (i == lo) break;
     Inertia a = JointView{sd.joints + (i - 1) * CACTO_JOINT_COLS}.inertia();
     add_inertia(a, act_inertia(se3_ld<SL>(C.X + i * 12 * SL + c), acc));
     acc = a;
-    if (i > 1) inertia_st<SL>(C.Ic + (i - 1) * 10 * SL + c, acc);
-  }
-#pragma unroll RO_JU
-  for (int i = 0; i < NJ; ++i) {
-    JointView j{sd.joints + i * CACTO_JOINT_COLS};
-    SV F = inertia_mul(i == 0 ? acc : inertia_ld<SL>(C.Ic + i * 10 * SL + c), joint_S(j));
-    Mout[(i * NJ + i) * SL] = sdot(joint_S(j), F);
-#pragma unroll RO_JU
-    for (int k = i; k > 0; --k) {
-      F = act_force(se3_ld<SL>(C.X + k * 12 * SL + c), F);
-      JointView jp{sd.joints + (k - 1) * CACTO_JOINT_COLS};
-      const double mij = sdot(joint_S(jp), F);
-      Mout[(i * NJ + (k - 1)) * SL] = mij;
-      Mout[((k - 1) * NJ + i) * SL] = mij;
-    }
   }
 }
 
@@ -551,8 +547,8 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
 
 // One workgroup = SL episode slots (lane c < SL of wave 0 <-> slot c). Per step:
 //   actor (4 waves, MFMA, weights stationary)                                -> a (LDS)
-//   wave 0: s' = f(s, a) (chains with configuration-dependent M: RNEA on wave 0 and CRBA on
-//   wave 3 first, then the Cholesky step), the next actor input, the stores of (a_t, s_{t+1}),
+//   wave 0: s' = f(s, a) (chains with configuration-dependent M: RNEA on wave 0 and the CRBA
+//   columns on waves 1-3 first, then the Cholesky step), the next actor input, the stores of (a_t, s_{t+1}),
 //   finished episodes retired and their slots refilled.
 // Rewards and end-effector positions depend only on (s_t, a_t): k_rollout_rewards computes them
 // for every recorded step afterwards, fully parallel, so the sequential per-step chain is only
@@ -570,7 +566,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   const cacto_sys_params& p = sd.p;
   const Lane L;
   const int G = gridDim.x;
-  // chains with configuration-dependent M: RNEA (wave 0) and CRBA (wave 3) run concurrently
+  // chains with configuration-dependent M: RNEA (wave 0) and CRBA (waves 1-3) run concurrently
   const bool split_dyn = NJ > 0 && !(RoConstDyn<NJ>::ok && p.const_dyn);
   constexpr int REGK = RoSplit<NJ, NG>::REGK, LDSK = RoSplit<NJ, NG>::LDSK;
   RoActorRegs<ns, REGK> R;
@@ -609,10 +605,10 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (L.wave == 0 && active) {
           ro_chain_nle<NJ, SL>(sd, Sh.ch, c, Sh.sS + c * ns, Sh.sS + c * ns + NJ, Sh.hS + c);
           RSTAMP(9);
-        } else if (L.wave == 3 && active) {
-          ro_chain_mass<NJ, SL>(sd, Sh.ch, c, Sh.MS + c);
+        } else if (active) {
+          ro_chain_mass_cols<NJ, SL>(sd, Sh.ch, c, Sh.MS + c, RoMassCols<NJ>::lo(L.wave), RoMassCols<NJ>::hi(L.wave));
 #ifdef CACTO_STAMPS
-          if (blockIdx.x == 0 && L.lane == 0 && it == 20) g_rstamps[10] = __builtin_amdgcn_s_memtime();
+          if (blockIdx.x == 0 && L.lane == 0 && it == 20) g_rstamps[9 + L.wave] = __builtin_amdgcn_s_memtime();
 #endif
         }
       }

@@ -36,9 +36,10 @@ def main():
     names = ["actor", "E1 (dynamics | reward terms)", "E2 (reward combine + stores + refill | EE(s'))"]
     print(system, R, "step cycles %.0f: " % (t[3] - t[0]) + ", ".join("%s %.0f" % (nm, d) for nm, d in zip(names, np.diff(t))))
     print("   actor: layer 1 (+ placements) %.0f, layer 2 %.0f, layer 3 %.0f" % (a1, a2, t[1] - float(st[5])))
-    if st[9] > st[1] and st[10] > st[1]:
-        print("   chain dynamics after the actor: RNEA (wave 0) %.0f, CRBA (wave 3) %.0f"
-              % (float(st[9]) - t[1], float(st[10]) - t[1]))
+    if st[9] > st[1]:
+        print("   chain dynamics after the actor: RNEA (wave 0) %.0f, CRBA columns (waves 1-3) %s"
+              % (float(st[9]) - t[1], ", ".join("%.0f" % (float(st[9 + w]) - t[1]) if st[9 + w] > st[1] else "-"
+                                                   for w in (1, 2, 3))))
     print("   wave 0 after the dynamics phase: s' %.0f, advance/stores %.0f, refill+ballot %.0f, barrier %.0f"
           % (float(st[6]) - t[2], float(st[7]) - float(st[6]), float(st[8]) - float(st[7]), t[3] - float(st[8])))
 
