@@ -285,8 +285,14 @@ __device__ __forceinline__ void ro_placements(const SysDevice& sd, RoChain<NJ, S
   }
 }
 
-// Joint loops: unrolled for short chains; a 6-joint chain keeps one joint's values live at a time.
+// Joint loops: unrolled for short chains; a 6-joint chain keeps one joint's values live at a time
+// in the CRBA columns, while the RNEA's forward pass (wave 0, the longest per-step chain) is unrolled fully so a
+// joint's force terms overlap the next joint's velocity / acceleration recursion (no spills; the
+// backward pass unrolled would spill).
 #define RO_JU (NJ <= 3 ? NJ : 1)
+#ifndef RO_NLE_JU
+#define RO_NLE_JU NJ
+#endif
 
 // chain_nle (env.h) with X from the workspace and the forces parked there: same operations in the
 // same order, so h is bit-identical.
@@ -295,7 +301,7 @@ __device__ __forceinline__ void ro_chain_nle(const SysDevice& sd, RoChain<NJ, SL
                                              const double* v, double* hout) {
   const SV gacc{v3(-sd.p.gravity[0], -sd.p.gravity[1], -sd.p.gravity[2]), v3(0, 0, 0)};
   SV vp{v3(0, 0, 0), v3(0, 0, 0)}, ap = gacc, fc;
-#pragma unroll RO_JU
+#pragma unroll RO_NLE_JU
   for (int i = 0; i < NJ; ++i) {
     JointView j{sd.joints + i * CACTO_JOINT_COLS};
     const SE3 X = se3_ld<SL>(C.X + i * 12 * SL + c);
