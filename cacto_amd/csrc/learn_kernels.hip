@@ -819,8 +819,13 @@ __device__ __forceinline__ void adam_apply(const AdamNet& N, const AdamScalars& 
   }
 }
 
+// One workgroup per item: the 64-row chunks are dealt to the 4 waves (chunk ch to wave ch % 4),
+// each chunk's partial is formed exactly as before and parked in LDS (part[ch]), and wave 0 sums
+// them in chunk order and runs the Adam step: the same sums in the same order (bit-identical),
+// with a quarter of the chunk loads and MFMAs on each wave.
+constexpr int WA_MAXCH = 16;  // fused path: <= 1024 rows of 64
 __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, const int32_t* __restrict__ step,
-                                                int lane, float* tr) {
+                                                int wave, int lane, float* tr, float* part) {
   const int g = lane >> 4, c = lane & 15;
   int l = 0;
   while (item >= N.ioff[l + 1]) ++l;
@@ -840,7 +845,10 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
     int p[4];
     float mm[4], vv[4], th[4], tg[4];
     bool ok[4];
-    if (full) {
+    if (wave != 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ok[q] = false, p[q] = 0, mm[q] = vv[q] = th[q] = tg[q] = 0.f;
+    } else if (full) {
       const float4 m4 = *reinterpret_cast<const float4*>(N.m + pT), v4 = *reinterpret_cast<const float4*>(N.v + pT);
       const float4 t4 = *reinterpret_cast<const float4*>(N.src + pT);
       const float4 g4 = N.target ? *reinterpret_cast<const float4*>(N.target + pT) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -873,56 +881,61 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
     }
     CSTAMP(5);
 #endif
-    // chunks in batches of CB: all their panel loads are in flight together (one latency per batch)
-    constexpr int CB = 4;
-    floatx4 gs = {0.f, 0.f, 0.f, 0.f};
-    for (int cb = 0; cb < a.nch; cb += CB) {
+    // this wave's chunks (ch = wave + 4 j), all their panel loads in flight together
+    constexpr int CB = WA_MAXCH / 4;
+    {
       float4 A[CB][4], Bv[CB][4];
 #pragma unroll
       for (int j = 0; j < CB; ++j) {
-        const int ch = min(cb + j, a.nch - 1);
+        const int ch = min(wave + 4 * j, a.nch - 1);
         const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+        if (wave + 4 * j < a.nch) {
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int r = min(lo + 16 * w, hi - 16);  // clamped (branch-free); unused past hi
-          A[j][w] = *reinterpret_cast<const float4*>(ap + r);
-          Bv[j][w] = *reinterpret_cast<const float4*>(bp + r);
+          for (int w = 0; w < 4; ++w) {
+            const int r = min(lo + 16 * w, hi - 16);  // clamped (branch-free); unused past hi
+            A[j][w] = *reinterpret_cast<const float4*>(ap + r);
+            Bv[j][w] = *reinterpret_cast<const float4*>(bp + r);
+          }
         }
       }
 #pragma unroll
       for (int j = 0; j < CB; ++j) {
-        const int ch = cb + j;
-        const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
-        floatx4 part[4];
+        const int ch = wave + 4 * j;
+        if (ch < a.nch) {
+          const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+          floatx4 part4[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-          if (lo + 16 * w < hi) {
-            acc = mfma4(A[j][w].x, Bv[j][w].x, acc);
-            acc = mfma4(A[j][w].y, Bv[j][w].y, acc);
-            acc = mfma4(A[j][w].z, Bv[j][w].z, acc);
-            acc = mfma4(A[j][w].w, Bv[j][w].w, acc);
+          for (int w = 0; w < 4; ++w) {
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+            if (lo + 16 * w < hi) {
+              acc = mfma4(A[j][w].x, Bv[j][w].x, acc);
+              acc = mfma4(A[j][w].y, Bv[j][w].y, acc);
+              acc = mfma4(A[j][w].z, Bv[j][w].z, acc);
+              acc = mfma4(A[j][w].w, Bv[j][w].w, acc);
+            }
+            part4[w] = acc;
           }
-          part[w] = acc;
-        }
-        floatx4 s4 = part[0];
+          floatx4 s4 = part4[0];
 #pragma unroll
-        for (int w = 1; w < 4; ++w) {
-          s4[0] += part[w][0];
-          s4[1] += part[w][1];
-          s4[2] += part[w][2];
-          s4[3] += part[w][3];
-        }
-        if (ch == 0) {
-          gs = s4;
-        } else if (ch < a.nch) {
-          gs[0] += s4[0];
-          gs[1] += s4[1];
-          gs[2] += s4[2];
-          gs[3] += s4[3];
+          for (int w = 1; w < 4; ++w) {
+            s4[0] += part4[w][0];
+            s4[1] += part4[w][1];
+            s4[2] += part4[w][2];
+            s4[3] += part4[w][3];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) part[ch * 256 + q * 64 + lane] = s4[q];
         }
       }
     }
+    __syncthreads();
+    if (wave != 0) return;
+    floatx4 gs;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gs[q] = part[q * 64 + lane];
+    for (int ch = 1; ch < a.nch; ++ch)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gs[q] += part[ch * 256 + q * 64 + lane];
     CSTAMP(2);
 #ifdef CACTO_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: the GEMM's results landed
@@ -972,39 +985,46 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
   } else {
     const int ot = rem - Ly.IT * Ly.OT;
     const int oc = 16 * ot + c;
-    const bool ok = g == 0 && oc < Ly.out;
+    const bool ok = wave == 0 && g == 0 && oc < Ly.out;
     const int pp = ok ? Ly.boff + oc : 0;
-    const float mm = N.m[pp], vv = N.v[pp], th = N.src[pp], tg = N.target ? N.target[pp] : 0.f;
+    float mm = 0.f, vv = 0.f, th = 0.f, tg = 0.f;
+    if (wave == 0) mm = N.m[pp], vv = N.v[pp], th = N.src[pp], tg = N.target ? N.target[pp] : 0.f;
     const float* bp = Ly.RT + (size_t)(16 * min(ot, Ly.OT - 1) + c) * a.ld + 4 * g;
     // per chunk: its (<= 4) 16-row steps from max(lo, bias_r0), summed in row order from 0 — the
-    // sequence k_wgrad's 64-row groups and 16-row tail produce — then the shuffles over g
-    constexpr int CB = 4;
-    float gsum = 0.f;
-    for (int cb = 0; cb < a.nch; cb += CB) {
+    // sequence k_wgrad's 64-row groups and 16-row tail produce — then the shuffles over g; chunks
+    // dealt to the waves as for the weight tiles, summed in chunk order by wave 0
+    constexpr int CB = WA_MAXCH / 4;
+    {
       float4 v4[CB][4];
 #pragma unroll
       for (int j = 0; j < CB; ++j) {
-        const int ch = min(cb + j, a.nch - 1);
+        const int ch = min(wave + 4 * j, a.nch - 1);
         const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
         const int r0 = max(lo, a.bias_r0);
+        if (wave + 4 * j < a.nch)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v4[j][k] = *reinterpret_cast<const float4*>(bp + max(0, min(r0 + 16 * k, hi - 16)));
+          for (int k = 0; k < 4; ++k) v4[j][k] = *reinterpret_cast<const float4*>(bp + max(0, min(r0 + 16 * k, hi - 16)));
       }
 #pragma unroll
       for (int j = 0; j < CB; ++j) {
-        const int ch = cb + j;
-        const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
-        const int r0 = max(lo, a.bias_r0);
-        float sb = 0.f;
+        const int ch = wave + 4 * j;
+        if (ch < a.nch) {
+          const int lo = a.r_begin + ch * a.CH, hi = min(a.r_end, lo + a.CH);
+          const int r0 = max(lo, a.bias_r0);
+          float sb = 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (r0 + 16 * k < hi) sb += (v4[j][k].x + v4[j][k].y) + (v4[j][k].z + v4[j][k].w);
-        sb += __shfl_xor(sb, 16);
-        sb += __shfl_xor(sb, 32);
-        if (ch == 0) gsum = sb;
-        else if (ch < a.nch) gsum = gsum + sb;
+          for (int k = 0; k < 4; ++k)
+            if (r0 + 16 * k < hi) sb += (v4[j][k].x + v4[j][k].y) + (v4[j][k].z + v4[j][k].w);
+          sb += __shfl_xor(sb, 16);
+          sb += __shfl_xor(sb, 32);
+          part[ch * 256 + lane] = sb;
+        }
       }
     }
+    __syncthreads();
+    if (wave != 0) return;
+    float gsum = part[lane];
+    for (int ch = 1; ch < a.nch; ++ch) gsum = gsum + part[ch * 256 + lane];
     const AdamScalars s = adam_scalars(N.ad, step);
     if (ok) adam_apply(N, s, pp, gsum, mm, vv, th, tg, -1, 0, 0);
   }
@@ -1012,7 +1032,7 @@ __device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, cons
 
 // One or two networks (the paired update runs the critic of update t and the actor of t - 1).
 // Work list: workgroup b runs on XCD b % 8 (the dispatcher's round robin; used for locality only,
-// nothing depends on it) and takes 4 items of that XCD's bin. The bins group the tiles of a layer
+// nothing depends on it) and takes one item of that XCD's bin (its 4 waves split the item's row chunks). The bins group the tiles of a layer
 // into blocks of in-tiles x out-tiles, so each XCD's L2 fetches a panel slice once for several
 // tiles instead of every XCD fetching every slice from the memory-side cache.
 __global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, const int32_t* __restrict__ items,
@@ -1021,11 +1041,12 @@ __global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, cons
   // the item is wave-uniform: readfirstlane lets the compiler keep the network descriptor in
   // scalar registers (s_load from the kernel arguments) instead of chasing it through VGPR pointers
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int code = __builtin_amdgcn_readfirstlane(items[(blockIdx.x & 7) * stride + (blockIdx.x >> 3) * 4 + wave]);
-  __shared__ float tr[4][256];  // per wave: one 16 x 16 transpose
+  const int code = __builtin_amdgcn_readfirstlane(items[(blockIdx.x & 7) * stride + (blockIdx.x >> 3)]);
+  __shared__ float tr[256];                    // wave 0: one 16 x 16 transpose
+  __shared__ float part[WA_MAXCH * 256];       // per-chunk partial sums
   if (code >= 0) {
-    if ((code >> 15) == 0) wgrad_adam_item(n0, code & 0x7fff, step, lane, tr[wave]);
-    else wgrad_adam_item(n1, code & 0x7fff, step, lane, tr[wave]);
+    if ((code >> 15) == 0) wgrad_adam_item(n0, code & 0x7fff, step, wave, lane, tr, part);
+    else wgrad_adam_item(n1, code & 0x7fff, step, wave, lane, tr, part);
   }
   CSTAMP(4);
 #ifdef CACTO_STAMPS
@@ -1302,7 +1323,13 @@ AdamNet actor_adam_net(const cacto_sys* sys, const cacto_nets* nets, const cacto
 int launch_wgrad_adam(const cacto_sys* sys, int mode, const AdamNet& n0, const AdamNet* n1, const int32_t* step,
                       hipStream_t st) {
   const int stride = sys->wa_stride[mode];
-  hipLaunchKernelGGL(k_wgrad_adam, dim3(8 * (stride / 4)), dim3(256), 0, st, n0, n1 ? *n1 : n0, sys->wa_items[mode],
+  // one item per workgroup (the 4 waves split its chunks); fused_adam keeps every row set within
+  // WA_MAXCH chunks of 64
+  if (n0.wg.nch > WA_MAXCH || (n1 && n1->wg.nch > WA_MAXCH)) {
+    set_error("k_wgrad_adam: more than WA_MAXCH row chunks");
+    return CACTO_EINVAL;
+  }
+  hipLaunchKernelGGL(k_wgrad_adam, dim3(8 * stride), dim3(256), 0, st, n0, n1 ? *n1 : n0, sys->wa_items[mode],
                      stride, step);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
