@@ -15,7 +15,7 @@ struct cacto_sys {
   hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its two events
   hipEvent_t ev_critic = nullptr, ev_actor[2] = {nullptr, nullptr};
   std::mutex pipe_mu;  // one two-stream pipeline at a time per handle (they share side / events)
-  // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (net << 15 | item, -1 = none), for
+  // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (layer << 16 | net << 15 | item, -1 = none), for
   // the critic alone, the actor alone and both (built at creation, cacto_build_wgrad_adam_items)
   int32_t* wa_items[3] = {nullptr, nullptr, nullptr};
   int wa_stride[3] = {0, 0, 0};

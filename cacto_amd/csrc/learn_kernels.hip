@@ -824,11 +824,9 @@ __device__ __forceinline__ void adam_apply(const AdamNet& N, const AdamScalars& 
 // them in chunk order and runs the Adam step: the same sums in the same order (bit-identical),
 // with a quarter of the chunk loads and MFMAs on each wave.
 constexpr int WA_MAXCH = 16;  // fused path: <= 1024 rows of 64
-__device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, const int32_t* __restrict__ step,
+__device__ __forceinline__ void wgrad_adam_item(const AdamNet& N, int item, int l, const int32_t* __restrict__ step,
                                                 int wave, int lane, float* tr, float* part) {
-  const int g = lane >> 4, c = lane & 15;
-  int l = 0;
-  while (item >= N.ioff[l + 1]) ++l;
+  const int g = lane >> 4, c = lane & 15;  // l: the item's layer, from the work list (no search)
   const int rem = item - N.ioff[l];
   const WgLayer& Ly = N.wg.l[l];
   const WgArgs& a = N.wg;
@@ -1045,8 +1043,9 @@ __global__ void __launch_bounds__(256) k_wgrad_adam(AdamNet n0, AdamNet n1, cons
   __shared__ float tr[256];                    // wave 0: one 16 x 16 transpose
   __shared__ float part[WA_MAXCH * 256];       // per-chunk partial sums
   if (code >= 0) {
-    if ((code >> 15) == 0) wgrad_adam_item(n0, code & 0x7fff, step, wave, lane, tr, part);
-    else wgrad_adam_item(n1, code & 0x7fff, step, wave, lane, tr, part);
+    const int l = (code >> 16) & 0xf;
+    if (((code >> 15) & 1) == 0) wgrad_adam_item(n0, code & 0x7fff, l, step, wave, lane, tr, part);
+    else wgrad_adam_item(n1, code & 0x7fff, l, step, wave, lane, tr, part);
   }
   CSTAMP(4);
 #ifdef CACTO_STAMPS
@@ -1365,6 +1364,8 @@ int actor_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
 // = 8 blocks (bi chosen so the blocks are as square as the tile grid allows), block k to bin k; a
 // layer's bias tiles go to the bin of their out-tile block. Item numbering is AdamNet's (per layer:
 // IT * OT weight tiles, row-major in (it, ot), then OT bias tiles).
+// Code: bits 0-14 the item, bit 15 the network (n1 of the paired launch), bits 16-19 the layer
+// (so the kernel does not search AdamNet::ioff with dependent scalar loads); -1 = no item.
 int cacto_build_wgrad_adam_items(cacto_sys* sys) {
   std::vector<int32_t> bins[3][8];
   const NetTopo* nets[2] = {&sys->critic, &sys->actor};
@@ -1389,11 +1390,11 @@ int cacto_build_wgrad_adam_items(cacto_sys* sys) {
         for (int it = 0; it < IT; ++it)
           for (int ot = 0; ot < OT; ++ot) {
             const int bin = ((it * bi) / IT) * bo + std::min(bo - 1, (ot * bo) / OT);
-            bins[mode][bin % 8].push_back((tag << 15) | (base + it * OT + ot));
+            bins[mode][bin % 8].push_back((l << 16) | (tag << 15) | (base + it * OT + ot));
           }
         for (int ot = 0; ot < OT; ++ot) {
           const int bin = std::min(bo - 1, (ot * bo) / OT);
-          bins[mode][bin % 8].push_back((tag << 15) | (base + IT * OT + ot));
+          bins[mode][bin % 8].push_back((l << 16) | (tag << 15) | (base + IT * OT + ot));
         }
         base += IT * OT + OT;
       }
