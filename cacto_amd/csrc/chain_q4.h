@@ -1,0 +1,530 @@
+// The learner chains on 4-sample tiles (q4.h): NN.compute_critic_grad (Sobolev double backprop,
+// NeuralNetwork.py:150-180) and NN.compute_actor_grad (dynamics Jacobian path,
+// NeuralNetwork.py:182-233), the same operations as the 16-sample chains of learn_kernels.hip with
+// every activation tile in the F4 layout (one float per lane per 16-feature tile). They write the
+// same operand panels (feature-major, sample rows), so k_wgrad / k_wgrad_adam / k_adam are shared.
+//
+// Per tile a wave owns the out tiles ot = wave, wave + 4, ... of each layer and, after q4_reduce,
+// one element per lane: feature 16 ot + (lane & 15) of sample lane >> 4 (F4 index q4e(ot, lane)).
+// All elementwise arrays (cos / sin / pre-activation / zbar tiles) use the F4 layout, so an epilogue
+// reads its operands at the index it writes. Per-sample work (row gathers, input normalisation,
+// dynamics, losses) runs one (sample, feature) element per thread.
+//
+// Included by learn_kernels.hip (uses its GradBufs, ChainScalars, clog).
+#pragma once
+
+#include "q4.h"
+
+namespace cacto {
+
+// ---------------------------------------------------------------- critic (fixed 64-64-128-128-1 shape)
+struct Q4CriticFwd {
+  Q4Frags<1, 1> f0;
+  Q4Frags<4, 1> f1;
+  Q4Frags<4, 2> f2;
+  Q4Frags<8, 2> f3;
+  Q4Split<2> f4;
+  template <bool BIAS>
+  __device__ __forceinline__ void load(const NetView& N, int wave, int lane) {
+    f0.load<BIAS>(N.fwd(0), N.biasp(0), 4, 64, wave, lane);
+    f1.load<BIAS>(N.fwd(1), N.biasp(1), 4, 64, wave, lane);
+    f2.load<BIAS>(N.fwd(2), N.biasp(2), 8, 128, wave, lane);
+    f3.load<BIAS>(N.fwd(3), N.biasp(3), 8, 128, wave, lane);
+  }
+  __device__ __forceinline__ void load_last(const NetView& N, int wave, int lane) {
+    f4.load<true>(N.fwd(4), 8, N.biasp(4), 1, wave, lane);
+  }
+};
+
+// transposed passes G_l = D_l W_l^T: l3 2 x 8 k-tiles, l2 1 x 8, l1 1 x 4, l0 split-K 1 of 4
+struct Q4CriticBwd {
+  Q4Frags<8, 2> g3;
+  Q4Frags<8, 1> g2;
+  Q4Frags<4, 1> g1;
+  float w5[2];  // W5[16 (wave + 4 t) + c, 0]: the lane's feature of layer-3 out tiles wave, wave + 4
+  __device__ __forceinline__ void load(const NetView& N, int wave, int lane) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) w5[t] = N.flat[N.t.woff[4] + 16 * (wave + 4 * t) + (lane & 15)];
+    g3.load<false>(N.bwd(3), nullptr, 8, 128, wave, lane);
+    g2.load<false>(N.bwd(2), nullptr, 4, 64, wave, lane);
+    g1.load<false>(N.bwd(1), nullptr, 4, 64, wave, lane);
+  }
+};
+
+// Critic forward over the F4 input tile X0 (see net_common.h critic_forward_tile_f): with Hs every
+// h_l = sin z_l is kept (24 tiles at ZOFF), else h alternates in H (2 x 8 tiles); with Cs cos z_l is
+// kept. hook(l, ot, h) per hidden element; V[i] (LDS) receives sample i's value when WANT_V.
+template <bool WANT_V, typename Hook>
+__device__ void q4_critic_forward_f(const Q4CriticFwd& F, const float* X0, float* Cs, float* Hs, float* H, float* red,
+                                    float* V, const Lane& L, Hook&& hook) {
+  auto epi = [&](int l, float* out) {
+    return [&, l, out](int ot, float z) {
+      float h, c;
+      fast_sincos(z, &h, &c);
+      const int e = q4e(ot, L.lane);
+      if (Cs) Cs[ZOFF[l] * 64 + e] = c;
+      out[e] = h;
+      hook(l, ot, h);
+    };
+  };
+  const float* in = X0;
+  float* out = Hs ? Hs + ZOFF[0] * 64 : H;
+  F.f0.run<true>(in, 4, L.wave, L.lane, epi(0, out));
+  __syncthreads();
+  in = out;
+  out = Hs ? Hs + ZOFF[1] * 64 : H + 8 * 64;
+  F.f1.run<true>(in, 4, L.wave, L.lane, epi(1, out));
+  __syncthreads();
+  in = out;
+  out = Hs ? Hs + ZOFF[2] * 64 : H;
+  F.f2.run<true>(in, 8, L.wave, L.lane, epi(2, out));
+  __syncthreads();
+  in = out;
+  out = Hs ? Hs + ZOFF[3] * 64 : H + 8 * 64;
+  F.f3.run<true>(in, 8, L.wave, L.lane, epi(3, out));
+  __syncthreads();
+  if (WANT_V) {
+    F.f4.run<true>(8, out, red, L.wave, L.lane, [&](int, float v) {
+      if ((L.lane & 15) == 0) V[L.lane >> 4] = v;
+    });
+    __syncthreads();
+  }
+}
+
+template <bool WANT_V, typename Hook>
+__device__ void q4_critic_forward(const NetView& N, const float* X0, float* Cs, float* Hs, float* H, float* red,
+                                  float* V, const Lane& L, Hook&& hook) {
+  Q4CriticFwd F;
+  F.load<true>(N, L.wave, L.lane);
+  if (WANT_V) F.load_last(N, L.wave, L.lane);
+  q4_critic_forward_f<WANT_V>(F, X0, Cs, Hs, H, red, V, L, hook);
+}
+
+// Critic input gradient from the cos tiles Cs (net_common.h critic_first_backward): G4 = W5,
+// D_l = G_{l+1} cos z_l, G_l = D_l W_l^T. G tiles (G1 at 0, G2 at 4, G3 at 8) when Gs, D via
+// hookD(l, ot, d), dV/dx0 in G0 (F4, one tile).
+template <typename HookD>
+__device__ void q4_critic_first_backward(const NetView& N, const float* Cs, float* P /* 2 x 8 tiles */, float* Gs,
+                                         float* G0, float* red, const Lane& L, HookD&& hookD) {
+  const int goff[4] = {0, 0, 4, 8};
+  Q4CriticBwd F;
+  F.load(N, L.wave, L.lane);
+  Q4Split<1> F0;
+  F0.load<false>(N.bwd(0), 4, nullptr, 16, L.wave, L.lane);
+  float* D = P;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int ot = L.wave + 4 * t, e = q4e(ot, L.lane);
+    const float d = fmul(F.w5[t], Cs[ZOFF[3] * 64 + e]);
+    D[e] = d;
+    hookD(3, ot, d);
+  }
+  __syncthreads();
+  auto epi = [&](int l, float* Dn) {
+    return [&, l, Dn](int it, float g) {
+      const int e = q4e(it, L.lane);
+      if (Gs) Gs[goff[l] * 64 + e] = g;
+      const float d = fmul(g, Cs[ZOFF[l - 1] * 64 + e]);
+      Dn[e] = d;
+      hookD(l - 1, it, d);
+    };
+  };
+  float* Dn = P + 8 * 64;
+  F.g3.run<false>(D, 8, L.wave, L.lane, epi(3, Dn));
+  __syncthreads();
+  D = Dn;
+  Dn = P;
+  F.g2.run<false>(D, 4, L.wave, L.lane, epi(2, Dn));
+  __syncthreads();
+  D = Dn;
+  Dn = P + 8 * 64;
+  F.g1.run<false>(D, 4, L.wave, L.lane, epi(1, Dn));
+  __syncthreads();
+  D = Dn;
+  F0.run<false>(4, D, red, L.wave, L.lane, [&](int, float g) { G0[q4e(0, L.lane)] = g; });
+  __syncthreads();
+}
+
+// input normalisation of the F4 element e = 4 f + i (utils.py:17-24), norms loaded once
+struct Q4Norm {
+  float n, nT;
+  int f, ns;
+  bool on;
+  __device__ __forceinline__ Q4Norm(const cacto_sys_params& p, int e) {
+    ns = p.nb_state;
+    on = p.normalize != 0;
+    f = e >> 2;
+    n = (float)p.state_norm[min(f, ns - 1)];
+    nT = (float)p.state_norm[ns - 1];
+  }
+  __device__ __forceinline__ float forward(float s) const {
+    if (f >= ns) return 0.f;
+    if (!on) return s;
+    if (f == ns - 1) return fsub(fmul(fdiv(s, nT), 2.0f), 1.0f);
+    return fdiv(s, n);
+  }
+};
+
+struct Q4CriticLds {
+  float X0[64], XT[64], G0[64];
+  float Cs[24 * 64];  // cos z_l
+  float Hs[24 * 64];  // h_l = sin z_l
+  float G[16 * 64];
+  float ZB[24 * 64];
+  float GB[16 * 64];
+  float red[4 * 64];
+  float stage[4 * 64];  // gathered rows: [0] s, [1] s_next, [2] dV/dx, [3] (R, d, w) per sample
+  float Vn[4], V[4], y[4], Vb[4], Vt2[4];
+};
+
+// one 4-sample tile of the critic chain (critic_chain's operations, F4 layout)
+__device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, const SysDevice* __restrict__ sdp,
+                                                const NetView& C, const NetView& Tg, const ChainScalars& cs,
+                                                const double* __restrict__ storage, const int32_t* __restrict__ idx,
+                                                const float* __restrict__ isw, int B, const GradBufs& gb,
+                                                float* __restrict__ y_out, float* __restrict__ V_out,
+                                                float* __restrict__ Vt_out, int32_t* __restrict__ step) {
+  float *X0 = S.X0, *XT = S.XT, *G0 = S.G0, *Cs = S.Cs, *Hs = S.Hs, *G = S.G, *ZB = S.ZB, *GB = S.GB, *red = S.red;
+  const cacto_sys_params& p = sdp->p;
+  const Lane L;
+  const int ns = p.nb_state, cols = 3 * ns + 3, s0 = tile * Q4_TILE;
+  const int ld = gb.ld, Bp = gb.Bp;
+  const bool sob = cs.w_S != 0.f;
+  const int goff[4] = {0, 0, 4, 8};
+  if (tile == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
+
+  Q4CriticFwd TF;  // the target network, in flight during the row gathers
+  float w5[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) w5[t] = C.flat[C.t.woff[4] + 16 * (L.wave + 4 * t) + L.c];
+  const Q4Norm nrm(p, L.lane);
+  {
+    // one (sample c, column) per lane, wave w gathers array w: s, s_next, dV/dx, then (R, d, w);
+    // branch-free (clamped indices, zeroed after), so no load sits under a branch
+    const int c = L.lane >> 4, f = L.lane & 15;
+    const bool valid = s0 + c < B;
+    const int sc = min(s0 + c, B - 1), fc = min(f, ns - 1);
+    const int32_t row = idx[sc];
+    TF.load<true>(Tg, L.wave, L.lane);
+    TF.load_last(Tg, L.wave, L.lane);
+    const int col = L.wave == 0 ? fc : L.wave < 3 ? L.wave * ns + 1 + fc : (f == 0 ? ns : 3 * ns + 1);
+    const double x = storage[(size_t)row * cols + col];
+    const float wv = isw ? isw[sc] : 1.f;
+    const bool keep = valid && (L.wave < 3 ? f < ns : f < 2);
+    float v = keep ? (float)x : 0.f;
+    if (L.wave == 3 && f == 2) v = valid ? wv : 0.f;
+    S.stage[L.wave * 64 + c * 16 + f] = v;
+  }
+  __syncthreads();
+  if (L.wave < 2) {  // wave 0: X0, wave 1: XT (element lane = 4 f + i)
+    const int f = L.lane >> 2, i = L.lane & 3;
+    const float v = nrm.forward(S.stage[L.wave * 64 + i * 16 + min(f, 15)]);
+    (L.wave == 0 ? X0 : XT)[L.lane] = v;
+  }
+  __syncthreads();
+  const float* Rs = S.stage + 3 * 64;  // Rs[16 c] = R, [16 c + 1] = d, [16 c + 2] = w
+
+  // y = R + (1 - d) * V_tgt(s_next)   (NeuralNetwork.py:153-158)
+  if (!cs.MC) q4_critic_forward_f<true>(TF, XT, nullptr, nullptr, Hs, red, S.Vn, L, [](int, int, float) {});
+  if (L.tid < 4) {
+    const int c = L.tid;
+    S.y[c] = cs.MC ? Rs[16 * c] : fadd(Rs[16 * c], fmul(fsub(1.f, Rs[16 * c + 1]), S.Vn[c]));
+  }
+  if (cs.want_vt) q4_critic_forward_f<true>(TF, X0, nullptr, nullptr, Hs, red, S.Vt2, L, [](int, int, float) {});
+
+  // forward at s, keeping sin z and cos z; h_l -> LT_l second half
+  if (L.wave == 0) {
+    const int f = L.lane >> 2, i = L.lane & 3;
+    gb.LT[0][(size_t)f * ld + Bp + s0 + i] = X0[L.lane];
+  }
+  q4_critic_forward<true>(C, X0, Cs, Hs, Hs, red, S.V, L,
+                          [&](int l, int ot, float h) { q4_store_panel(gb.LT[l + 1], ld, Bp + s0, ot, L.lane, h); });
+
+  if (sob) {
+    // first backward: D_l -> RT_l first half; G_l kept; G_0 = dV/dx0
+    q4_critic_first_backward(C, Cs, GB, G, G0, red, L,
+                             [&](int l, int ot, float d) { q4_store_panel(gb.RT[l], ld, s0, ot, L.lane, d); });
+    Q4CriticFwd SF;
+    SF.load<false>(C, L.wave, L.lane);
+    // Sobolev loss gradient w.r.t. dV/ds, then w.r.t. G_0 (NeuralNetwork.py:167-170): element
+    // (feature f, sample i) = lane 4 f + i of wave 0
+    if (L.wave == 0) {
+      const int f = L.lane >> 2, i = L.lane & 3;
+      float gb0 = 0.f;
+      if (f < ns - 1) {
+        const float nf = (float)p.state_norm[f];
+        auto nback = [&](float g) { return !p.normalize ? g : fdiv(g, nf); };  // not the time column
+        const float gsq = fdiv(fmul(fdiv(1.f, (float)cs.B_global), Rs[16 * i + 2]), (float)(ns - 1));
+        const float dvds = nback(G0[L.lane]);
+        const float yp = clog(dvds), yt = clog(S.stage[2 * 64 + i * 16 + f]);
+        const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
+        gb0 = nback(clog_backward(dvds, gyp));
+      }
+      GB[L.lane] = gb0;
+      gb.LT[0][(size_t)f * ld + s0 + i] = gb0;
+    }
+    __syncthreads();
+    // backward of the first backward, l = 0..3, on the forward fragments (no bias)
+    auto sp_epi = [&](int l, float* nxt) {
+      return [&, l, nxt](int ot, float acc) {
+        const int e = q4e(ot, L.lane);
+        const float sz = Hs[ZOFF[l] * 64 + e], cz = Cs[ZOFF[l] * 64 + e];
+        const float gu = l < 3 ? G[goff[l + 1] * 64 + e] : (ot >= 4 ? w5[1] : w5[0]);
+        ZB[ZOFF[l] * 64 + e] = fmul(-fmul(acc, gu), sz);  // CosGrad: -grad * sin(x)
+        const float gn = fmul(acc, cz);                    // MulGrad into the upstream grad
+        nxt[e] = gn;
+        q4_store_panel(gb.LT[l + 1], ld, s0, ot, L.lane, gn);
+      };
+    };
+    float* nA = GB + 8 * 64;
+    SF.f0.run<false>(GB, 4, L.wave, L.lane, sp_epi(0, nA));
+    __syncthreads();
+    SF.f1.run<false>(nA, 4, L.wave, L.lane, sp_epi(1, GB));
+    __syncthreads();
+    SF.f2.run<false>(GB, 8, L.wave, L.lane, sp_epi(2, nA));
+    __syncthreads();
+    SF.f3.run<false>(nA, 8, L.wave, L.lane, sp_epi(3, GB));
+    __syncthreads();
+    if (L.tid < 4) gb.RT[4][s0 + L.tid] = 1.f;  // dW5 += Gbar_4 (G_4 = W5[:, 0])
+  } else {
+    for (int k = L.tid; k < 24 * 64; k += CACTO_THREADS) ZB[k] = 0.f;
+  }
+
+  // the transposed fragments of the last backward pass, in flight during the value loss
+  Q4CriticBwd HB;
+  HB.load(C, L.wave, L.lane);
+  // value loss: Vbar = (2 * ((wS/B) * w)) * (V - y)   (Keras MSE, SUM_OVER_BATCH_SIZE)
+  if (L.tid < 4) {
+    const int c = L.tid;
+    const float wv = sob ? cs.w_S : 1.f;
+    const float gl = fmul(fdiv(wv, (float)cs.B_global), Rs[16 * c + 2]);
+    S.Vb[c] = fmul(fmul(2.f, gl), fsub(S.V[c], S.y[c]));
+    gb.RT[4][Bp + s0 + c] = S.Vb[c];
+    if (s0 + c < B) {
+      if (y_out) y_out[s0 + c] = S.y[c];
+      if (V_out) V_out[s0 + c] = S.V[c];
+      if (Vt_out && cs.want_vt) Vt_out[s0 + c] = S.Vt2[c];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {  // zbar_3 += (Vbar * W5) * cos(z3): out tiles wave, wave + 4
+    const int e = q4e(L.wave + 4 * t, L.lane);
+    const float vb = S.Vb[L.lane >> 4];
+    ZB[ZOFF[3] * 64 + e] = fadd(ZB[ZOFF[3] * 64 + e], fmul(fmul(vb, w5[t]), Cs[ZOFF[3] * 64 + e]));
+  }
+  __syncthreads();
+  // backward through the forward graph: zbar_{l-1} += (zbar_l W_l^T) * cos(z_{l-1})
+  auto hb_epi = [&](int l) {
+    return [&, l](int it, float acc) {
+      const int e = ZOFF[l - 1] * 64 + q4e(it, L.lane);
+      ZB[e] = fadd(ZB[e], fmul(acc, Cs[e]));
+    };
+  };
+  auto store_rt = [&](int l) {
+    for (int ot = L.wave; ot < C.t.OT[l]; ot += CACTO_NWAVES)
+      q4_store_panel(gb.RT[l], ld, Bp + s0, ot, L.lane, ZB[ZOFF[l] * 64 + q4e(ot, L.lane)]);
+  };
+  store_rt(3);
+  HB.g3.run<false>(ZB + ZOFF[3] * 64, 8, L.wave, L.lane, hb_epi(3));
+  __syncthreads();
+  store_rt(2);
+  HB.g2.run<false>(ZB + ZOFF[2] * 64, 4, L.wave, L.lane, hb_epi(2));
+  __syncthreads();
+  store_rt(1);
+  HB.g1.run<false>(ZB + ZOFF[1] * 64, 4, L.wave, L.lane, hb_epi(1));
+  __syncthreads();
+  store_rt(0);
+}
+
+__global__ void __launch_bounds__(CACTO_THREADS)
+    k_critic_grad_q4(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, ChainScalars cs,
+                     const double* __restrict__ storage, const int32_t* __restrict__ idx,
+                     const float* __restrict__ isw, int B, GradBufs gb, float* __restrict__ y_out,
+                     float* __restrict__ V_out, float* __restrict__ Vt_out, int32_t* __restrict__ step) {
+  __shared__ Q4CriticLds S;
+  q4_critic_chain(S, blockIdx.x, sdp, C, Tg, cs, storage, idx, isw, B, gb, y_out, V_out, Vt_out, step);
+}
+
+// ---------------------------------------------------------------- actor chain
+struct Q4ActorLds {
+  float X0[64], XS[64], G0[64], ZB3[64];
+  float ZA[32 * 64];  // actor z1, z2
+  float H[32 * 64];   // actor h ping-pong; later critic H (16 tiles) + actor zbar2 (16)
+  float ZC[24 * 64];  // critic cos z at s'
+  float red[4 * 64];
+  float st[64], stn[64], gn[64];  // [sample][16]
+  float A[Q4_TILE * CACTO_MAX_ACTION];
+  float Fu[Q4_TILE * CACTO_MAX_STATE * CACTO_MAX_ACTION];
+  float dra[Q4_TILE * CACTO_MAX_ACTION];
+  double term_s[Q4_TILE];
+};
+
+// one 4-sample tile of the actor chain (actor_chain's operations, F4 layout). The actor's shape is
+// fixed (ns -> 256 -> 256 -> na, ns, na <= 16: KT = 1 / 16 / 16, OT = 16 / 16 / 1; the host checks).
+template <int NJ>
+__device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, const SysDevice* __restrict__ sdp,
+                                               const NetView& Ac, const NetView& C, const ChainScalars& cs,
+                                               const double* __restrict__ storage, const int32_t* __restrict__ idx,
+                                               int B, const GradBufs& gb, int32_t* __restrict__ step) {
+  float *X0 = S.X0, *XS = S.XS, *G0 = S.G0, *ZB3 = S.ZB3, *ZA = S.ZA, *H = S.H, *ZC = S.ZC, *red = S.red;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const Lane L;
+  const int ns = p.nb_state, na = p.nb_action, cols = 3 * ns + 3, s0 = tile * Q4_TILE;
+  const int ld = gb.ld;
+  if (tile == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
+  Q4Frags<1, 4> F1;  // actor layer 1 (ns -> 256), in flight during the row gathers
+  F1.load<true>(Ac.fwd(0), Ac.biasp(0), 16, 256, L.wave, L.lane);
+  if (L.wave == 0) {
+    const int c = L.lane >> 4, f = L.lane & 15;
+    const bool valid = s0 + c < B;
+    const double* rp = storage + (size_t)(valid ? idx[s0 + c] : 0) * cols;
+    S.st[c * 16 + f] = (valid && f < ns) ? (float)rp[f] : 0.f;
+    if (f == 0) S.term_s[c] = valid ? rp[3 * ns + 2] : 0.0;
+  }
+  __syncthreads();
+  if (L.wave == 0) {  // input of layer 0 (normalised) -> LT_0
+    const int f = L.lane >> 2, i = L.lane & 3;
+    const float v = f < ns ? normalize_feature(p, f, S.st[i * 16 + f]) : 0.f;
+    X0[L.lane] = v;
+    gb.LT[0][(size_t)f * ld + s0 + i] = v;
+  }
+  __syncthreads();
+  // actor forward; z1, z2 kept; h1 -> LT_1, h2 -> LT_2
+  auto lepi = [&](int l) {
+    return [&, l](int ot, float z) {
+      const float h = z > 0.f ? z : fmul(z, 0.3f);  // LeakyReLU(alpha=0.3)
+      const int e = q4e(ot, L.lane);
+      ZA[l * 16 * 64 + e] = z;
+      H[l * 16 * 64 + e] = h;
+      q4_store_panel(gb.LT[l + 1], ld, s0, ot, L.lane, h);
+    };
+  };
+  Q4Split<4> F3;  // the action layer (256 -> na), issued with layer 1's MFMAs
+  F1.run<true>(X0, 16, L.wave, L.lane, lepi(0));
+  F3.load<true>(Ac.fwd(2), 16, Ac.biasp(2), na, L.wave, L.lane);
+  __syncthreads();
+  q4_layer_t<16, true>(Ac.fwd(1), 16, H, L.wave, L.lane, lepi(1), Ac.biasp(1), 256);
+  __syncthreads();
+  F3.run<true>(16, H + 16 * 64, red, L.wave, L.lane, [&](int, float v) {
+    const int f = L.lane & 15;
+    if (f < na) S.A[(L.lane >> 4) * na + f] = v;
+  });
+  __syncthreads();
+  // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
+  if (L.tid < Q4_TILE) {
+    constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
+    const int c = L.tid;
+    double s[NS], a[NA], sn[NS], F[NS * NA];
+#pragma unroll
+    for (int f = 0; f < NS; ++f) s[f] = (double)S.st[c * 16 + f];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) a[i] = (double)S.A[c * na + i];
+    if constexpr (NJ > 0 && NJ <= 3) {
+      if (p.const_dyn) env_simulate_derivative_const<NJ>(sd, s, a, true, sn, F);
+      else env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
+    } else {
+      env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
+    }
+#pragma unroll
+    for (int f = 0; f < 16; ++f) S.stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NS * NA; ++k) S.Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
+  } else if (L.tid >= 64 && L.tid < 64 + Q4_TILE) {
+    // wave 1, alongside the dynamics: only d reward / d a enters the actor gradient
+    // (NeuralNetwork.py:199-204), and only the control cost depends on a
+    constexpr int NA = Dims<NJ>::NA;
+    const int c = L.tid - 64;
+    float af[NA], g[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) af[i] = S.A[c * na + i];
+    const double tc = S.term_s[c];
+    const double w6 = 6 >= p.n_weights ? 0.0 : tc * p.w_terminal[6] + (1.0 - tc) * p.w_running[6];
+    (void)reward_batch_f32<NA>(p, w6, af, 0.0, g);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) S.dra[c * na + i] = g[i];
+  }
+  __syncthreads();
+  if (L.wave == 0) {
+    const int f = L.lane >> 2, i = L.lane & 3;
+    XS[L.lane] = f < ns ? normalize_feature(p, f, S.stn[i * 16 + f]) : 0.f;
+  }
+  __syncthreads();
+  // critic (already updated) at s': dV/dx0 (NeuralNetwork.py:190-195); V(s') is not used
+  float* HC = H;              // 16 tiles
+  float* ZB2 = H + 16 * 64;   // 16 tiles
+  q4_critic_forward<false>(C, XS, ZC, nullptr, HC, red, nullptr, L, [](int, int, float) {});
+  q4_critic_first_backward(C, ZC, HC, nullptr, G0, red, L, [](int, int, float) {});
+  // dQ/da = dV/ds' Fu + dr/da ; abar = -dQ/da / B  (NeuralNetwork.py:206-231)
+  if (L.wave == 0) {  // d normalize / d s of every (state f, sample i) element at once
+    const int f = L.lane >> 2, i = L.lane & 3;
+    if (f < ns) S.gn[i * 16 + f] = normalize_backward(p, f, G0[L.lane]);
+  }
+  // the two backward layers' first fragments, in flight during the rest of the dQ/da phase
+  // (W3^T: KT = 1, every tile; W2^T: the first tile's 16 blocks)
+  Q4Frags<1, 4> B2;
+  FragTile<16> B1;
+  B2.load<false>(Ac.bwd(2), nullptr, 16, 256, L.wave, L.lane);
+  B1.load(Ac.bwd(1), L.wave, L.lane);
+  __syncthreads();
+  if (L.wave == 0) {  // element (action j, sample i) = lane 4 j + i
+    const int j = L.lane >> 2, i = L.lane & 3;
+    float abar = 0.f;
+    if (j < na && s0 + i < B) {
+      float q = 0.f;
+      for (int f = 0; f < ns; ++f) {
+        const float t = fmul(S.gn[i * 16 + f], S.Fu[i * CACTO_MAX_STATE * CACTO_MAX_ACTION + f * na + j]);
+        q = (f == 0) ? t : fadd(q, t);
+      }
+      q = fadd(q, S.dra[i * na + j]);
+      abar = fmul(-q, fdiv(1.f, (float)cs.B_global));
+    }
+    ZB3[L.lane] = abar;
+    gb.RT[2][(size_t)j * ld + s0 + i] = abar;
+  }
+  __syncthreads();
+  // zbar2 = (abar W3^T) * lrelu'(z2) ; zbar1 = (zbar2 W2^T) * lrelu'(z1)
+  auto bepi = [&](int l) {
+    return [&, l](int it, float acc) {
+      const int e = q4e(it, L.lane);
+      const float z = ZA[l * 16 * 64 + e];
+      const float o = z > 0.f ? acc : fmul(acc, 0.3f);
+      if (l == 1) ZB2[e] = o;
+      q4_store_panel(gb.RT[l], ld, s0, it, L.lane, o);
+    };
+  };
+  B2.run<false>(ZB3, 16, L.wave, L.lane, bepi(1));
+  __syncthreads();
+  q4_layer_t<16, false>(Ac.bwd(1), 16, ZB2, L.wave, L.lane, bepi(0), nullptr, 256, &B1);
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(CACTO_THREADS)
+    k_actor_grad_q4(const SysDevice* __restrict__ sdp, NetView Ac, NetView C, ChainScalars cs,
+                    const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
+                    int32_t* __restrict__ step) {
+  __shared__ Q4ActorLds S;
+  q4_actor_chain<NJ>(S, blockIdx.x, sdp, Ac, C, cs, storage, idx, B, gb, step);
+}
+
+// the critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the rest)
+// in one grid, as k_chain_pair
+template <int NJ>
+__global__ void __launch_bounds__(CACTO_THREADS)
+    k_chain_pair_q4(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, NetView Ac, ChainScalars cs,
+                    const double* __restrict__ storage, const int32_t* __restrict__ idx_c,
+                    const float* __restrict__ isw, const int32_t* __restrict__ idx_a, int B, int nct, GradBufs gbc,
+                    GradBufs gba, float* __restrict__ y_out, float* __restrict__ V_out, int32_t* __restrict__ step) {
+  constexpr size_t bytes = sizeof(Q4CriticLds) > sizeof(Q4ActorLds) ? sizeof(Q4CriticLds) : sizeof(Q4ActorLds);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[bytes];
+  if ((int)blockIdx.x < nct) {
+    q4_critic_chain(*reinterpret_cast<Q4CriticLds*>(smem), blockIdx.x, sdp, C, Tg, cs, storage, idx_c, isw, B, gbc,
+                    y_out, V_out, nullptr, step);
+  } else {
+    q4_actor_chain<NJ>(*reinterpret_cast<Q4ActorLds*>(smem), blockIdx.x - nct, sdp, Ac, C, cs, storage, idx_a, B, gba,
+                       step);
+  }
+}
+
+}  // namespace cacto

@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(64) k_ddp_derivs(const SysDevice* __restrict__
   const int t = blockIdx.y;
   if (e >= n_ep) return;
   const int Te = nsteps[e];
-  if (t > Te) return;
+  if (t > Te) return;  // also Te < 0: a dropped episode (main.py:236), skipped
   const SysDevice& sd = *sdp;
   double x[N], w[7];
 #pragma unroll
@@ -518,6 +518,7 @@ __global__ void __launch_bounds__(64) k_ddp_backward(const SysDevice* __restrict
   const SysDevice& sd = *sdp;
   const cacto_sys_params& p = sd.p;
   const int Te = nsteps[e];
+  if (Te < 0) return;  // a dropped episode (main.py:236): no labels
   const double* Se = S + (size_t)e * ldS * ns;
   const double* Ue = U + (size_t)e * ldU * na;
   double* Oe = dVdx + (size_t)e * ldS * ns;
@@ -684,6 +685,7 @@ __global__ void __launch_bounds__(64) k_ddp_riccati_wave(const SysDevice* __rest
   const cacto_sys_params& p = sdp->p;
   const double w6 = p.w_running[6];
   const int Te = nsteps[e];
+  if (Te < 0) return;  // a dropped episode (main.py:236): no labels (uniform over the workgroup)
   double* Oe = dVdx + (size_t)e * ldS * ns;
   const double* Ue = U + (size_t)e * ldU * na;
   {

@@ -11,6 +11,7 @@
 //   -> k_wgrad: one wave per (layer, 16x16 output tile | bias tile, row chunk) -> slab[chunk][P]
 //   -> k_adam : sum chunks in fixed order (deterministic), Adam, packed copies, soft update.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "net_common.h"
@@ -516,6 +517,13 @@ __global__ void __launch_bounds__(CACTO_THREADS)
                     step);
   }
 }
+
+}  // namespace cacto
+
+// the same chains on 4-sample tiles (small batches)
+#include "chain_q4.h"
+
+namespace cacto {
 
 // ---------------------------------------------------------------- weight-gradient GEMM
 struct WgLayer {
@@ -1073,25 +1081,51 @@ using namespace cacto;
 
 namespace {
 
+// Samples per chain workgroup: 4-sample tiles (chain_q4.h) up to a padded batch of Q4_MAX_BP, so a
+// reference-size batch (64 / 128) spreads over 4x the workgroups; 16-sample tiles above. A function
+// of the batch only, so every update path of one batch size runs the same chain kernels
+// (bit-identical results). CACTO_Q4_MAX_BP overrides the bound (read once; benchmarks).
+inline int q4_max_bp() {
+  static const int v = [] {
+    const char* e = std::getenv("CACTO_Q4_MAX_BP");
+    return e ? std::atoi(e) : 512;
+  }();
+  return v;
+}
+inline int chain_tile(int Bp) { return Bp <= q4_max_bp() ? Q4_TILE : CACTO_TILE; }
+
 template <int NJ>
 struct LaunchActorChain {
   static int run(const cacto_sys* sys, NetView Ac, NetView C, ChainScalars cs, const double* storage,
                  const int32_t* idx, int B, GradBufs gb, int32_t* step, hipStream_t st) {
     const int Bp = (B + 15) / 16 * 16;
-    hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage, idx,
-                       B, gb, step);
+    if (chain_tile(Bp) == Q4_TILE)
+      hipLaunchKernelGGL(k_actor_grad_q4<NJ>, dim3(Bp / Q4_TILE), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs,
+                         storage, idx, B, gb, step);
+    else
+      hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage,
+                         idx, B, gb, step);
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
   }
 };
 
+// nct: critic tiles (= actor tiles) of the batch's chain tile size
 template <int NJ>
 struct LaunchChainPair {
   static int run(const cacto_sys* sys, NetView C, NetView Tg, NetView Ac, ChainScalars cs, const double* storage,
-                 const int32_t* idx_c, const float* isw, const int32_t* idx_a, int B, int nct, GradBufs gbc,
-                 GradBufs gba, float* y, float* V, int32_t* step, hipStream_t st) {
-    hipLaunchKernelGGL(k_chain_pair<NJ>, dim3(2 * nct), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, Ac, cs, storage,
-                       idx_c, isw, idx_a, B, nct, gbc, gba, y, V, step);
+                 const int32_t* idx_c, const float* isw, const int32_t* idx_a, int B, GradBufs gbc, GradBufs gba,
+                 float* y, float* V, int32_t* step, hipStream_t st) {
+    const int Bp = gbc.Bp;
+    if (chain_tile(Bp) == Q4_TILE) {
+      const int nct = Bp / Q4_TILE;
+      hipLaunchKernelGGL(k_chain_pair_q4<NJ>, dim3(2 * nct), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, Ac, cs,
+                         storage, idx_c, isw, idx_a, B, nct, gbc, gba, y, V, step);
+    } else {
+      const int nct = Bp / CACTO_TILE;
+      hipLaunchKernelGGL(k_chain_pair<NJ>, dim3(2 * nct), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, Ac, cs,
+                         storage, idx_c, isw, idx_a, B, nct, gbc, gba, y, V, step);
+    }
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
   }
@@ -1221,8 +1255,12 @@ int launch_critic_chain(const cacto_sys* sys, const cacto_nets* nets, const cact
   float* yb = y ? y : w.scal;
   float* Vb = V ? V : w.scal + w.Bp;
   float* Vtb = Vt ? Vt : w.scal + 2 * w.Bp;
-  hipLaunchKernelGGL(k_critic_grad, dim3(w.Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, cs, storage, idx, isw,
-                     B, w.crit, yb, Vb, Vtb, nets->step_d);
+  if (chain_tile(w.Bp) == Q4_TILE)
+    hipLaunchKernelGGL(k_critic_grad_q4, dim3(w.Bp / Q4_TILE), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, cs,
+                       storage, idx, isw, B, w.crit, yb, Vb, Vtb, nets->step_d);
+  else
+    hipLaunchKernelGGL(k_critic_grad, dim3(w.Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, cs, storage, idx,
+                       isw, B, w.crit, yb, Vb, Vtb, nets->step_d);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }
@@ -1508,7 +1546,7 @@ extern "C" int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* n
     const NetView Tg = cacto_make_view(sys, CACTO_NET_CRITIC, nets->target_d);
     const NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
     if (int e = dispatch_nj<LaunchChainPair>(sys->host.p, sys, C, Tg, Ac, chain_scalars(cfg, B), storage_d, idx_c_d,
-                                             is_w_d, idx_a_d, B, w.Bp / 16, w.crit, w.act, yb, Vb, nets->step_d, st))
+                                             is_w_d, idx_a_d, B, w.crit, w.act, yb, Vb, nets->step_d, st))
       return e;
   } else if (idx_c_d) {
     if (int e = launch_critic_chain(sys, nets, cfg, storage_d, idx_c_d, is_w_d, B, yb, Vb, nullptr, w, st)) return e;
@@ -1580,7 +1618,6 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
                          const Workspace& w, hipStream_t st) {
   float* const y = w.scal;
   float* const V = w.scal + w.Bp;
-  const int nct = w.Bp / 16;
   const int soft = cfg->MC ? 0 : 1;
   const ChainScalars cs = chain_scalars(cfg, B);
   const NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
@@ -1604,7 +1641,7 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
       }
     }
     if (t < K && t > 0) {
-      if (int e = dispatch_nj<LaunchChainPair>(sys->host.p, sys, C, Tg, Ac, cs, storage_d, idx, isw, idx_prev, B, nct,
+      if (int e = dispatch_nj<LaunchChainPair>(sys->host.p, sys, C, Tg, Ac, cs, storage_d, idx, isw, idx_prev, B,
                                                w.crit, w.act, y, V, nets->step_d, st))
         return e;
       if (int e = launch_wgrad_adam(sys, 2, cn, &an, nets->step_d, st)) return e;

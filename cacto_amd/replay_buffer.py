@@ -57,29 +57,37 @@ class ReplayBuffer:
     def _rows_added(self, start, n):
         pass
 
-    def _row_offsets(self, nsteps):
+    def _row_offsets(self, rows):
         """Exclusive prefix sum of the episode row counts on the device; the last batch's copy is
-        reused when the lengths repeat (one create_TO_init batch is added many times in a bench)."""
-        key = nsteps.tobytes()
+        reused when the counts repeat (one create_TO_init batch is added many times in a bench)."""
+        key = rows.tobytes()
         if getattr(self, "_off_key", None) != key:
-            off = np.zeros(len(nsteps) + 1, dtype=np.int64)
-            np.cumsum(nsteps + 1, out=off[1:])
+            off = np.zeros(len(rows) + 1, dtype=np.int64)
+            np.cumsum(rows, out=off[1:])
             self._off_key, self._off = key, (torch.as_tensor(off, device=DEVICE), int(off[-1]))
         return self._off
 
-    def add_episodes(self, S_traj, rewards, nsteps, R_term=None, dVdx=None, want_total=False):
+    def add_episodes(self, S_traj, rewards, nsteps, R_term=None, dVdx=None, want_total=False, status=None):
         """RL_AC.RL_Solve (RL.py:145-189) for a batch of episodes, with the rows of each episode
         added in order as main.py:240 adds them, all on the device (cacto_rl_solve_add).
 
         S_traj [E, ldS, ns] f64 device (s_0..s_T per episode, e.g. cacto_rollout's S_traj);
         rewards [E, ldR] f64 device: r_0..r_T, or r_0..r_{T-1} with R_term [E] giving r_T;
         nsteps: host ints (NSTEPS_SH per episode); dVdx [E, ldS, ns] f64 device or None (zeros).
-        Returns total_reward_to_go [E, ldS] (device) when want_total, else None."""
+        status [E] (a rollout's, host or device): episodes with status != 0 hit a NaN state and are
+        dropped as main.py:236 drops them (no rows; the kept episodes' rows stay contiguous, in
+        order). Returns total_reward_to_go [E, ldS] (device) when want_total, else None."""
         nsteps = np.asarray(nsteps, dtype=np.int64)
         E = len(nsteps)
         if E == 0:
             return None
-        off_d, n = self._row_offsets(nsteps)
+        rows = nsteps + 1
+        if status is not None:
+            st = status.cpu().numpy() if torch.is_tensor(status) else np.asarray(status)
+            rows = np.where(st.reshape(-1) == 0, rows, 0)
+            if not rows.any():
+                return None
+        off_d, n = self._row_offsets(rows)
         if n > self.N:
             raise ValueError("cannot add more rows than REPLAY_SIZE at once")
         f64 = lambda t: t.to(device=DEVICE, dtype=torch.float64).contiguous()

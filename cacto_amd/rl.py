@@ -68,6 +68,9 @@ class Adam:
         """optimizer.apply_gradients(zip(grads, model.trainable_variables)) (RL.py:105, :109)."""
         grads = [g for g, _ in grads_and_vars]
         flat = torch.cat([torch.as_tensor(g, dtype=torch.float32, device=DEVICE).reshape(-1) for g in grads])
+        model = self.learner.critic_model if self.which == CRITIC else self.learner.actor_model
+        if flat.numel() != model.P:
+            raise ValueError("apply_gradients: %d gradient values for a model of %d parameters" % (flat.numel(), model.P))
         # the device Adam reads the counter as Keras `iterations + 1` (the fused update's gradient
         # kernels advance it; a standalone apply_gradients advances it here)
         self.learner.steps[0 if self.which == CRITIC else 1] += 1
@@ -296,6 +299,9 @@ class RL_AC:
         it on the current stream, one call for the Adam steps. is_w / y / V only with K = 1 (PER)."""
         import torch.distributed as dist
         K, B = int(idx_steps.shape[0]), int(idx_steps.shape[1])
+        if K != 1 and (is_w is not None or y is not None or V is not None):
+            raise ValueError("_update_rows_n_dp: IS weights / y / V belong to one update (K == 1); "
+                             "K PER updates go through update_rows_n_per_dp")
         ws = self.workspace(B)
         cfg = self._cfg_for(B)
         Pc, Pa = self.critic_model.P, self.actor_model.P
@@ -314,6 +320,47 @@ class RL_AC:
         def apply(c, a, _):
             L.lib().call("cacto_update_pair_apply", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(g),
                          int(c is not None), int(a is not None), int(not self.conf.MC), stream())
+        dp_pipeline(K, grads, lambda t: dist.all_reduce(t, group=self.dp_group), apply)
+
+    def update_rows_n_per_dp(self, buffer, uniforms):
+        """K data-parallel PER updates (RL.py:122-137 on every rank's replay shard, the sampling of
+        replay_buffer.py:139-188 over the union of the shards) in the paired schedule of
+        dp_pipeline: step t samples update t (one all-gather of the shards' (sum, min, rows), then
+        the stratified sample and IS weights, all on the device), computes [critic gradient of
+        update t | actor gradient of update t - 1] into one buffer, all-reduces it ONCE, applies
+        both Adam steps, then updates the local priorities of update t. uniforms [K, B] (this
+        rank's random.random() draws, in order) go to the device in one copy. Every kernel sees the
+        inputs of the sequential loop (sample -> update -> priorities), so the result equals K
+        update_rows + update_priorities_device calls (bit for bit when the collective's sums are
+        order-independent, e.g. two ranks)."""
+        import torch.distributed as dist
+        K, B = int(uniforms.shape[0]), int(uniforms.shape[1])
+        u = uniforms.to(device=DEVICE, dtype=torch.float64).contiguous()
+        ws = self.workspace(B)
+        cfg = self._cfg_for(B)
+        Pc, Pa = self.critic_model.P, self.actor_model.P
+        g = self._dp_grad_buf(Pc + Pa)
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        V = torch.empty_like(y)
+        drawn = {}
+
+        def grads(c, a):
+            if c is not None:
+                drawn[c] = buffer.sample_device(u[c])
+                drawn.pop(c - 2, None)
+            ic, wc = drawn[c] if c is not None else (None, None)
+            ia = drawn[a][0] if a is not None else None
+            L.lib().call("cacto_update_pair_grads", self.sys.handle, C.byref(self.nets), C.byref(cfg),
+                         dptr(buffer.storage, torch.float64), dptr(ic, torch.int32), dptr(wc), dptr(ia, torch.int32),
+                         B, dptr(g), dptr(y if c is not None else None), dptr(V if c is not None else None), dptr(ws),
+                         ws.numel() * 4, stream())
+            return g[:Pc] if a is None else (g[Pc:] if c is None else g)
+
+        def apply(c, a, _):
+            L.lib().call("cacto_update_pair_apply", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(g),
+                         int(c is not None), int(a is not None), int(not self.conf.MC), stream())
+            if c is not None:
+                buffer.update_priorities_device(drawn[c][0], y, V)
         dp_pipeline(K, grads, lambda t: dist.all_reduce(t, group=self.dp_group), apply)
 
     def _dp_grad_buf(self, n):
@@ -347,25 +394,19 @@ class RL_AC:
         if per:
             if self.dp_world > 1 and buffer.dp_world != self.dp_world:
                 buffer.set_data_parallel(self.dp_world, self.dp_group)
-            if self.dp_world == 1:
-                # the updates between two checkpoint saves as one pipelined call; the uniforms are
-                # the per-step random.random() draws of the sequential loop, in the same order
-                i = 0
-                while i < n:
-                    k = min(n - i, self.conf.save_interval - update_step_counter % self.conf.save_interval)
-                    U = np.array([[buffer.random.random() for _ in range(B)] for _ in range(k)], dtype=np.float64)
+            # the updates between two checkpoint saves as one pipelined call; the uniforms are the
+            # per-step random.random() draws of the sequential loop, in the same order
+            i = 0
+            while i < n:
+                k = min(n - i, self.conf.save_interval - update_step_counter % self.conf.save_interval)
+                U = np.array([[buffer.random.random() for _ in range(B)] for _ in range(k)], dtype=np.float64)
+                if self.dp_world == 1:
                     self.update_rows_n_per(buffer, torch.as_tensor(U, device=DEVICE))
-                    for _ in range(k):
-                        update_step_counter = self._after_step(update_step_counter)
-                    i += k
-                return update_step_counter
-            for _ in range(n):
-                idx, w = buffer.sample_device()
-                y = torch.empty(B, dtype=torch.float32, device=DEVICE)
-                V = torch.empty_like(y)
-                self.update_rows(buffer.storage, idx, w, y, V)
-                buffer.update_priorities_device(idx, y, V)
-                update_step_counter = self._after_step(update_step_counter)
+                else:
+                    self.update_rows_n_per_dp(buffer, torch.as_tensor(U, device=DEVICE))
+                for _ in range(k):
+                    update_step_counter = self._after_step(update_step_counter)
+                i += k
             return update_step_counter
         idx_all = buffer.sample_indices(n, rng)                  # [n, B] int32 on device
         # the updates between two checkpoint saves (RL.py:139-141) run as one pipelined call
@@ -527,3 +568,28 @@ class RL_AC:
         states = out["S"][0].cpu().numpy()
         controls = out["A"][0].double().cpu().numpy() if "A" in out else np.zeros((T, na))
         return self.init_rand_state, states, controls, self.NSTEPS_SH, 1
+
+    def create_TO_init_batch(self, ep, ICS_list):
+        """create_TO_init for every initial state of a main.py iteration (main.py:174-224 calls it
+        once per episode) in ONE rollout launch and one device->host copy: returns the list of
+        tuples create_TO_init returns, in order — (None, None, None, None, 0) for NSTEPS_SH == 0 or
+        an episode dropped for a NaN state (RL.py:229-231). The per-episode attributes create_TO_init
+        leaves for RL_Solve (state_arr, ee_pos_arr) are not set; batched callers take the device
+        path (rollout_batch -> TO.backward_pass_batch -> ReplayBuffer.add_episodes)."""
+        ICS = np.asarray(ICS_list, dtype=np.float64).reshape(len(ICS_list), -1)
+        ns_ = [self.nsteps_sh(s) for s in ICS]
+        fail = (None, None, None, None, 0)
+        T = max(ns_) if ns_ else 0
+        if T <= 0:
+            return [fail for _ in ns_]
+        na = self.conf.nb_action
+        out = self.rollout_batch(ICS, ns_, T, ep=ep, want=("S", "A"))
+        S, A, st = out["S"].cpu().numpy(), out["A"].double().cpu().numpy(), out["status"].cpu().numpy()
+        res = []
+        for k, n in enumerate(ns_):
+            if n <= 0 or st[k] != 0:
+                res.append(fail)
+            else:
+                res.append((ICS[k].copy(), S[k, :n + 1].copy(), A[k, :n].copy() if ep != 0 else np.zeros((n, na)),
+                            n, 1))
+        return res

@@ -33,12 +33,17 @@ class TO:
                                        torch.tensor([T - 1], dtype=torch.int32, device=DEVICE), mu=mu)
         return out[0].cpu().numpy()
 
-    def backward_pass_batch(self, S_traj, U_traj, nsteps, mu=1e-9, out=None):
+    def backward_pass_batch(self, S_traj, U_traj, nsteps, mu=1e-9, out=None, status=None):
         """Device batch: S_traj [E, ldS, ns] f64, U_traj [E, ldU, na] f64, nsteps [E] int32 (Te per
-        episode: Te + 1 states). Returns dVdx [E, ldS, ns] f64 (rows past Te untouched)."""
+        episode: Te + 1 states). Returns dVdx [E, ldS, ns] f64 (rows past Te untouched).
+        status [E] int32 (device, a rollout's): episodes with status != 0 were dropped for a NaN
+        state (RL.py:229-231, main.py:236) and get no labels (their rows stay untouched)."""
         E, ldS = S_traj.shape[0], S_traj.shape[1]
         if out is None:
             out = torch.zeros_like(S_traj)
+        if status is not None:
+            nsteps = torch.where(status.to(device=DEVICE) == 0, nsteps.to(device=DEVICE, dtype=torch.int32),
+                                 torch.full_like(nsteps, -1, dtype=torch.int32, device=DEVICE)).contiguous()
         L.lib().call("cacto_ddp_backward", self.sys.handle, dptr(S_traj, torch.float64), ldS,
                      dptr(U_traj, torch.float64), U_traj.shape[1], dptr(nsteps, torch.int32), E, float(mu),
                      dptr(out, torch.float64), stream())

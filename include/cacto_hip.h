@@ -311,6 +311,8 @@ int cacto_rollout_rewards(const cacto_sys* sys, const double* S_traj_d, const fl
  *   S_traj_d [n_ep, ldS, ns] f64 (s_0..s_Te; the time column is ignored), U_traj_d [n_ep, ldU, na]
  *   f64 (u_0..u_{Te-1}), output dVdx_d [n_ep, ldS, ns] f64: V_x(s_t) for t = 0..Te, time column 0 —
  *   the layout cacto_rl_solve_add reads. mu: the Qbar_uu regulariser (1e-9 in the reference).
+ *   nsteps_d[e] < 0 skips episode e (a rollout dropped for a NaN state, RL.py:229-231 /
+ *   main.py:236): nothing is read or written for it.
  * The reward's derivatives are those of the TO cost (= -reward, environment_TO.py): closed forms
  * for the planar family (SI, DI, car), hyper-dual forward-mode derivatives through the forward
  * kinematics (manipulator, UR5) and the body check points (car_park). Dynamics Jacobians as

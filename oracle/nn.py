@@ -56,6 +56,25 @@ def actor_forward(params, S, norm, keep=False):
     return a
 
 
+def actor_forward32(params, S, norm):
+    """The actor as TF runs it (NeuralNetwork.py:51-63, NN.eval :130-138): float32 tensors and
+    float32 ops throughout, so IEEE float32 overflow / inf / NaN propagate as in the reference
+    (the float64 `actor_forward` above cannot overflow where the reference does). Normalisation in
+    float32 (RealDiv, then *2 - 1 for the time column, utils.py:17-24)."""
+    f32 = np.float32
+    W1, b1, W2, b2, W3, b3 = [np.asarray(p, dtype=f32) for p in params]
+    x = np.asarray(S, dtype=f32).copy()
+    nm = np.asarray(norm, dtype=f32)
+    with np.errstate(over="ignore", invalid="ignore"):
+        x[:, :-1] = x[:, :-1] / nm[:-1]
+        x[:, -1] = x[:, -1] / nm[-1] * f32(2) - f32(1)
+        z1 = x @ W1 + b1
+        h1 = np.where(z1 > 0, z1, z1 * f32(LEAKY_ALPHA))
+        z2 = h1 @ W2 + b2
+        h2 = np.where(z2 > 0, z2, z2 * f32(LEAKY_ALPHA))
+        return h2 @ W3 + b3
+
+
 def critic_forward(params, S, norm, keep=False):
     P = [np.asarray(p, dtype=np.float64) for p in params]
     h = normalize(S, norm)

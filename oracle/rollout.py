@@ -10,7 +10,7 @@ States are float64 throughout, as in the reference's numpy arrays.
 """
 import numpy as np
 
-from .nn import actor_forward
+from .nn import actor_forward, actor_forward32
 
 
 def actor_eval32(actor, s, norm):
@@ -84,7 +84,10 @@ def nsteps_sh(conf, s0):
     return conf.NSTEPS - int(s0[-1] / conf.dt)
 
 
-def to_init_rollout(env, actor, s0, ep):
+def to_init_rollout(env, actor, s0, ep, f32=False, fail_step=None):
+    """RL_AC.create_TO_init (RL.py:197-233). f32: the actor in TF's float32 arithmetic
+    (`actor_forward32`: overflow to inf / NaN as the reference's). fail_step (a list) receives the
+    step i whose s_{i+1} was NaN when the episode is dropped (RL.py:229-231)."""
     conf = env.conf
     T = nsteps_sh(conf, s0)
     if T == 0:
@@ -94,8 +97,16 @@ def to_init_rollout(env, actor, s0, ep):
     U = np.zeros((T, conf.nb_action))
     S[0] = s0
     for i in range(T):
-        U[i] = 0.0 if ep == 0 else actor_eval32(actor, S[i], norm)
-        S[i + 1] = env.simulate(S[i], U[i])
+        if ep == 0:
+            U[i] = 0.0
+        elif f32:
+            U[i] = actor_forward32(actor, np.asarray(S[i])[None, :], norm)[0]
+        else:
+            U[i] = actor_eval32(actor, S[i], norm)
+        with np.errstate(over="ignore", invalid="ignore"):
+            S[i + 1] = env.simulate(S[i], U[i])
         if np.isnan(S[i + 1]).any():
+            if fail_step is not None:
+                fail_step.append(i)
             return None
     return S, U, T

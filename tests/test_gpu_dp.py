@@ -164,6 +164,41 @@ def _per_worker(rank, port, q):
         dist.destroy_process_group()
 
 
+def _per_loop_worker(rank, port, q):
+    """The data-parallel PER loop two ways on this rank's shard: K sequential (sample -> update ->
+    priorities) steps, and RL_AC.update_rows_n_per_dp (the paired, pipelined form)."""
+    dist = _init(rank, port)
+    try:
+        from cacto_amd.confs import load_conf
+        from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+        conf = load_conf("double_integrator", fresh=True)
+        conf.prioritized_replay_alpha = 0.6
+        conf.BATCH_SIZE = B_LOCAL
+        rows = _rows(900 + 300 * rank, 90 + rank)
+        U = np.random.default_rng(300 + rank).uniform(size=(K + 1, B_LOCAL))
+        out = []
+        for pipelined in (False, True):
+            rl = _learner(WORLD)
+            buf = PrioritizedReplayBuffer(conf, rl.sys)
+            buf.set_data_parallel(WORLD)
+            buf.add_rows(rows)
+            if pipelined:
+                rl.update_rows_n_per_dp(buf, torch.as_tensor(U, device="cuda"))
+            else:
+                y = torch.empty(B_LOCAL, dtype=torch.float32, device="cuda")
+                V = torch.empty_like(y)
+                for k in range(K + 1):
+                    idx, w = buf.sample_device(torch.as_tensor(U[k], device="cuda"))
+                    rl.update_rows(buf.storage, idx, w, y, V)
+                    buf.update_priorities_device(idx, y, V)
+            torch.cuda.synchronize()
+            out.append((_state(rl), rl.steps.cpu().tolist(), buf.sum_tree.cpu().numpy(), buf.min_tree.cpu().numpy(),
+                        buf.exp_counter.cpu().numpy(), float(buf.max_priority.item())))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
 def _per_shard(rank):
     rng = np.random.default_rng(200 + rank)
     n_rows = 700 + 500 * rank                                # shards of different fill
@@ -312,3 +347,24 @@ def test_dp_baseline_configs_on_gpu(system, w_S, B, weighted):
     h = B // WORLD
     for r in range(WORLD):
         np.testing.assert_allclose(res[r][1], yg[r * h:(r + 1) * h], rtol=1e-5, atol=1e-5)
+
+
+def test_dp_per_loop_pipelined_equals_sequential():
+    """learn_and_update's data-parallel PER branch (RL.py:122-137, replay_buffer.py:139-218 on
+    each rank's shard): the paired pipeline (one shard-stats all-gather and one gradient all-reduce
+    per update, uniforms pre-drawn and copied once) equals the sequential sample -> update ->
+    priority-update loop bit for bit on every rank — weights, moments, counters, both trees,
+    exp_counter, max_priority — and the replicas' weights stay identical."""
+    res = _spawn(_per_loop_worker, lambda r: ())
+    for r in range(WORLD):
+        seq, pip = res[r][0]
+        for a, b in zip(seq[0], pip[0]):
+            assert np.array_equal(a, b)
+        assert seq[1] == pip[1] == [K + 1, K + 1]
+        for a, b in zip(seq[2:5], pip[2:5]):
+            assert np.array_equal(a, b)
+        assert seq[5] == pip[5]
+    for a, b in zip(res[0][0][1][0], res[1][0][1][0]):
+        assert np.array_equal(a, b)
+    # the shards differ (each rank's own rows and priorities)
+    assert not np.array_equal(res[0][0][1][2], res[1][0][1][2])

@@ -1,0 +1,195 @@
+"""The NaN-abort path of create_TO_init (RL.py:229-231) and its consumers (main.py:181-187, :236)
+on the device.
+
+A policy is built so that some episodes of a batch hit a NaN state: the trained double-integrator
+actor (the reference's own actor_final.h5 weights) with hidden unit 0 of both layers rewired into a
+gate on the normalised x position, g = lrelu(5e19 * lrelu(1e19 * (x/15 - 0.1))), feeding every
+action with weight 1e-38. In float32 (TF's arithmetic, `oracle.nn.actor_forward32`) the gate
+overflows to +inf once x/15 exceeds ~0.78, the action becomes inf and the next state NaN; below
+that the gate adds at most a few units of control. Some episodes start past the threshold (dropped
+at step 0), some cross it mid-episode, most never do. The oracle's float32 to_init_rollout decides
+which episodes the reference would drop; episodes whose outcome changes when the gate's gain moves
+by 0.2 % are too close to the threshold to pin and are excluded from the status check.
+
+Checked: status == 1 exactly for the episodes the oracle drops, under a refilling schedule
+(sched=(1, 3): 12 slots for 48 episodes); every kept episode's trajectory, rewards and EE rows
+bit-identical to a clean run of the kept episodes alone; create_TO_init / create_TO_init_batch
+return the reference's failure tuple; the DDP labels and the replay rows skip the dropped episodes
+exactly as main.py:236 removes them.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_weights
+from oracle import env as oenv
+from oracle import rollout as oroll
+from cacto_amd.confs import load_conf
+
+pytestmark = pytest.mark.gpu
+
+THETA, G1, G2 = 0.1, 1e19, 5e19
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def gated_actor(base, g2=G2):
+    W1, b1, W2, b2, W3, b3 = [np.array(p, dtype=np.float32) for p in base]
+    W1[:, 0] = 0
+    W1[0, 0] = G1
+    b1[0] = np.float32(-G1 * THETA)
+    W2[0, :] = 0
+    W2[:, 0] = 0
+    W2[0, 0] = g2
+    b2[0] = 0
+    W3[0, :] = np.float32(1e-38)
+    return [W1, b1, W2, b2, W3, b3]
+
+
+def oracle_outcomes(oe, base, S0):
+    """Per episode: the oracle's failure step (None = kept) and whether it is stable under a
+    +-0.2 % change of the gate gain."""
+    runs = []
+    for g2 in (G2 * (1 - 2e-3), G2, G2 * (1 + 2e-3)):
+        act = gated_actor(base, g2)
+        r = []
+        for s in S0:
+            fs = []
+            oroll.to_init_rollout(oe, act, np.asarray(s), 1, f32=True, fail_step=fs)
+            r.append(fs[0] if fs else None)
+        runs.append(r)
+    return runs[1], [runs[0][k] == runs[1][k] == runs[2][k] for k in range(len(S0))]
+
+
+@pytest.fixture(scope="module")
+def setup():
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.rl import RL_AC
+    conf = load_conf("double_integrator", fresh=True)
+    genv, oe = make_env(conf), oenv.make_env(conf)
+    nn = NN(genv, conf, w_S=1e-2, seed=0)
+    rl = RL_AC(genv, nn, conf)
+    w = load_weights("di_seed0_final")
+    rl.setup_model(weights=w)
+    base = w["actor"]
+    rl.actor_model.set_weights(gated_actor(base))
+    rng = random.Random(21)
+    S0 = np.array([oe.reset(rng) for _ in range(48)])
+    fail, stable = oracle_outcomes(oe, base, S0)
+    return conf, genv, oe, rl, S0, fail, stable
+
+
+def test_status_matches_oracle_under_refill(setup):
+    conf, genv, oe, rl, S0, fail, stable = setup
+    ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    T = max(ns_)
+    got = rl.rollout_batch(S0, ns_, T, ep=1, sched=(1, 3))
+    st = got["status"].cpu().numpy()
+    pinned = [k for k in range(len(S0)) if stable[k]]
+    assert sum(fail[k] is not None for k in pinned) >= 6, "the construction must drop several episodes"
+    assert sum(fail[k] is not None and fail[k] > 5 for k in pinned) >= 2, "and some mid-episode"
+    for k in pinned:
+        assert st[k] == (1 if fail[k] is not None else 0), (k, fail[k], st[k])
+    # a dropped episode's trajectory is NaN from its failing state on, never a stale value
+    S = got["S"].cpu().numpy()
+    for k in pinned:
+        if fail[k] is not None:
+            assert np.isnan(S[k, fail[k] + 1]).any()
+            assert np.isnan(S[k, ns_[k]]).any()
+
+
+def test_kept_episodes_equal_a_clean_run(setup):
+    conf, genv, oe, rl, S0, fail, stable = setup
+    ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    T = max(ns_)
+    got = rl.rollout_batch(S0, ns_, T, ep=1, sched=(1, 3))
+    st = got["status"].cpu().numpy()
+    keep = np.where(st == 0)[0]
+    assert len(keep) >= 30
+    ref = rl.rollout_batch(S0[keep], [ns_[k] for k in keep], T, ep=1)
+    assert (ref["status"].cpu().numpy() == 0).all()
+    for j, k in enumerate(keep):
+        n = ns_[k]
+        np.testing.assert_array_equal(got["S"][k, :n + 1].cpu().numpy(), ref["S"][j, :n + 1].cpu().numpy())
+        np.testing.assert_array_equal(got["A"][k, :n].cpu().numpy(), ref["A"][j, :n].cpu().numpy())
+        np.testing.assert_array_equal(got["R"][k, :n].cpu().numpy(), ref["R"][j, :n].cpu().numpy())
+        np.testing.assert_array_equal(got["EE"][k, :n + 1].cpu().numpy(), ref["EE"][j, :n + 1].cpu().numpy())
+    # the reward / EE pass skipped the NaN states of the dropped episodes (rows stay as allocated)
+    EE = got["EE"].cpu().numpy()
+    S = got["S"].cpu().numpy()
+    for k in np.where(st != 0)[0]:
+        bad = np.isnan(S[k, :ns_[k] + 1]).any(axis=1)
+        assert bad.any()
+        assert (EE[k, :ns_[k] + 1][bad] == 0).all()
+    # kept episodes agree with the oracle's float32 rollout
+    base = load_weights("di_seed0_final")["actor"]
+    act = gated_actor(base)
+    for k in keep[::6]:
+        r = oroll.to_init_rollout(oe, act, S0[k], 1, f32=True)
+        assert r is not None
+        np.testing.assert_allclose(got["S"][k, :ns_[k] + 1].cpu().numpy(), r[0], rtol=1e-4, atol=2e-4)
+
+
+def test_create_to_init_failure_tuple(setup):
+    conf, genv, oe, rl, S0, fail, stable = setup
+    bad = [k for k in range(len(S0)) if stable[k] and fail[k] is not None]
+    good = [k for k in range(len(S0)) if stable[k] and fail[k] is None]
+    for k in bad[:3]:
+        assert rl.create_TO_init(1, S0[k]) == (None, None, None, None, 0)
+    for k in good[:2]:
+        ics, states, controls, n, flag = rl.create_TO_init(1, S0[k])
+        assert flag == 1 and n == conf.NSTEPS - int(S0[k][-1] / conf.dt)
+        assert states.shape == (n + 1, conf.nb_state) and controls.shape == (n, conf.nb_action)
+    # the batched form: one launch, the same tuples in order
+    sel = bad[:3] + good[:4]
+    batch = rl.create_TO_init_batch(1, [S0[k] for k in sel])
+    for k, b in zip(sel, batch):
+        one = rl.create_TO_init(1, S0[k])
+        assert b[4] == one[4]
+        if one[4] == 0:
+            assert b == (None, None, None, None, 0)
+        else:
+            np.testing.assert_array_equal(b[0], one[0])
+            np.testing.assert_array_equal(b[1], one[1])
+            np.testing.assert_array_equal(b[2], one[2])
+            assert b[3] == one[3]
+
+
+def test_ddp_and_buffer_drop_failed_episodes(setup):
+    from cacto_amd.replay_buffer import ReplayBuffer
+    from cacto_amd.to import TO
+    conf, genv, oe, rl, S0, fail, stable = setup
+    ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    T = max(ns_)
+    got = rl.rollout_batch(S0, ns_, T, ep=1, sched=(1, 3))
+    status = got["status"]
+    st = status.cpu().numpy()
+    keep = np.where(st == 0)[0]
+    assert 0 < len(keep) < len(S0)
+    ref = rl.rollout_batch(S0[keep], [ns_[k] for k in keep], T, ep=1)
+    to = TO(genv, conf)
+    n_all = torch.tensor(ns_, dtype=torch.int32, device="cuda")
+    n_keep = torch.tensor([ns_[k] for k in keep], dtype=torch.int32, device="cuda")
+    lab = to.backward_pass_batch(got["S"], got["A"].double(), n_all, status=status)
+    lab_ref = to.backward_pass_batch(ref["S"], ref["A"].double(), n_keep)
+    L, Lr = lab.cpu().numpy(), lab_ref.cpu().numpy()
+    for j, k in enumerate(keep):
+        np.testing.assert_array_equal(L[k, :ns_[k] + 1], Lr[j, :ns_[k] + 1])
+    for k in np.where(st != 0)[0]:
+        assert (L[k] == 0).all()                       # skipped: the zero-initialised rows are untouched
+    E = len(S0)
+    b1, b2 = ReplayBuffer(conf), ReplayBuffer(conf)
+    zero = torch.zeros(E, dtype=torch.float64, device="cuda")
+    b1.add_episodes(got["S"], got["R"], ns_, R_term=zero, dVdx=lab, status=status)
+    b2.add_episodes(ref["S"], ref["R"], [ns_[k] for k in keep], R_term=zero[:len(keep)], dVdx=lab_ref)
+    rows = sum(ns_[k] + 1 for k in keep)
+    assert b1.next_idx == b2.next_idx == rows
+    np.testing.assert_array_equal(b1.storage[:rows].cpu().numpy(), b2.storage[:rows].cpu().numpy())
+    assert not np.isnan(b1.storage[:rows].cpu().numpy()).any()

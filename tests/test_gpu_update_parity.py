@@ -189,6 +189,55 @@ def test_per_loop_car_park_matches_oracle():
     _assert_weights(rl, nets, K)
 
 
+def test_learn_and_update_per_branch_matches_oracle(tmp_path):
+    """RL_AC.learn_and_update(counter, PrioritizedReplayBuffer(conf), ep) itself — the PER branch
+    of RL.py:120-143 as main.py:242 calls it — with UPDATE_LOOPS[ep] = 7 updates starting at
+    counter 2 with save_interval 4, so the loop is cut at both checkpoint saves (counters 4 and 8:
+    chunks of 2, 4 and 1 pipelined updates). The uniforms come from the buffer's own `random`
+    (replay_buffer.py:176-179 draws B per sample call in order); the oracle replays the same
+    stream through its sequential sample -> IS-weighted update -> priority update -> target loop."""
+    import random as pyrandom
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    conf = load_conf("car_park", fresh=True)
+    conf.prioritized_replay_alpha = 0.6
+    conf.UPDATE_LOOPS = np.array([7, 7], dtype=int)
+    conf.save_interval = 4
+    conf.NNs_path = str(tmp_path)
+    (tmp_path / "N_try_0").mkdir()
+    conf, env, oe, rl = _setup("car_park", None, 0.0, conf=conf)
+    per = PrioritizedReplayBuffer(conf, rl.sys, py_random=pyrandom.Random(77))
+    o = obuf.PrioritizedReplayBuffer(conf.REPLAY_SIZE, conf.nb_state, 0.6, conf.prioritized_replay_beta,
+                                     conf.prioritized_replay_eps, conf.fresh_factor, conf.BATCH_SIZE)
+    rng = np.random.default_rng(29)
+    n_rows, B = 3000, conf.BATCH_SIZE
+    rows = _rows(conf, n_rows, rng)
+    per.add_rows(rows)
+    o.add_rows(rows)
+    nets = _weights(rl)
+    counter = rl.learn_and_update(2, per, 1)
+    assert counter == 9
+    ur = pyrandom.Random(77)
+    opt = (onn.KerasAdam(conf.CRITIC_LEARNING_RATE), onn.KerasAdam(conf.ACTOR_LEARNING_RATE))
+    for k in range(7):
+        U = np.array([ur.random() for _ in range(B)])
+        idx = o.sample_proportional(U)
+        w = o.sample_weights(idx).reshape(B, 1)
+        nets, _, _, y, V = _oracle_update(conf, oe, nets, opt, rows[idx], w, 0.0)
+        o.update_priorities(idx, y.astype(np.float32), V.astype(np.float32))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(per.exp_counter[:n_rows].cpu().numpy(), o.exp_counter[:n_rows])
+    cap = per.cap
+    np.testing.assert_allclose(per.sum_tree.cpu().numpy()[cap:cap + n_rows], o.it_sum.value[cap:cap + n_rows],
+                               rtol=2e-5, atol=1e-4)
+    assert rl.steps.cpu().tolist() == [7, 7]
+    _assert_weights(rl, nets, 7)
+    # the checkpoints of the two saves (RL.py:139-141 -> RL_save_weights)
+    for step in (4, 8):
+        for name in ("actor", "critic", "target_critic"):
+            assert (tmp_path / "N_try_0" / ("%s_%d.h5" % (name, step))).exists()
+    assert not (tmp_path / "N_try_0" / "actor_9.h5").exists()
+
+
 # ------------------------------------------------------------------ (c) LR schedule boundary
 def test_manipulator_lr_schedule_crosses_boundary():
     """configs[2]: PiecewiseConstantDecay(boundaries=[200, 300, 400, 500]*REPLAY_SIZE/B, values
