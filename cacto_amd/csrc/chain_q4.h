@@ -4,64 +4,93 @@
 // every activation tile in the F4 layout (one float per lane per 16-feature tile). They write the
 // same operand panels (feature-major, sample rows), so k_wgrad / k_wgrad_adam / k_adam are shared.
 //
-// Per tile a wave owns the out tiles ot = wave, wave + 4, ... of each layer and, after q4_reduce,
-// one element per lane: feature 16 ot + (lane & 15) of sample lane >> 4 (F4 index q4e(ot, lane)).
-// All elementwise arrays (cos / sin / pre-activation / zbar tiles) use the F4 layout, so an epilogue
-// reads its operands at the index it writes. Per-sample work (row gathers, input normalisation,
-// dynamics, losses) runs one (sample, feature) element per thread.
+// 8 waves per workgroup. A chain is a sequence of small dependent layer steps (a few hundred MFMA
+// cycles each for 4 samples), so what bounds it is latency: the barriers between steps and the
+// memory latency of weight fragments that every Adam step has just rewritten (they come from the
+// memory-side cache). The 8 waves are used to cut both:
+//   * the critic's target forward at s' (waves 4-7) runs beside its forward at s (waves 0-3), two
+//     4-wave teams sharing the barriers of one pass;
+//   * every other layer runs as one 8-wave team (out tiles wave, wave + 8), so the actor's 256-wide
+//     layers are one pair of out tiles per wave, loaded together;
+//   * each pass's fragments are issued one phase before the pass (during the previous pass or the
+//     dynamics), so no pass starts on a cold load.
+// After q4_reduce a wave holds, per out tile, one element per lane: feature 16 ot + (lane & 15) of
+// sample lane >> 4 (F4 index q4e(ot, lane)). All elementwise arrays (cos / sin / pre-activation /
+// zbar tiles) use the F4 layout, so an epilogue reads its operands at the index it writes.
+// Per-sample work (row gathers, input normalisation, dynamics, losses) runs one (sample, feature)
+// element per thread.
 //
-// Included by learn_kernels.hip (uses its GradBufs, ChainScalars, clog).
+// Included by learn_kernels.hip (uses its GradBufs, ChainScalars, clog, CSTAMP).
 #pragma once
 
 #include "q4.h"
 
 namespace cacto {
 
+constexpr int Q4_NW = 8;  // waves per q4 chain workgroup
+constexpr int Q4_THREADS = 64 * Q4_NW;
+
 // ---------------------------------------------------------------- critic (fixed 64-64-128-128-1 shape)
+// A forward pass's fragments for a team of NW waves (out tiles wi + NW t): layers 0-1 have 4 out
+// tiles, layers 2-3 have 8, the output layer is split over the team's k-tiles.
+template <int NW>
 struct Q4CriticFwd {
-  Q4Frags<1, 1> f0;
-  Q4Frags<4, 1> f1;
-  Q4Frags<4, 2> f2;
-  Q4Frags<8, 2> f3;
-  Q4Split<2> f4;
+  static constexpr int N8 = 8 / NW;
+  Q4Frags<1, 1, NW> f0;
+  Q4Frags<4, 1, NW> f1;
+  Q4Frags<4, N8, NW> f2;
+  Q4Frags<8, N8, NW> f3;
+  Q4Split<N8, NW> f4;
   template <bool BIAS>
-  __device__ __forceinline__ void load(const NetView& N, int wave, int lane) {
-    f0.load<BIAS>(N.fwd(0), N.biasp(0), 4, 64, wave, lane);
-    f1.load<BIAS>(N.fwd(1), N.biasp(1), 4, 64, wave, lane);
-    f2.load<BIAS>(N.fwd(2), N.biasp(2), 8, 128, wave, lane);
-    f3.load<BIAS>(N.fwd(3), N.biasp(3), 8, 128, wave, lane);
+  __device__ __forceinline__ void load(const NetView& N, int wi, int lane) {
+    f0.template load<BIAS>(N.fwd(0), N.biasp(0), 4, 64, wi, lane);
+    f1.template load<BIAS>(N.fwd(1), N.biasp(1), 4, 64, wi, lane);
+    f2.template load<BIAS>(N.fwd(2), N.biasp(2), 8, 128, wi, lane);
+    f3.template load<BIAS>(N.fwd(3), N.biasp(3), 8, 128, wi, lane);
   }
-  __device__ __forceinline__ void load_last(const NetView& N, int wave, int lane) {
-    f4.load<true>(N.fwd(4), 8, N.biasp(4), 1, wave, lane);
+  __device__ __forceinline__ void load_last(const NetView& N, int wi, int lane) {
+    f4.template load<true>(N.fwd(4), 8, N.biasp(4), 1, wi, lane);
   }
 };
 
-// transposed passes G_l = D_l W_l^T: l3 2 x 8 k-tiles, l2 1 x 8, l1 1 x 4, l0 split-K 1 of 4
+// The transposed passes G_l = D_l W_l^T for an 8-wave team: l3 one of 8 out tiles per wave, l2 / l1
+// 4 out tiles (waves 0-3), l0 split over the 4 k-tiles. Loaded once per chain and used by both the
+// first backward and the backward of the forward graph.
 struct Q4CriticBwd {
-  Q4Frags<8, 2> g3;
-  Q4Frags<8, 1> g2;
-  Q4Frags<4, 1> g1;
-  float w5[2];  // W5[16 (wave + 4 t) + c, 0]: the lane's feature of layer-3 out tiles wave, wave + 4
+  Q4Frags<8, 1, Q4_NW> g3;
+  Q4Frags<8, 1, Q4_NW> g2;
+  Q4Frags<4, 1, Q4_NW> g1;
+  Q4Split<1, Q4_NW> g0;
+  float w5;  // W5[16 wave + c, 0]: the lane's feature of layer-3 out tile `wave`
   __device__ __forceinline__ void load(const NetView& N, int wave, int lane) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) w5[t] = N.flat[N.t.woff[4] + 16 * (wave + 4 * t) + (lane & 15)];
+    load_g3(N, wave, lane);
+    load_rest(N, wave, lane);
+  }
+  // in two parts, so a pass can issue them as its own fragments die
+  __device__ __forceinline__ void load_g3(const NetView& N, int wave, int lane) {
+    w5 = N.flat[N.t.woff[4] + 16 * wave + (lane & 15)];
     g3.load<false>(N.bwd(3), nullptr, 8, 128, wave, lane);
+  }
+  __device__ __forceinline__ void load_rest(const NetView& N, int wave, int lane) {
     g2.load<false>(N.bwd(2), nullptr, 4, 64, wave, lane);
     g1.load<false>(N.bwd(1), nullptr, 4, 64, wave, lane);
+    g0.load<false>(N.bwd(0), 4, nullptr, 16, wave, lane);
   }
 };
 
-// Critic forward over the F4 input tile X0 (see net_common.h critic_forward_tile_f): with Hs every
-// h_l = sin z_l is kept (24 tiles at ZOFF), else h alternates in H (2 x 8 tiles); with Cs cos z_l is
-// kept. hook(l, ot, h) per hidden element; V[i] (LDS) receives sample i's value when WANT_V.
-template <bool WANT_V, typename Hook>
-__device__ void q4_critic_forward_f(const Q4CriticFwd& F, const float* X0, float* Cs, float* Hs, float* H, float* red,
-                                    float* V, const Lane& L, Hook&& hook) {
+// Critic forward over the F4 input tile X0 for a team (net_common.h critic_forward_tile_f): with Hs
+// every h_l = sin z_l is kept (24 tiles at ZOFF), else h alternates in H (2 x 8 tiles); with Cs
+// cos z_l is kept. hook(l, ot, h) per hidden element, mid(l) after layer l's epilogues (the caller
+// issues the next pass's fragment loads there); V[i] (LDS) receives sample i's value when WANT_V.
+// `red`: the team's NW x 64 floats.
+template <bool WANT_V, int NW, typename Hook, typename Mid>
+__device__ void q4_critic_forward_f(const Q4CriticFwd<NW>& F, const float* X0, float* Cs, float* Hs, float* H,
+                                    float* red, float* V, int wi, int lane, Hook&& hook, Mid&& mid) {
   auto epi = [&](int l, float* out) {
     return [&, l, out](int ot, float z) {
       float h, c;
       fast_sincos(z, &h, &c);
-      const int e = q4e(ot, L.lane);
+      const int e = q4e(ot, lane);
       if (Cs) Cs[ZOFF[l] * 64 + e] = c;
       out[e] = h;
       hook(l, ot, h);
@@ -69,60 +98,51 @@ __device__ void q4_critic_forward_f(const Q4CriticFwd& F, const float* X0, float
   };
   const float* in = X0;
   float* out = Hs ? Hs + ZOFF[0] * 64 : H;
-  F.f0.run<true>(in, 4, L.wave, L.lane, epi(0, out));
+  F.f0.template run<true>(in, 4, wi, lane, epi(0, out));
+  mid(0);
   __syncthreads();
   in = out;
   out = Hs ? Hs + ZOFF[1] * 64 : H + 8 * 64;
-  F.f1.run<true>(in, 4, L.wave, L.lane, epi(1, out));
+  F.f1.template run<true>(in, 4, wi, lane, epi(1, out));
+  mid(1);
   __syncthreads();
   in = out;
   out = Hs ? Hs + ZOFF[2] * 64 : H;
-  F.f2.run<true>(in, 8, L.wave, L.lane, epi(2, out));
+  F.f2.template run<true>(in, 8, wi, lane, epi(2, out));
+  mid(2);
   __syncthreads();
   in = out;
   out = Hs ? Hs + ZOFF[3] * 64 : H + 8 * 64;
-  F.f3.run<true>(in, 8, L.wave, L.lane, epi(3, out));
+  F.f3.template run<true>(in, 8, wi, lane, epi(3, out));
+  mid(3);
   __syncthreads();
   if (WANT_V) {
-    F.f4.run<true>(8, out, red, L.wave, L.lane, [&](int, float v) {
-      if ((L.lane & 15) == 0) V[L.lane >> 4] = v;
+    F.f4.template run<true>(8, out, red, wi, lane, [&](int, float v) {
+      if ((lane & 15) == 0) V[lane >> 4] = v;
     });
     __syncthreads();
   }
 }
 
-template <bool WANT_V, typename Hook>
-__device__ void q4_critic_forward(const NetView& N, const float* X0, float* Cs, float* Hs, float* H, float* red,
-                                  float* V, const Lane& L, Hook&& hook) {
-  Q4CriticFwd F;
-  F.load<true>(N, L.wave, L.lane);
-  if (WANT_V) F.load_last(N, L.wave, L.lane);
-  q4_critic_forward_f<WANT_V>(F, X0, Cs, Hs, H, red, V, L, hook);
-}
-
-// Critic input gradient from the cos tiles Cs (net_common.h critic_first_backward): G4 = W5,
-// D_l = G_{l+1} cos z_l, G_l = D_l W_l^T. G tiles (G1 at 0, G2 at 4, G3 at 8) when Gs, D via
-// hookD(l, ot, d), dV/dx0 in G0 (F4, one tile).
-template <typename HookD>
-__device__ void q4_critic_first_backward(const NetView& N, const float* Cs, float* P /* 2 x 8 tiles */, float* Gs,
-                                         float* G0, float* red, const Lane& L, HookD&& hookD) {
+// Critic input gradient from the cos tiles Cs (net_common.h critic_first_backward), 8 waves:
+// G4 = W5, D_l = G_{l+1} cos z_l, G_l = D_l W_l^T. G tiles (G1 at 0, G2 at 4, G3 at 8) when Gs,
+// D via hookD(l, ot, d), dV/dx0 in G0 (F4, one tile); mid() after the first transposed layer.
+template <typename HookD, typename Mid>
+__device__ void q4_critic_first_backward(const Q4CriticBwd& F, const float* Cs, float* P /* 2 x 8 tiles */,
+                                         float* Gs, float* G0, float* red, int wave, int lane, HookD&& hookD,
+                                         Mid&& mid) {
   const int goff[4] = {0, 0, 4, 8};
-  Q4CriticBwd F;
-  F.load(N, L.wave, L.lane);
-  Q4Split<1> F0;
-  F0.load<false>(N.bwd(0), 4, nullptr, 16, L.wave, L.lane);
   float* D = P;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int ot = L.wave + 4 * t, e = q4e(ot, L.lane);
-    const float d = fmul(F.w5[t], Cs[ZOFF[3] * 64 + e]);
+  {
+    const int e = q4e(wave, lane);
+    const float d = fmul(F.w5, Cs[ZOFF[3] * 64 + e]);
     D[e] = d;
-    hookD(3, ot, d);
+    hookD(3, wave, d);
   }
   __syncthreads();
   auto epi = [&](int l, float* Dn) {
     return [&, l, Dn](int it, float g) {
-      const int e = q4e(it, L.lane);
+      const int e = q4e(it, lane);
       if (Gs) Gs[goff[l] * 64 + e] = g;
       const float d = fmul(g, Cs[ZOFF[l - 1] * 64 + e]);
       Dn[e] = d;
@@ -130,18 +150,19 @@ __device__ void q4_critic_first_backward(const NetView& N, const float* Cs, floa
     };
   };
   float* Dn = P + 8 * 64;
-  F.g3.run<false>(D, 8, L.wave, L.lane, epi(3, Dn));
+  F.g3.run<false>(D, 8, wave, lane, epi(3, Dn));
+  mid();
   __syncthreads();
   D = Dn;
   Dn = P;
-  F.g2.run<false>(D, 4, L.wave, L.lane, epi(2, Dn));
+  F.g2.run<false>(D, 4, wave, lane, epi(2, Dn));
   __syncthreads();
   D = Dn;
   Dn = P + 8 * 64;
-  F.g1.run<false>(D, 4, L.wave, L.lane, epi(1, Dn));
+  F.g1.run<false>(D, 4, wave, lane, epi(1, Dn));
   __syncthreads();
   D = Dn;
-  F0.run<false>(4, D, red, L.wave, L.lane, [&](int, float g) { G0[q4e(0, L.lane)] = g; });
+  F.g0.run<false>(4, D, red, wave, lane, [&](int, float g) { G0[q4e(0, lane)] = g; });
   __syncthreads();
 }
 
@@ -169,15 +190,16 @@ struct Q4CriticLds {
   float X0[64], XT[64], G0[64];
   float Cs[24 * 64];  // cos z_l
   float Hs[24 * 64];  // h_l = sin z_l
+  float HT[16 * 64];  // the target forward's h ping-pong (waves 4-7)
   float G[16 * 64];
   float ZB[24 * 64];
   float GB[16 * 64];
-  float red[4 * 64];
+  float red[Q4_NW * 64];
   float stage[4 * 64];  // gathered rows: [0] s, [1] s_next, [2] dV/dx, [3] (R, d, w) per sample
-  float Vn[4], V[4], y[4], Vb[4], Vt2[4];
+  float Vn[4], V[4], y[4], Vb[4], Vt2[4], Vx[4];
 };
 
-// one 4-sample tile of the critic chain (critic_chain's operations, F4 layout)
+// one 4-sample tile of the critic chain (critic_chain's operations, F4 layout, 8 waves)
 __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, const SysDevice* __restrict__ sdp,
                                                 const NetView& C, const NetView& Tg, const ChainScalars& cs,
                                                 const double* __restrict__ storage, const int32_t* __restrict__ idx,
@@ -186,116 +208,138 @@ __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, 
                                                 float* __restrict__ Vt_out, int32_t* __restrict__ step) {
   float *X0 = S.X0, *XT = S.XT, *G0 = S.G0, *Cs = S.Cs, *Hs = S.Hs, *G = S.G, *ZB = S.ZB, *GB = S.GB, *red = S.red;
   const cacto_sys_params& p = sdp->p;
-  const Lane L;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int team = wave >> 2, wi4 = wave & 3;  // the two 4-wave teams of the forward passes
   const int ns = p.nb_state, cols = 3 * ns + 3, s0 = tile * Q4_TILE;
   const int ld = gb.ld, Bp = gb.Bp;
   const bool sob = cs.w_S != 0.f;
   const int goff[4] = {0, 0, 4, 8};
-  if (tile == 0 && L.tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
+  CSTAMP(0);
+  if (tile == 0 && tid == 0 && step) step[0] += 1;  // Keras critic optimizer iterations
 
-  Q4CriticFwd TF;  // the target network, in flight during the row gathers
-  float w5[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) w5[t] = C.flat[C.t.woff[4] + 16 * (L.wave + 4 * t) + L.c];
-  const Q4Norm nrm(p, L.lane);
-  {
+  // the forward passes' fragments, in flight during the row gathers: waves 0-3 the critic (forward
+  // at s), waves 4-7 the target network (forward at s')
+  Q4CriticFwd<4> F;
+  const NetView& FN = team ? Tg : C;
+  const float w5 = C.flat[C.t.woff[4] + 16 * wave + (lane & 15)];
+  const Q4Norm nrm(p, lane);
+  if (wave < 4) {
     // one (sample c, column) per lane, wave w gathers array w: s, s_next, dV/dx, then (R, d, w);
-    // branch-free (clamped indices, zeroed after), so no load sits under a branch
-    const int c = L.lane >> 4, f = L.lane & 15;
+    // branch-free inside (clamped indices, zeroed after), so no load sits under a lane branch
+    const int c = lane >> 4, f = lane & 15;
     const bool valid = s0 + c < B;
     const int sc = min(s0 + c, B - 1), fc = min(f, ns - 1);
     const int32_t row = idx[sc];
-    TF.load<true>(Tg, L.wave, L.lane);
-    TF.load_last(Tg, L.wave, L.lane);
-    const int col = L.wave == 0 ? fc : L.wave < 3 ? L.wave * ns + 1 + fc : (f == 0 ? ns : 3 * ns + 1);
+    F.load<true>(FN, wi4, lane);
+    F.load_last(FN, wi4, lane);
+    const int col = wave == 0 ? fc : wave < 3 ? wave * ns + 1 + fc : (f == 0 ? ns : 3 * ns + 1);
     const double x = storage[(size_t)row * cols + col];
     const float wv = isw ? isw[sc] : 1.f;
-    const bool keep = valid && (L.wave < 3 ? f < ns : f < 2);
+    const bool keep = valid && (wave < 3 ? f < ns : f < 2);
     float v = keep ? (float)x : 0.f;
-    if (L.wave == 3 && f == 2) v = valid ? wv : 0.f;
-    S.stage[L.wave * 64 + c * 16 + f] = v;
+    if (wave == 3 && f == 2) v = valid ? wv : 0.f;
+    S.stage[wave * 64 + c * 16 + f] = v;
+  } else {
+    F.load<true>(FN, wi4, lane);
+    F.load_last(FN, wi4, lane);
   }
   __syncthreads();
-  if (L.wave < 2) {  // wave 0: X0, wave 1: XT (element lane = 4 f + i)
-    const int f = L.lane >> 2, i = L.lane & 3;
-    const float v = nrm.forward(S.stage[L.wave * 64 + i * 16 + min(f, 15)]);
-    (L.wave == 0 ? X0 : XT)[L.lane] = v;
+  if (wave < 2) {  // wave 0: X0, wave 1: XT (element lane = 4 f + i)
+    const int f = lane >> 2, i = lane & 3;
+    const float v = nrm.forward(S.stage[wave * 64 + i * 16 + min(f, 15)]);
+    (wave == 0 ? X0 : XT)[lane] = v;
+    if (wave == 0) gb.LT[0][(size_t)f * ld + Bp + s0 + i] = v;  // LT_0 second half: the input at s
   }
   __syncthreads();
+  CSTAMP(1);
   const float* Rs = S.stage + 3 * 64;  // Rs[16 c] = R, [16 c + 1] = d, [16 c + 2] = w
 
-  // y = R + (1 - d) * V_tgt(s_next)   (NeuralNetwork.py:153-158)
-  if (!cs.MC) q4_critic_forward_f<true>(TF, XT, nullptr, nullptr, Hs, red, S.Vn, L, [](int, int, float) {});
-  if (L.tid < 4) {
-    const int c = L.tid;
+  // forward at s (waves 0-3: sin z, cos z kept, h_l -> LT_l second half) beside the target
+  // forward at s' (waves 4-7: y = R + (1 - d) * V_tgt(s_next), NeuralNetwork.py:153-158; run even
+  // for MC, whose y ignores it). The transposed fragments of the backward passes are issued after
+  // layer 2.
+  Q4CriticBwd HB;
+  q4_critic_forward_f<true, 4>(
+      F, team ? XT : X0, team ? nullptr : Cs, team ? nullptr : Hs, team ? S.HT : Hs, red + team * 4 * 64,
+      team ? S.Vn : S.V, wi4, lane,
+      [&](int l, int ot, float h) {
+        if (team == 0) q4_store_panel(gb.LT[l + 1], ld, Bp + s0, ot, lane, h);
+      },
+      [&](int l) {
+        if (l == 2) HB.load_g3(C, wave, lane);
+        if (l == 3) HB.load_rest(C, wave, lane);
+      });
+  if (tid < 4) {
+    const int c = tid;
     S.y[c] = cs.MC ? Rs[16 * c] : fadd(Rs[16 * c], fmul(fsub(1.f, Rs[16 * c + 1]), S.Vn[c]));
   }
-  if (cs.want_vt) q4_critic_forward_f<true>(TF, X0, nullptr, nullptr, Hs, red, S.Vt2, L, [](int, int, float) {});
-
-  // forward at s, keeping sin z and cos z; h_l -> LT_l second half
-  if (L.wave == 0) {
-    const int f = L.lane >> 2, i = L.lane & 3;
-    gb.LT[0][(size_t)f * ld + Bp + s0 + i] = X0[L.lane];
+  CSTAMP(2);
+  if (cs.want_vt) {  // the extra V_tgt(s) of NeuralNetwork.py:178 (waves 4-7; waves 0-3 repeat into scratch)
+    q4_critic_forward_f<true, 4>(F, X0, nullptr, nullptr, team ? S.HT : GB, red + team * 4 * 64,
+                                 team ? S.Vt2 : S.Vx, wi4, lane, [](int, int, float) {}, [](int) {});
   }
-  q4_critic_forward<true>(C, X0, Cs, Hs, Hs, red, S.V, L,
-                          [&](int l, int ot, float h) { q4_store_panel(gb.LT[l + 1], ld, Bp + s0, ot, L.lane, h); });
+  CSTAMP(3);
 
+  Q4CriticFwd<Q4_NW> SF;  // the forward fragments of the Sobolev passes (8-wave layout, no bias)
   if (sob) {
     // first backward: D_l -> RT_l first half; G_l kept; G_0 = dV/dx0
-    q4_critic_first_backward(C, Cs, GB, G, G0, red, L,
-                             [&](int l, int ot, float d) { q4_store_panel(gb.RT[l], ld, s0, ot, L.lane, d); });
-    Q4CriticFwd SF;
-    SF.load<false>(C, L.wave, L.lane);
+    q4_critic_first_backward(
+        HB, Cs, GB, G, G0, red, wave, lane, [&](int l, int ot, float d) { q4_store_panel(gb.RT[l], ld, s0, ot, lane, d); },
+        [&]() { SF.load<false>(C, wave, lane); });
+    CSTAMP(4);
     // Sobolev loss gradient w.r.t. dV/ds, then w.r.t. G_0 (NeuralNetwork.py:167-170): element
     // (feature f, sample i) = lane 4 f + i of wave 0
-    if (L.wave == 0) {
-      const int f = L.lane >> 2, i = L.lane & 3;
+    if (wave == 0) {
+      const int f = lane >> 2, i = lane & 3;
       float gb0 = 0.f;
       if (f < ns - 1) {
         const float nf = (float)p.state_norm[f];
         auto nback = [&](float g) { return !p.normalize ? g : fdiv(g, nf); };  // not the time column
         const float gsq = fdiv(fmul(fdiv(1.f, (float)cs.B_global), Rs[16 * i + 2]), (float)(ns - 1));
-        const float dvds = nback(G0[L.lane]);
+        const float dvds = nback(G0[lane]);
         const float yp = clog(dvds), yt = clog(S.stage[2 * 64 + i * 16 + f]);
         const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
         gb0 = nback(clog_backward(dvds, gyp));
       }
-      GB[L.lane] = gb0;
+      GB[lane] = gb0;
       gb.LT[0][(size_t)f * ld + s0 + i] = gb0;
     }
     __syncthreads();
+    CSTAMP(5);
     // backward of the first backward, l = 0..3, on the forward fragments (no bias)
     auto sp_epi = [&](int l, float* nxt) {
       return [&, l, nxt](int ot, float acc) {
-        const int e = q4e(ot, L.lane);
+        const int e = q4e(ot, lane);
         const float sz = Hs[ZOFF[l] * 64 + e], cz = Cs[ZOFF[l] * 64 + e];
-        const float gu = l < 3 ? G[goff[l + 1] * 64 + e] : (ot >= 4 ? w5[1] : w5[0]);
-        ZB[ZOFF[l] * 64 + e] = fmul(-fmul(acc, gu), sz);  // CosGrad: -grad * sin(x)
-        const float gn = fmul(acc, cz);                    // MulGrad into the upstream grad
+        const float gu = l < 3 ? G[goff[l + 1] * 64 + e] : w5;  // layer 3: out tile `wave`
+        ZB[ZOFF[l] * 64 + e] = fmul(-fmul(acc, gu), sz);       // CosGrad: -grad * sin(x)
+        const float gn = fmul(acc, cz);                         // MulGrad into the upstream grad
         nxt[e] = gn;
-        q4_store_panel(gb.LT[l + 1], ld, s0, ot, L.lane, gn);
+        q4_store_panel(gb.LT[l + 1], ld, s0, ot, lane, gn);
       };
     };
     float* nA = GB + 8 * 64;
-    SF.f0.run<false>(GB, 4, L.wave, L.lane, sp_epi(0, nA));
+    SF.f0.run<false>(GB, 4, wave, lane, sp_epi(0, nA));
     __syncthreads();
-    SF.f1.run<false>(nA, 4, L.wave, L.lane, sp_epi(1, GB));
+    CSTAMP(6);
+    SF.f1.run<false>(nA, 4, wave, lane, sp_epi(1, GB));
     __syncthreads();
-    SF.f2.run<false>(GB, 8, L.wave, L.lane, sp_epi(2, nA));
+    CSTAMP(7);
+    SF.f2.run<false>(GB, 8, wave, lane, sp_epi(2, nA));
     __syncthreads();
-    SF.f3.run<false>(nA, 8, L.wave, L.lane, sp_epi(3, GB));
+    CSTAMP(8);
+    SF.f3.run<false>(nA, 8, wave, lane, sp_epi(3, GB));
     __syncthreads();
-    if (L.tid < 4) gb.RT[4][s0 + L.tid] = 1.f;  // dW5 += Gbar_4 (G_4 = W5[:, 0])
+    CSTAMP(9);
+    if (tid < 4) gb.RT[4][s0 + tid] = 1.f;  // dW5 += Gbar_4 (G_4 = W5[:, 0])
   } else {
-    for (int k = L.tid; k < 24 * 64; k += CACTO_THREADS) ZB[k] = 0.f;
+    for (int k = tid; k < 24 * 64; k += Q4_THREADS) ZB[k] = 0.f;
   }
+  CSTAMP(10);
 
-  // the transposed fragments of the last backward pass, in flight during the value loss
-  Q4CriticBwd HB;
-  HB.load(C, L.wave, L.lane);
   // value loss: Vbar = (2 * ((wS/B) * w)) * (V - y)   (Keras MSE, SUM_OVER_BATCH_SIZE)
-  if (L.tid < 4) {
-    const int c = L.tid;
+  if (tid < 4) {
+    const int c = tid;
     const float wv = sob ? cs.w_S : 1.f;
     const float gl = fmul(fdiv(wv, (float)cs.B_global), Rs[16 * c + 2]);
     S.Vb[c] = fmul(fmul(2.f, gl), fsub(S.V[c], S.y[c]));
@@ -307,37 +351,42 @@ __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, 
     }
   }
   __syncthreads();
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {  // zbar_3 += (Vbar * W5) * cos(z3): out tiles wave, wave + 4
-    const int e = q4e(L.wave + 4 * t, L.lane);
-    const float vb = S.Vb[L.lane >> 4];
-    ZB[ZOFF[3] * 64 + e] = fadd(ZB[ZOFF[3] * 64 + e], fmul(fmul(vb, w5[t]), Cs[ZOFF[3] * 64 + e]));
+  {  // zbar_3 += (Vbar * W5) * cos(z3): out tile `wave`
+    const int e = ZOFF[3] * 64 + q4e(wave, lane);
+    ZB[e] = fadd(ZB[e], fmul(fmul(S.Vb[lane >> 4], w5), Cs[e]));
   }
   __syncthreads();
+  CSTAMP(11);
   // backward through the forward graph: zbar_{l-1} += (zbar_l W_l^T) * cos(z_{l-1})
   auto hb_epi = [&](int l) {
     return [&, l](int it, float acc) {
-      const int e = ZOFF[l - 1] * 64 + q4e(it, L.lane);
+      const int e = ZOFF[l - 1] * 64 + q4e(it, lane);
       ZB[e] = fadd(ZB[e], fmul(acc, Cs[e]));
     };
   };
   auto store_rt = [&](int l) {
-    for (int ot = L.wave; ot < C.t.OT[l]; ot += CACTO_NWAVES)
-      q4_store_panel(gb.RT[l], ld, Bp + s0, ot, L.lane, ZB[ZOFF[l] * 64 + q4e(ot, L.lane)]);
+    for (int ot = wave; ot < C.t.OT[l]; ot += Q4_NW)
+      q4_store_panel(gb.RT[l], ld, Bp + s0, ot, lane, ZB[ZOFF[l] * 64 + q4e(ot, lane)]);
   };
   store_rt(3);
-  HB.g3.run<false>(ZB + ZOFF[3] * 64, 8, L.wave, L.lane, hb_epi(3));
+  HB.g3.run<false>(ZB + ZOFF[3] * 64, 8, wave, lane, hb_epi(3));
   __syncthreads();
+  CSTAMP(12);
   store_rt(2);
-  HB.g2.run<false>(ZB + ZOFF[2] * 64, 4, L.wave, L.lane, hb_epi(2));
+  HB.g2.run<false>(ZB + ZOFF[2] * 64, 4, wave, lane, hb_epi(2));
   __syncthreads();
+  CSTAMP(13);
   store_rt(1);
-  HB.g1.run<false>(ZB + ZOFF[1] * 64, 4, L.wave, L.lane, hb_epi(1));
+  HB.g1.run<false>(ZB + ZOFF[1] * 64, 4, wave, lane, hb_epi(1));
   __syncthreads();
+  CSTAMP(14);
   store_rt(0);
+  CSTAMP(15);
+  __syncthreads();
+  CSTAMP_FLUSH;
 }
 
-__global__ void __launch_bounds__(CACTO_THREADS)
+__global__ void __launch_bounds__(Q4_THREADS)
     k_critic_grad_q4(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, ChainScalars cs,
                      const double* __restrict__ storage, const int32_t* __restrict__ idx,
                      const float* __restrict__ isw, int B, GradBufs gb, float* __restrict__ y_out,
@@ -352,7 +401,7 @@ struct Q4ActorLds {
   float ZA[32 * 64];  // actor z1, z2
   float H[32 * 64];   // actor h ping-pong; later critic H (16 tiles) + actor zbar2 (16)
   float ZC[24 * 64];  // critic cos z at s'
-  float red[4 * 64];
+  float red[Q4_NW * 64];
   float st[64], stn[64], gn[64];  // [sample][16]
   float A[Q4_TILE * CACTO_MAX_ACTION];
   float Fu[Q4_TILE * CACTO_MAX_STATE * CACTO_MAX_ACTION];
@@ -360,8 +409,8 @@ struct Q4ActorLds {
   double term_s[Q4_TILE];
 };
 
-// one 4-sample tile of the actor chain (actor_chain's operations, F4 layout). The actor's shape is
-// fixed (ns -> 256 -> 256 -> na, ns, na <= 16: KT = 1 / 16 / 16, OT = 16 / 16 / 1; the host checks).
+// one 4-sample tile of the actor chain (actor_chain's operations, F4 layout, 8 waves). The actor's
+// shape is fixed (ns -> 256 -> 256 -> na, ns, na <= 16: KT = 1 / 16 / 16, OT = 16 / 16 / 1).
 template <int NJ>
 __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, const SysDevice* __restrict__ sdp,
                                                const NetView& Ac, const NetView& C, const ChainScalars& cs,
@@ -370,52 +419,63 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   float *X0 = S.X0, *XS = S.XS, *G0 = S.G0, *ZB3 = S.ZB3, *ZA = S.ZA, *H = S.H, *ZC = S.ZC, *red = S.red;
   const SysDevice& sd = *sdp;
   const cacto_sys_params& p = sd.p;
-  const Lane L;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int ns = p.nb_state, na = p.nb_action, cols = 3 * ns + 3, s0 = tile * Q4_TILE;
   const int ld = gb.ld;
-  if (tile == 0 && L.tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
-  Q4Frags<1, 4> F1;  // actor layer 1 (ns -> 256), in flight during the row gathers
-  F1.load<true>(Ac.fwd(0), Ac.biasp(0), 16, 256, L.wave, L.lane);
-  if (L.wave == 0) {
-    const int c = L.lane >> 4, f = L.lane & 15;
+  CSTAMP(0);
+  if (tile == 0 && tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
+  // layer 1 (ns -> 256) and the wave's pair of layer-2 out tiles, in flight during the row gathers
+  Q4Frags<1, 2, Q4_NW> F1;
+  F1.load<true>(Ac.fwd(0), Ac.biasp(0), 16, 256, wave, lane);
+  Q4Pair<16, Q4_NW> W2;
+  W2.load(Ac.fwd(1), 0, wave, lane);
+  if (wave == 0) {
+    const int c = lane >> 4, f = lane & 15;
     const bool valid = s0 + c < B;
     const double* rp = storage + (size_t)(valid ? idx[s0 + c] : 0) * cols;
     S.st[c * 16 + f] = (valid && f < ns) ? (float)rp[f] : 0.f;
     if (f == 0) S.term_s[c] = valid ? rp[3 * ns + 2] : 0.0;
   }
   __syncthreads();
-  if (L.wave == 0) {  // input of layer 0 (normalised) -> LT_0
-    const int f = L.lane >> 2, i = L.lane & 3;
+  if (wave == 0) {  // input of layer 0 (normalised) -> LT_0
+    const int f = lane >> 2, i = lane & 3;
     const float v = f < ns ? normalize_feature(p, f, S.st[i * 16 + f]) : 0.f;
-    X0[L.lane] = v;
+    X0[lane] = v;
     gb.LT[0][(size_t)f * ld + s0 + i] = v;
   }
   __syncthreads();
+  CSTAMP(1);
   // actor forward; z1, z2 kept; h1 -> LT_1, h2 -> LT_2
   auto lepi = [&](int l) {
     return [&, l](int ot, float z) {
       const float h = z > 0.f ? z : fmul(z, 0.3f);  // LeakyReLU(alpha=0.3)
-      const int e = q4e(ot, L.lane);
+      const int e = q4e(ot, lane);
       ZA[l * 16 * 64 + e] = z;
       H[l * 16 * 64 + e] = h;
-      q4_store_panel(gb.LT[l + 1], ld, s0, ot, L.lane, h);
+      q4_store_panel(gb.LT[l + 1], ld, s0, ot, lane, h);
     };
   };
-  Q4Split<4> F3;  // the action layer (256 -> na), issued with layer 1's MFMAs
-  F1.run<true>(X0, 16, L.wave, L.lane, lepi(0));
-  F3.load<true>(Ac.fwd(2), 16, Ac.biasp(2), na, L.wave, L.lane);
+  F1.run<true>(X0, 16, wave, lane, lepi(0));
+  Q4Split<2, Q4_NW> F3;  // the action layer (256 -> na)
+  F3.load<true>(Ac.fwd(2), 16, Ac.biasp(2), na, wave, lane);
   __syncthreads();
-  q4_layer_t<16, true>(Ac.fwd(1), 16, H, L.wave, L.lane, lepi(1), Ac.biasp(1), 256);
+  q4_layer_pairs<16, true, Q4_NW>(Ac.fwd(1), H, wave, lane, lepi(1), Ac.biasp(1), W2);
+  // the critic's forward fragments at s', in flight during the action layer and the dynamics (for
+  // the revolute chains after the dynamics: their float64 recursions need the registers)
+  constexpr bool early_cf = NJ <= 2;
+  Q4CriticFwd<Q4_NW> CF;
+  if (early_cf) CF.load<true>(C, wave, lane);
   __syncthreads();
-  F3.run<true>(16, H + 16 * 64, red, L.wave, L.lane, [&](int, float v) {
-    const int f = L.lane & 15;
-    if (f < na) S.A[(L.lane >> 4) * na + f] = v;
+  F3.run<true>(16, H + 16 * 64, red, wave, lane, [&](int, float v) {
+    const int f = lane & 15;
+    if (f < na) S.A[(lane >> 4) * na + f] = v;
   });
   __syncthreads();
+  CSTAMP(2);
   // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
-  if (L.tid < Q4_TILE) {
+  if (tid < Q4_TILE) {
     constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
-    const int c = L.tid;
+    const int c = tid;
     double s[NS], a[NA], sn[NS], F[NS * NA];
 #pragma unroll
     for (int f = 0; f < NS; ++f) s[f] = (double)S.st[c * 16 + f];
@@ -431,11 +491,11 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
     for (int f = 0; f < 16; ++f) S.stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
 #pragma unroll
     for (int k = 0; k < NS * NA; ++k) S.Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
-  } else if (L.tid >= 64 && L.tid < 64 + Q4_TILE) {
+  } else if (tid >= 64 && tid < 64 + Q4_TILE) {
     // wave 1, alongside the dynamics: only d reward / d a enters the actor gradient
     // (NeuralNetwork.py:199-204), and only the control cost depends on a
     constexpr int NA = Dims<NJ>::NA;
-    const int c = L.tid - 64;
+    const int c = tid - 64;
     float af[NA], g[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) af[i] = S.A[c * na + i];
@@ -446,30 +506,40 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
     for (int i = 0; i < NA; ++i) S.dra[c * na + i] = g[i];
   }
   __syncthreads();
-  if (L.wave == 0) {
-    const int f = L.lane >> 2, i = L.lane & 3;
-    XS[L.lane] = f < ns ? normalize_feature(p, f, S.stn[i * 16 + f]) : 0.f;
+  CSTAMP(3);
+  if (!early_cf) CF.load<true>(C, wave, lane);
+  if (wave == 0) {
+    const int f = lane >> 2, i = lane & 3;
+    XS[lane] = f < ns ? normalize_feature(p, f, S.stn[i * 16 + f]) : 0.f;
   }
   __syncthreads();
+  CSTAMP(4);
   // critic (already updated) at s': dV/dx0 (NeuralNetwork.py:190-195); V(s') is not used
-  float* HC = H;              // 16 tiles
-  float* ZB2 = H + 16 * 64;   // 16 tiles
-  q4_critic_forward<false>(C, XS, ZC, nullptr, HC, red, nullptr, L, [](int, int, float) {});
-  q4_critic_first_backward(C, ZC, HC, nullptr, G0, red, L, [](int, int, float) {});
+  float* HC = H;             // 16 tiles
+  float* ZB2 = H + 16 * 64;  // 16 tiles
+  Q4CriticBwd CB;
+  q4_critic_forward_f<false, Q4_NW>(CF, XS, ZC, nullptr, HC, red, nullptr, wave, lane, [](int, int, float) {},
+                                    [&](int l) {
+                                      if (l == 1) CB.load(C, wave, lane);
+                                    });
+  CSTAMP(5);
+  // the backward layers' fragments (W3^T: KT = 1; W2^T: the wave's pair), in flight from the
+  // middle of the critic's first backward through the dQ/da phase
+  Q4Frags<1, 2, Q4_NW> B2;
+  Q4Pair<16, Q4_NW> B1;
+  q4_critic_first_backward(CB, ZC, HC, nullptr, G0, red, wave, lane, [](int, int, float) {}, [&]() {
+    B2.load<false>(Ac.bwd(2), nullptr, 16, 256, wave, lane);
+    B1.load(Ac.bwd(1), 0, wave, lane);
+  });
+  CSTAMP(6);
   // dQ/da = dV/ds' Fu + dr/da ; abar = -dQ/da / B  (NeuralNetwork.py:206-231)
-  if (L.wave == 0) {  // d normalize / d s of every (state f, sample i) element at once
-    const int f = L.lane >> 2, i = L.lane & 3;
-    if (f < ns) S.gn[i * 16 + f] = normalize_backward(p, f, G0[L.lane]);
+  if (wave == 0) {  // d normalize / d s of every (state f, sample i) element at once
+    const int f = lane >> 2, i = lane & 3;
+    if (f < ns) S.gn[i * 16 + f] = normalize_backward(p, f, G0[lane]);
   }
-  // the two backward layers' first fragments, in flight during the rest of the dQ/da phase
-  // (W3^T: KT = 1, every tile; W2^T: the first tile's 16 blocks)
-  Q4Frags<1, 4> B2;
-  FragTile<16> B1;
-  B2.load<false>(Ac.bwd(2), nullptr, 16, 256, L.wave, L.lane);
-  B1.load(Ac.bwd(1), L.wave, L.lane);
   __syncthreads();
-  if (L.wave == 0) {  // element (action j, sample i) = lane 4 j + i
-    const int j = L.lane >> 2, i = L.lane & 3;
+  if (wave == 0) {  // element (action j, sample i) = lane 4 j + i
+    const int j = lane >> 2, i = lane & 3;
     float abar = 0.f;
     if (j < na && s0 + i < B) {
       float q = 0.f;
@@ -480,27 +550,36 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
       q = fadd(q, S.dra[i * na + j]);
       abar = fmul(-q, fdiv(1.f, (float)cs.B_global));
     }
-    ZB3[L.lane] = abar;
+    ZB3[lane] = abar;
     gb.RT[2][(size_t)j * ld + s0 + i] = abar;
   }
   __syncthreads();
+  CSTAMP(7);
   // zbar2 = (abar W3^T) * lrelu'(z2) ; zbar1 = (zbar2 W2^T) * lrelu'(z1)
   auto bepi = [&](int l) {
     return [&, l](int it, float acc) {
-      const int e = q4e(it, L.lane);
+      const int e = q4e(it, lane);
       const float z = ZA[l * 16 * 64 + e];
       const float o = z > 0.f ? acc : fmul(acc, 0.3f);
       if (l == 1) ZB2[e] = o;
-      q4_store_panel(gb.RT[l], ld, s0, it, L.lane, o);
+      q4_store_panel(gb.RT[l], ld, s0, it, lane, o);
     };
   };
-  B2.run<false>(ZB3, 16, L.wave, L.lane, bepi(1));
+  B2.run<false>(ZB3, 16, wave, lane, bepi(1));
   __syncthreads();
-  q4_layer_t<16, false>(Ac.bwd(1), 16, ZB2, L.wave, L.lane, bepi(0), nullptr, 256, &B1);
+  CSTAMP(8);
+  q4_layer_pairs<16, false, Q4_NW>(Ac.bwd(1), ZB2, wave, lane, bepi(0), nullptr, B1);
+  CSTAMP(9);
+  __syncthreads();
+  CSTAMP_FLUSH;
+#ifdef CACTO_STAMPS
+  if (tile == 0 && tid == 0)
+    for (int k_ = 0; k_ < 32; ++k_) g_astamps[k_] = cacto_stamp_s[k_];
+#endif
 }
 
 template <int NJ>
-__global__ void __launch_bounds__(CACTO_THREADS)
+__global__ void __launch_bounds__(Q4_THREADS)
     k_actor_grad_q4(const SysDevice* __restrict__ sdp, NetView Ac, NetView C, ChainScalars cs,
                     const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
                     int32_t* __restrict__ step) {
@@ -511,7 +590,7 @@ __global__ void __launch_bounds__(CACTO_THREADS)
 // the critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the rest)
 // in one grid, as k_chain_pair
 template <int NJ>
-__global__ void __launch_bounds__(CACTO_THREADS)
+__global__ void __launch_bounds__(Q4_THREADS)
     k_chain_pair_q4(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, NetView Ac, ChainScalars cs,
                     const double* __restrict__ storage, const int32_t* __restrict__ idx_c,
                     const float* __restrict__ isw, const int32_t* __restrict__ idx_a, int B, int nct, GradBufs gbc,

@@ -1100,7 +1100,7 @@ struct LaunchActorChain {
                  const int32_t* idx, int B, GradBufs gb, int32_t* step, hipStream_t st) {
     const int Bp = (B + 15) / 16 * 16;
     if (chain_tile(Bp) == Q4_TILE)
-      hipLaunchKernelGGL(k_actor_grad_q4<NJ>, dim3(Bp / Q4_TILE), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs,
+      hipLaunchKernelGGL(k_actor_grad_q4<NJ>, dim3(Bp / Q4_TILE), dim3(Q4_THREADS), 0, st, sys->dev, Ac, C, cs,
                          storage, idx, B, gb, step);
     else
       hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage,
@@ -1119,7 +1119,7 @@ struct LaunchChainPair {
     const int Bp = gbc.Bp;
     if (chain_tile(Bp) == Q4_TILE) {
       const int nct = Bp / Q4_TILE;
-      hipLaunchKernelGGL(k_chain_pair_q4<NJ>, dim3(2 * nct), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, Ac, cs,
+      hipLaunchKernelGGL(k_chain_pair_q4<NJ>, dim3(2 * nct), dim3(Q4_THREADS), 0, st, sys->dev, C, Tg, Ac, cs,
                          storage, idx_c, isw, idx_a, B, nct, gbc, gba, y, V, step);
     } else {
       const int nct = Bp / CACTO_TILE;
@@ -1256,7 +1256,7 @@ int launch_critic_chain(const cacto_sys* sys, const cacto_nets* nets, const cact
   float* Vb = V ? V : w.scal + w.Bp;
   float* Vtb = Vt ? Vt : w.scal + 2 * w.Bp;
   if (chain_tile(w.Bp) == Q4_TILE)
-    hipLaunchKernelGGL(k_critic_grad_q4, dim3(w.Bp / Q4_TILE), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, cs,
+    hipLaunchKernelGGL(k_critic_grad_q4, dim3(w.Bp / Q4_TILE), dim3(Q4_THREADS), 0, st, sys->dev, C, Tg, cs,
                        storage, idx, isw, B, w.crit, yb, Vb, Vtb, nets->step_d);
   else
     hipLaunchKernelGGL(k_critic_grad, dim3(w.Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, cs, storage, idx,

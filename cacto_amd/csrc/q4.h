@@ -69,18 +69,21 @@ __device__ __forceinline__ float q4_bias(const float* __restrict__ bias, int ot,
   return (bias && f < nout) ? bias[f] : 0.f;
 }
 
-// A whole layer's fragments for one wave, held in registers: NT out tiles (ot = wave + 4 t) x KT
+// A team is NW waves working on one pass (the q4 chains run 8 waves per workgroup, as one team of
+// 8 or two teams of 4 doing independent passes side by side); wi is the wave's index in its team.
+
+// A whole layer's fragments for one wave, held in registers: NT out tiles (ot = wi + NW t) x KT
 // k-tiles, plus the lane's bias. Loads are branch-free (clamped tile index; see mlp.h Frags).
-template <int KT, int NT>
+template <int KT, int NT, int NW = CACTO_NWAVES>
 struct Q4Frags {
   float4 a[NT][KT];
   float b[NT];
   template <bool BIAS>
   __device__ __forceinline__ void load(const float4* __restrict__ A, const float* __restrict__ bias, int OT, int nout,
-                                       int wave, int lane) {
+                                       int wi, int lane) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int ot = min(wave + CACTO_NWAVES * t, OT - 1);
+      const int ot = min(wi + NW * t, OT - 1);
 #pragma unroll
       for (int k = 0; k < KT; ++k) a[t][k] = A[((size_t)ot * KT + k) * 64 + lane];
       const int f = 16 * ot + (lane & 15);
@@ -91,7 +94,7 @@ struct Q4Frags {
   // every tile's MFMAs, then the reductions, then the epilogues epi(ot, value) (value + bias
   // with BIAS): the epilogue VALU work overlaps the matrix core's tail
   template <bool BIAS, typename Epi>
-  __device__ __forceinline__ void run(const float* X, int OT, int wave, int lane, Epi&& epi) const {
+  __device__ __forceinline__ void run(const float* X, int OT, int wi, int lane, Epi&& epi) const {
     float x[KT];
 #pragma unroll
     for (int k = 0; k < KT; ++k) x[k] = X[64 * k + lane];
@@ -99,7 +102,7 @@ struct Q4Frags {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
-      if (wave + CACTO_NWAVES * t < OT) {
+      if (wi + NW * t < OT) {
 #pragma unroll
         for (int k = 0; k < KT; ++k) q4_ktile(x[k], a[t][k], c0, c1, c2, c3);
       }
@@ -107,7 +110,7 @@ struct Q4Frags {
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int ot = wave + CACTO_NWAVES * t;
+      const int ot = wi + NW * t;
       if (ot < OT) {
         const float v = q4_reduce(acc[t]);
         epi(ot, BIAS ? fadd(v, b[t]) : v);
@@ -117,82 +120,88 @@ struct Q4Frags {
 };
 
 // A single-out-tile layer (OT == 1: the critic's output, the actor's action layer, the critic's
-// input gradient): wave w takes k-tiles w, w + 4, ...; the four waves' partials are summed through
-// LDS `red` (4 x 64 floats) in wave order by wave 0, which runs the epilogue. Contains
-// __syncthreads(): all threads must call run().
-template <int NK>
+// input gradient): wave wi takes k-tiles wi, wi + NW, ...; the team's partials are summed through
+// LDS `red` (NW x 64 floats, the team's own) in wave order by the team's wave 0, which runs the
+// epilogue. Contains __syncthreads(): every thread of the workgroup must call run() (two teams
+// running a split layer at the same time share the barrier).
+template <int NK, int NW = CACTO_NWAVES>
 struct Q4Split {
   float4 a[NK];
   float b;
   template <bool BIAS>
   __device__ __forceinline__ void load(const float4* __restrict__ A, int KT, const float* __restrict__ bias, int nout,
-                                       int wave, int lane) {
+                                       int wi, int lane) {
 #pragma unroll
-    for (int i = 0; i < NK; ++i) a[i] = A[min(wave + CACTO_NWAVES * i, KT - 1) * 64 + lane];
+    for (int i = 0; i < NK; ++i) a[i] = A[min(wi + NW * i, KT - 1) * 64 + lane];
     const int f = lane & 15;
     b = BIAS ? bias[min(f, nout - 1)] : 0.f;
     if (f >= nout) b = 0.f;
   }
   template <bool BIAS, typename Epi>
-  __device__ __forceinline__ void run(int KT, const float* X, float* red, int wave, int lane, Epi&& epi) const {
+  __device__ __forceinline__ void run(int KT, const float* X, float* red, int wi, int lane, Epi&& epi) const {
     floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
-      const int kt = wave + CACTO_NWAVES * i;
+      const int kt = wi + NW * i;
       if (kt < KT) q4_ktile(X[64 * kt + lane], a[i], c0, c1, c2, c3);
     }
-    red[wave * 64 + lane] = q4_reduce((c0 + c1) + (c2 + c3));
+    red[wi * 64 + lane] = q4_reduce((c0 + c1) + (c2 + c3));
     __syncthreads();
-    if (wave == 0) {
+    if (wi == 0) {
       float s = red[lane];
 #pragma unroll
-      for (int w = 1; w < CACTO_NWAVES; ++w) s += red[w * 64 + lane];
+      for (int w = 1; w < NW; ++w) s += red[w * 64 + lane];
       epi(0, BIAS ? fadd(s, b) : s);
     }
   }
 };
 
-// A layer streamed from L2 tile by tile (the actor's 256-wide layers: 64 VGPRs of fragments per
-// tile): the next tile's fragments are in flight while the current tile's MFMAs run. The KT
-// activation operands are read from LDS once for all tiles. F0 (optional) = the first tile's
-// fragments, issued a phase early by the caller.
-template <int KT, bool BIAS, typename Epi>
-__device__ __forceinline__ void q4_layer_t(const float4* __restrict__ A, int OT, const float* X, int wave, int lane,
-                                           Epi&& epi, const float* __restrict__ bias, int nout,
-                                           const FragTile<KT>* F0 = nullptr) {
-  int ot = wave;
-  if (ot >= OT) return;
-  float4 a[KT];
-  if (F0) {
+// The actor's 256-wide layers (OT = 16: out tiles wi + NW t) with a wave's tiles taken in pairs:
+// both tiles' KT fragment blocks are issued together (branch-free), so a wave waits for one memory
+// latency per pair instead of one per tile (the weights come from the memory-side cache after every
+// Adam step; a one-tile-ahead prefetch still pays that latency per tile). The first pair is issued
+// by the caller a phase early (P0); with 8 waves it is the wave's only pair.
+template <int KT, int NW = CACTO_NWAVES>
+struct Q4Pair {
+  static constexpr int NP = 16 / (2 * NW);  // pairs per wave
+  float4 a[2][KT];
+  __device__ __forceinline__ void load(const float4* __restrict__ A, int p, int wi, int lane) {
 #pragma unroll
-    for (int k = 0; k < KT; ++k) a[k] = F0->a[k];
-  } else {
+    for (int u = 0; u < 2; ++u) {
+      const int ot = wi + NW * (2 * p + u);
 #pragma unroll
-    for (int k = 0; k < KT; ++k) a[k] = A[((size_t)ot * KT + k) * 64 + lane];
+      for (int k = 0; k < KT; ++k) a[u][k] = A[((size_t)ot * KT + k) * 64 + lane];
+    }
   }
-  float bv = BIAS ? q4_bias(bias, ot, lane, nout) : 0.f;
+};
+
+template <int KT, bool BIAS, int NW, typename Epi>
+__device__ __forceinline__ void q4_layer_pairs(const float4* __restrict__ A, const float* X, int wi, int lane,
+                                               Epi&& epi, const float* __restrict__ bias, const Q4Pair<KT, NW>& P0) {
+  constexpr int NP = Q4Pair<KT, NW>::NP;
   float x[KT];
 #pragma unroll
   for (int k = 0; k < KT; ++k) x[k] = X[64 * k + lane];
-  while (true) {
-    const int nxt = ot + CACTO_NWAVES;
-    float4 an[KT];
-    float bn = bv;
-    if (nxt < OT) {
+  float bv[2 * NP];
 #pragma unroll
-      for (int k = 0; k < KT; ++k) an[k] = A[((size_t)nxt * KT + k) * 64 + lane];
-      if (BIAS) bn = q4_bias(bias, nxt, lane, nout);
+  for (int t = 0; t < 2 * NP; ++t) bv[t] = BIAS ? bias[16 * (wi + NW * t) + (lane & 15)] : 0.f;
+  Q4Pair<KT, NW> P = P0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    floatx4 acc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+#pragma unroll
+      for (int k = 0; k < KT; ++k) q4_ktile(x[k], P.a[u][k], c0, c1, c2, c3);
+      acc[u] = (c0 + c1) + (c2 + c3);
     }
-    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+    if (p + 1 < NP) P.load(A, p + 1, wi, lane);  // the next pair, in flight during this pair's epilogue
 #pragma unroll
-    for (int k = 0; k < KT; ++k) q4_ktile(x[k], a[k], c0, c1, c2, c3);
-    const float v = q4_reduce((c0 + c1) + (c2 + c3));
-    epi(ot, BIAS ? fadd(v, bv) : v);
-    if (nxt >= OT) break;
-    ot = nxt;
-    bv = bn;
-#pragma unroll
-    for (int k = 0; k < KT; ++k) a[k] = an[k];
+    for (int u = 0; u < 2; ++u) {
+      const float v = q4_reduce(acc[u]);
+      epi(wi + NW * (2 * p + u), BIAS ? fadd(v, bv[2 * p + u]) : v);
+    }
   }
 }
 

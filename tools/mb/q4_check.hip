@@ -65,14 +65,25 @@ __global__ void __launch_bounds__(256) k_split(const float4* pk, const float* bi
   F.template run<true>(KT, Xs, red, wave, lane, [&](int, float v) { out[q4e(0, lane)] = v; });
 }
 
-template <int KT>
-__global__ void __launch_bounds__(256) k_stream(const float4* pk, const float* bias, int OT, int nout, const float* X,
-                                                float* out) {
-  __shared__ float Xs[KT * 64];
-  for (int k = threadIdx.x; k < KT * 64; k += 256) Xs[k] = X[k];
+// the 8-wave pair layout (one pair of out tiles per wave), as the q4 chains run it
+__global__ void __launch_bounds__(512) k_pairs8(const float4* pk, const float* bias, const float* X, float* out) {
+  __shared__ float Xs[16 * 64];
+  for (int k = threadIdx.x; k < 16 * 64; k += 512) Xs[k] = X[k];
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  q4_layer_t<KT, true>(pk, OT, Xs, wave, lane, [&](int ot, float v) { out[q4e(ot, lane)] = v; }, bias, nout);
+  Q4Pair<16, 8> P0;
+  P0.load(pk, 0, wave, lane);
+  q4_layer_pairs<16, true, 8>(pk, Xs, wave, lane, [&](int ot, float v) { out[q4e(ot, lane)] = v; }, bias, P0);
+}
+
+__global__ void __launch_bounds__(256) k_pairs(const float4* pk, const float* bias, const float* X, float* out) {
+  __shared__ float Xs[16 * 64];
+  for (int k = threadIdx.x; k < 16 * 64; k += 256) Xs[k] = X[k];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  Q4Pair<16, 4> P0;
+  P0.load(pk, 0, wave, lane);
+  q4_layer_pairs<16, true, 4>(pk, Xs, wave, lane, [&](int ot, float v) { out[q4e(ot, lane)] = v; }, bias, P0);
 }
 
 // mlp.h images of W [in][out]
@@ -197,7 +208,8 @@ int main() {
     else if (kind == 0 && KT == 1 && OT == 4) k_layer<1, 1, true><<<1, 256>>>(D.pk, bp, OT, O, D.X, D.out);
     else if (kind == 1 && KT == 8) k_split<2><<<1, 256>>>(D.pk, D.bias, KT, O, D.X, D.out);
     else if (kind == 1 && KT == 16) k_split<4><<<1, 256>>>(D.pk, D.bias, KT, O, D.X, D.out);
-    else if (kind == 2 && KT == 16) k_stream<16><<<1, 256>>>(D.pk, bp, OT, O, D.X, D.out);
+    else if (kind == 2 && KT == 16 && OT == 16 && bias) k_pairs8<<<1, 512>>>(D.pk, D.bias, D.X, D.out);
+    else if (kind == 3 && KT == 16 && OT == 16 && bias) k_pairs<<<1, 256>>>(D.pk, D.bias, D.X, D.out);
     else {
       printf("no kernel for %s\n", name);
       ++fails;
@@ -214,8 +226,8 @@ int main() {
   run_case("layer 5->64 fwd, bias (Q4Frags<1,1>)", 5, 64, false, 0);
   run_case("split 128->1, bias (Q4Split<2>)", 128, 1, false, 1);
   run_case("split 256->6, bias (Q4Split<4>)", 256, 6, false, 1);
-  run_case("streamed 256->256, bias (q4_layer_t<16>)", 256, 256, false, 2);
-  run_case("streamed 256x256 transposed (q4_layer_t<16>)", 256, 256, true, 2);
+  run_case("paired 256->256, bias, 8 waves (q4_layer_pairs<16, 8>)", 256, 256, false, 2);
+  run_case("paired 256->256, bias (q4_layer_pairs<16>)", 256, 256, false, 3);
   printf(fails ? "q4_check: %d FAILED\n" : "q4_check: all passed\n", fails);
   return fails ? 1 : 0;
 }
