@@ -80,10 +80,12 @@ struct Q4CriticBwd {
 
 // Critic forward over the F4 input tile X0 for a team (net_common.h critic_forward_tile_f): with Hs
 // every h_l = sin z_l is kept (24 tiles at ZOFF), else h alternates in H (2 x 8 tiles); with Cs
-// cos z_l is kept. hook(l, ot, h) per hidden element, mid(l) after layer l's epilogues (the caller
-// issues the next pass's fragment loads there); V[i] (LDS) receives sample i's value when WANT_V.
+// cos z_l is kept. hook(l, ot, h, c) per hidden element (h = sin z, c = cos z), mid(l) after layer
+// l's epilogues (the caller issues the next pass's fragment loads there); V[i] (LDS) receives sample
+// i's value when WANT_V — written by the team's wave 0 after the split's barrier; SYNC_V = false
+// leaves out the barrier that would publish it (a caller that reads V only after later barriers).
 // `red`: the team's NW x 64 floats.
-template <bool WANT_V, int NW, typename Hook, typename Mid>
+template <bool WANT_V, int NW, bool SYNC_V = true, typename Hook, typename Mid>
 __device__ void q4_critic_forward_f(const Q4CriticFwd<NW>& F, const float* X0, float* Cs, float* Hs, float* H,
                                     float* red, float* V, int wi, int lane, Hook&& hook, Mid&& mid) {
   auto epi = [&](int l, float* out) {
@@ -93,7 +95,7 @@ __device__ void q4_critic_forward_f(const Q4CriticFwd<NW>& F, const float* X0, f
       const int e = q4e(ot, lane);
       if (Cs) Cs[ZOFF[l] * 64 + e] = c;
       out[e] = h;
-      hook(l, ot, h);
+      hook(l, ot, h, c);
     };
   };
   const float* in = X0;
@@ -120,26 +122,28 @@ __device__ void q4_critic_forward_f(const Q4CriticFwd<NW>& F, const float* X0, f
     F.f4.template run<true>(8, out, red, wi, lane, [&](int, float v) {
       if ((lane & 15) == 0) V[lane >> 4] = v;
     });
-    __syncthreads();
+    if (SYNC_V) __syncthreads();
   }
 }
 
 // Critic input gradient from the cos tiles Cs (net_common.h critic_first_backward), 8 waves:
 // G4 = W5, D_l = G_{l+1} cos z_l, G_l = D_l W_l^T. G tiles (G1 at 0, G2 at 4, G3 at 8) when Gs,
-// D via hookD(l, ot, d), dV/dx0 in G0 (F4, one tile); mid() after the first transposed layer.
-template <typename HookD, typename Mid>
+// D via hookD(l, ot, d), dV/dx0 = G_0 through g0epi(lane, g) (wave 0; lane's element is feature
+// lane & 15 of sample lane >> 4); mid() after the first transposed layer. d3_done: the caller's
+// forward already wrote D_3 = W5 cos z3 into P (and its panel), so that step and its barrier go.
+template <typename HookD, typename Mid, typename G0Epi>
 __device__ void q4_critic_first_backward(const Q4CriticBwd& F, const float* Cs, float* P /* 2 x 8 tiles */,
-                                         float* Gs, float* G0, float* red, int wave, int lane, HookD&& hookD,
-                                         Mid&& mid) {
+                                         float* Gs, float* red, int wave, int lane, HookD&& hookD, Mid&& mid,
+                                         G0Epi&& g0epi, bool d3_done = false) {
   const int goff[4] = {0, 0, 4, 8};
   float* D = P;
-  {
+  if (!d3_done) {
     const int e = q4e(wave, lane);
     const float d = fmul(F.w5, Cs[ZOFF[3] * 64 + e]);
     D[e] = d;
     hookD(3, wave, d);
+    __syncthreads();
   }
-  __syncthreads();
   auto epi = [&](int l, float* Dn) {
     return [&, l, Dn](int it, float g) {
       const int e = q4e(it, lane);
@@ -162,7 +166,7 @@ __device__ void q4_critic_first_backward(const Q4CriticBwd& F, const float* Cs, 
   F.g1.run<false>(D, 4, wave, lane, epi(1, Dn));
   __syncthreads();
   D = Dn;
-  F.g0.run<false>(4, D, red, wave, lane, [&](int, float g) { G0[q4e(0, lane)] = g; });
+  F.g0.run<false>(4, D, red, wave, lane, [&](int, float g) { g0epi(lane, g); });
   __syncthreads();
 }
 
@@ -223,25 +227,24 @@ __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, 
   const NetView& FN = team ? Tg : C;
   const float w5 = C.flat[C.t.woff[4] + 16 * wave + (lane & 15)];
   const Q4Norm nrm(p, lane);
-  if (wave < 4) {
-    // one (sample c, column) per lane, wave w gathers array w: s, s_next, dV/dx, then (R, d, w);
-    // branch-free inside (clamped indices, zeroed after), so no load sits under a lane branch
-    const int c = lane >> 4, f = lane & 15;
+  {
+    // one (sample c, column) per lane, wave w gathers array w & 3: s, s_next, dV/dx, then (R, d, w)
+    // (waves 4-7 repeat the loads of waves 0-3, so every wave runs the same branch-free load
+    // sequence: index, row, then the fragments — a load under a wave branch would make the wait
+    // for the rows include the fragments)
+    const int c = lane >> 4, f = lane & 15, a = wave & 3;
     const bool valid = s0 + c < B;
     const int sc = min(s0 + c, B - 1), fc = min(f, ns - 1);
     const int32_t row = idx[sc];
-    F.load<true>(FN, wi4, lane);
-    F.load_last(FN, wi4, lane);
-    const int col = wave == 0 ? fc : wave < 3 ? wave * ns + 1 + fc : (f == 0 ? ns : 3 * ns + 1);
+    const int col = a == 0 ? fc : a < 3 ? a * ns + 1 + fc : (f == 0 ? ns : 3 * ns + 1);
     const double x = storage[(size_t)row * cols + col];
     const float wv = isw ? isw[sc] : 1.f;
-    const bool keep = valid && (wave < 3 ? f < ns : f < 2);
-    float v = keep ? (float)x : 0.f;
-    if (wave == 3 && f == 2) v = valid ? wv : 0.f;
-    S.stage[wave * 64 + c * 16 + f] = v;
-  } else {
     F.load<true>(FN, wi4, lane);
     F.load_last(FN, wi4, lane);
+    const bool keep = valid && (a < 3 ? f < ns : f < 2);
+    float v = keep ? (float)x : 0.f;
+    if (a == 3 && f == 2) v = valid ? wv : 0.f;
+    if (wave < 4) S.stage[wave * 64 + c * 16 + f] = v;
   }
   __syncthreads();
   if (wave < 2) {  // wave 0: X0, wave 1: XT (element lane = 4 f + i)
@@ -255,65 +258,98 @@ __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, 
   const float* Rs = S.stage + 3 * 64;  // Rs[16 c] = R, [16 c + 1] = d, [16 c + 2] = w
 
   // forward at s (waves 0-3: sin z, cos z kept, h_l -> LT_l second half) beside the target
-  // forward at s' (waves 4-7: y = R + (1 - d) * V_tgt(s_next), NeuralNetwork.py:153-158; run even
-  // for MC, whose y ignores it). The transposed fragments of the backward passes are issued after
-  // layer 2.
+  // forward at s' (waves 4-7: V_tgt(s_next) for y = R + (1 - d) * V_tgt(s_next),
+  // NeuralNetwork.py:153-158; run even for MC, whose y ignores it). The transposed fragments of the
+  // backward passes are issued after layers 2 and 3. With the Sobolev term, D_3 = W5 cos z3 (the
+  // first backward's input) is formed in the forward's last epilogue. V and V_tgt are read only
+  // after the first backward's barriers, so the pass ends without the barrier that publishes them.
+  const bool fuse_d3 = sob && !cs.want_vt;  // want_vt's extra pass reuses GB as scratch
+  float w5t[2];                             // W5 at the lane's features of team 0's layer-3 tiles
+#pragma unroll
+  for (int t = 0; t < 2; ++t) w5t[t] = C.flat[C.t.woff[4] + 16 * (wi4 + 4 * t) + (lane & 15)];
   Q4CriticBwd HB;
-  q4_critic_forward_f<true, 4>(
+  q4_critic_forward_f<true, 4, false>(
       F, team ? XT : X0, team ? nullptr : Cs, team ? nullptr : Hs, team ? S.HT : Hs, red + team * 4 * 64,
       team ? S.Vn : S.V, wi4, lane,
-      [&](int l, int ot, float h) {
-        if (team == 0) q4_store_panel(gb.LT[l + 1], ld, Bp + s0, ot, lane, h);
+      [&](int l, int ot, float h, float c) {
+        if (team == 0) {
+          q4_store_panel(gb.LT[l + 1], ld, Bp + s0, ot, lane, h);
+          if (l == 3 && fuse_d3) {
+            const float d = fmul(w5t[ot >> 2], c);
+            GB[q4e(ot, lane)] = d;
+            q4_store_panel(gb.RT[3], ld, s0, ot, lane, d);
+          }
+        }
       },
       [&](int l) {
         if (l == 2) HB.load_g3(C, wave, lane);
         if (l == 3) HB.load_rest(C, wave, lane);
       });
-  if (tid < 4) {
-    const int c = tid;
-    S.y[c] = cs.MC ? Rs[16 * c] : fadd(Rs[16 * c], fmul(fsub(1.f, Rs[16 * c + 1]), S.Vn[c]));
-  }
   CSTAMP(2);
   if (cs.want_vt) {  // the extra V_tgt(s) of NeuralNetwork.py:178 (waves 4-7; waves 0-3 repeat into scratch)
+    __syncthreads();  // the first pass's split finishers are done with `red`
     q4_critic_forward_f<true, 4>(F, X0, nullptr, nullptr, team ? S.HT : GB, red + team * 4 * 64,
-                                 team ? S.Vt2 : S.Vx, wi4, lane, [](int, int, float) {}, [](int) {});
+                                 team ? S.Vt2 : S.Vx, wi4, lane, [](int, int, float, float) {}, [](int) {});
   }
   CSTAMP(3);
+  // Vbar = (2 * ((wS/B) * w)) * (V - y) of the lane's sample (Keras MSE, SUM_OVER_BATCH_SIZE), every
+  // lane for itself: it enters zbar_3 in the layer-3 epilogue below
+  auto vbar = [&](int c) {
+    const float y = cs.MC ? Rs[16 * c] : fadd(Rs[16 * c], fmul(fsub(1.f, Rs[16 * c + 1]), S.Vn[c]));
+    const float wv = sob ? cs.w_S : 1.f;
+    const float gl = fmul(fdiv(wv, (float)cs.B_global), Rs[16 * c + 2]);
+    return fmul(fmul(2.f, gl), fsub(S.V[c], y));
+  };
+  auto outputs = [&]() {  // tid < 4: the value loss row of the output layer's panel, y / V / V_tgt outputs
+    const int c = tid;
+    const float y = cs.MC ? Rs[16 * c] : fadd(Rs[16 * c], fmul(fsub(1.f, Rs[16 * c + 1]), S.Vn[c]));
+    gb.RT[4][Bp + s0 + c] = vbar(c);
+    if (sob) gb.RT[4][s0 + c] = 1.f;  // dW5 += Gbar_4 (G_4 = W5[:, 0])
+    if (s0 + c < B) {
+      if (y_out) y_out[s0 + c] = y;
+      if (V_out) V_out[s0 + c] = S.V[c];
+      if (Vt_out && cs.want_vt) Vt_out[s0 + c] = S.Vt2[c];
+    }
+  };
 
   Q4CriticFwd<Q4_NW> SF;  // the forward fragments of the Sobolev passes (8-wave layout, no bias)
   if (sob) {
-    // first backward: D_l -> RT_l first half; G_l kept; G_0 = dV/dx0
+    // first backward: D_l -> RT_l first half; G_l kept; G_0 = dV/dx0 goes straight into the Sobolev
+    // loss gradient w.r.t. dV/ds and then G_0 (NeuralNetwork.py:167-170), in the finisher of its
+    // split layer (wave 0, lane = feature f of sample i)
     q4_critic_first_backward(
-        HB, Cs, GB, G, G0, red, wave, lane, [&](int l, int ot, float d) { q4_store_panel(gb.RT[l], ld, s0, ot, lane, d); },
-        [&]() { SF.load<false>(C, wave, lane); });
+        HB, Cs, GB, G, red, wave, lane, [&](int l, int ot, float d) { q4_store_panel(gb.RT[l], ld, s0, ot, lane, d); },
+        [&]() { SF.load<false>(C, wave, lane); },
+        [&](int ln, float g) {
+          const int f = ln & 15, i = ln >> 4;
+          float gb0 = 0.f;
+          if (f < ns - 1) {
+            const float nf = (float)p.state_norm[f];
+            auto nback = [&](float v) { return !p.normalize ? v : fdiv(v, nf); };  // not the time column
+            const float gsq = fdiv(fmul(fdiv(1.f, (float)cs.B_global), Rs[16 * i + 2]), (float)(ns - 1));
+            const float dvds = nback(g);
+            const float yp = clog(dvds), yt = clog(S.stage[2 * 64 + i * 16 + f]);
+            const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
+            gb0 = nback(clog_backward(dvds, gyp));
+          }
+          GB[q4e(0, ln)] = gb0;
+          gb.LT[0][(size_t)f * ld + s0 + i] = gb0;
+        },
+        fuse_d3);
     CSTAMP(4);
-    // Sobolev loss gradient w.r.t. dV/ds, then w.r.t. G_0 (NeuralNetwork.py:167-170): element
-    // (feature f, sample i) = lane 4 f + i of wave 0
-    if (wave == 0) {
-      const int f = lane >> 2, i = lane & 3;
-      float gb0 = 0.f;
-      if (f < ns - 1) {
-        const float nf = (float)p.state_norm[f];
-        auto nback = [&](float g) { return !p.normalize ? g : fdiv(g, nf); };  // not the time column
-        const float gsq = fdiv(fmul(fdiv(1.f, (float)cs.B_global), Rs[16 * i + 2]), (float)(ns - 1));
-        const float dvds = nback(G0[lane]);
-        const float yp = clog(dvds), yt = clog(S.stage[2 * 64 + i * 16 + f]);
-        const float gyp = fmul(fmul(2.f, gsq), fsub(yp, yt));
-        gb0 = nback(clog_backward(dvds, gyp));
-      }
-      GB[lane] = gb0;
-      gb.LT[0][(size_t)f * ld + s0 + i] = gb0;
-    }
-    __syncthreads();
     CSTAMP(5);
-    // backward of the first backward, l = 0..3, on the forward fragments (no bias)
+    const float vb = vbar(lane >> 4);
+    // backward of the first backward, l = 0..3, on the forward fragments (no bias); the layer-3
+    // epilogue also adds the value loss's zbar_3 += (Vbar * W5) * cos(z3)
     auto sp_epi = [&](int l, float* nxt) {
       return [&, l, nxt](int ot, float acc) {
         const int e = q4e(ot, lane);
         const float sz = Hs[ZOFF[l] * 64 + e], cz = Cs[ZOFF[l] * 64 + e];
         const float gu = l < 3 ? G[goff[l + 1] * 64 + e] : w5;  // layer 3: out tile `wave`
-        ZB[ZOFF[l] * 64 + e] = fmul(-fmul(acc, gu), sz);       // CosGrad: -grad * sin(x)
-        const float gn = fmul(acc, cz);                         // MulGrad into the upstream grad
+        float zb = fmul(-fmul(acc, gu), sz);                     // CosGrad: -grad * sin(x)
+        if (l == 3) zb = fadd(zb, fmul(fmul(vb, w5), cz));
+        ZB[ZOFF[l] * 64 + e] = zb;
+        const float gn = fmul(acc, cz);  // MulGrad into the upstream grad
         nxt[e] = gn;
         q4_store_panel(gb.LT[l + 1], ld, s0, ot, lane, gn);
       };
@@ -329,33 +365,20 @@ __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, 
     __syncthreads();
     CSTAMP(8);
     SF.f3.run<false>(nA, 8, wave, lane, sp_epi(3, GB));
+    if (tid < 4) outputs();
     __syncthreads();
     CSTAMP(9);
-    if (tid < 4) gb.RT[4][s0 + tid] = 1.f;  // dW5 += Gbar_4 (G_4 = W5[:, 0])
   } else {
-    for (int k = tid; k < 24 * 64; k += Q4_THREADS) ZB[k] = 0.f;
+    __syncthreads();  // V, V_tgt published
+    for (int k = tid; k < ZOFF[3] * 64; k += Q4_THREADS) ZB[k] = 0.f;
+    {  // zbar_3 = (Vbar * W5) * cos(z3): out tile `wave`
+      const int e = ZOFF[3] * 64 + q4e(wave, lane);
+      ZB[e] = fadd(0.f, fmul(fmul(vbar(lane >> 4), w5), Cs[e]));
+    }
+    if (tid < 4) outputs();
+    __syncthreads();
   }
   CSTAMP(10);
-
-  // value loss: Vbar = (2 * ((wS/B) * w)) * (V - y)   (Keras MSE, SUM_OVER_BATCH_SIZE)
-  if (tid < 4) {
-    const int c = tid;
-    const float wv = sob ? cs.w_S : 1.f;
-    const float gl = fmul(fdiv(wv, (float)cs.B_global), Rs[16 * c + 2]);
-    S.Vb[c] = fmul(fmul(2.f, gl), fsub(S.V[c], S.y[c]));
-    gb.RT[4][Bp + s0 + c] = S.Vb[c];
-    if (s0 + c < B) {
-      if (y_out) y_out[s0 + c] = S.y[c];
-      if (V_out) V_out[s0 + c] = S.V[c];
-      if (Vt_out && cs.want_vt) Vt_out[s0 + c] = S.Vt2[c];
-    }
-  }
-  __syncthreads();
-  {  // zbar_3 += (Vbar * W5) * cos(z3): out tile `wave`
-    const int e = ZOFF[3] * 64 + q4e(wave, lane);
-    ZB[e] = fadd(ZB[e], fmul(fmul(S.Vb[lane >> 4], w5), Cs[e]));
-  }
-  __syncthreads();
   CSTAMP(11);
   // backward through the forward graph: zbar_{l-1} += (zbar_l W_l^T) * cos(z_{l-1})
   auto hb_epi = [&](int l) {
@@ -407,7 +430,86 @@ struct Q4ActorLds {
   float Fu[Q4_TILE * CACTO_MAX_STATE * CACTO_MAX_ACTION];
   float dra[Q4_TILE * CACTO_MAX_ACTION];
   double term_s[Q4_TILE];
+  double dM[Q4_TILE * CACTO_MAX_JOINTS * CACTO_MAX_JOINTS];  // revolute chains: M(q) and h(q, v) per sample
+  double dh[Q4_TILE * CACTO_MAX_JOINTS];
+  // the system (joint table, tabled constant dynamics) copied at kernel entry: the float64
+  // recursions read a joint's parameters in long dependent sequences, one global load latency each
+  SysDevice sys;
 };
+
+// env_simulate_derivative (env.h) of a revolute chain for the tile's 4 samples, spread over threads
+// (the 4-sample tile leaves most of the workgroup idle during the float64 dynamics): M(q) by CRBA
+// (wave 1) beside h(q, v) by RNEA (wave 0) — chain_mass / chain_nle, the two halves of chain_terms
+// in its operation order — then per sample NJ + 1 threads each factor M and solve one right-hand
+// side: a - h (the step) or e_j (column j of M^-1, a column of Fu). The same operations on the same
+// values as the one-thread path, so s' and Fu are bit-identical to it. Contains two barriers.
+template <int NJ>
+__device__ __forceinline__ void q4_chain_dynamics(Q4ActorLds& S, const SysDevice& sd, int wave, int lane) {
+  constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
+  const cacto_sys_params& p = sd.p;
+  if (wave < 2 && lane < Q4_TILE) {
+    const int c = lane;
+    double q[NJ], v[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      q[i] = (double)S.st[c * 16 + i];
+      v[i] = (double)S.st[c * 16 + NJ + i];
+    }
+    if (wave == 0) {
+      double h[NJ];
+      chain_nle<NJ>(sd, q, v, h);
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) S.dh[c * NJ + i] = h[i];
+    } else {
+      double M[NJ * NJ];
+      chain_mass<NJ>(sd, q, M);
+#pragma unroll
+      for (int k = 0; k < NJ * NJ; ++k) S.dM[c * NJ * NJ + k] = M[k];
+    }
+  }
+  __syncthreads();
+  CSTAMP(12);
+  if (wave == 0 && lane < Q4_TILE * (NJ + 1)) {
+    const int c = lane / (NJ + 1), j = lane - c * (NJ + 1);
+    const double dt = p.dt;
+    double L[NJ * NJ], x[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) L[k] = S.dM[c * NJ * NJ + k];
+    (void)cholesky<NJ>(L);
+    if (j == 0) {
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) x[i] = (double)S.A[c * NA + i] - S.dh[c * NJ + i];
+      chol_solve<NJ>(L, x);
+      float* sn = S.stn + c * 16;
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {  // env_simulate_derivative's f32in update
+        const double s = (double)S.st[c * 16 + i], vv = (double)S.st[c * 16 + NJ + i];
+        const float vdt = __fmul_rn((float)vv, (float)dt);
+        sn[i] = (float)(s + (double)vdt);
+        sn[NJ + i] = (float)(double)(float)(vv + x[i] * dt);
+      }
+      sn[2 * NJ] = (float)((double)S.st[c * 16 + 2 * NJ] + dt);
+#pragma unroll
+      for (int f = NS; f < 16; ++f) sn[f] = 0.f;
+    } else {
+      const int col = j - 1;
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) x[i] = (i == col) ? 1.0 : 0.0;
+      chol_solve<NJ>(L, x);
+      float* F = S.Fu + c * CACTO_MAX_STATE * CACTO_MAX_ACTION;
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        double v = 0.0;
+        if (r >= NJ && r < 2 * NJ) {
+          v = x[r - NJ] * dt;
+          if (p.normalize) v *= sd.inv_norm[r];
+        }
+        F[r * NA + col] = (float)v;
+      }
+    }
+  }
+  __syncthreads();
+}
 
 // one 4-sample tile of the actor chain (actor_chain's operations, F4 layout, 8 waves). The actor's
 // shape is fixed (ns -> 256 -> 256 -> na, ns, na <= 16: KT = 1 / 16 / 16, OT = 16 / 16 / 1).
@@ -425,16 +527,28 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   CSTAMP(0);
   if (tile == 0 && tid == 0 && step) step[1] += 1;  // Keras actor optimizer iterations
   // layer 1 (ns -> 256) and the wave's pair of layer-2 out tiles, in flight during the row gathers
+  // (every wave loads the rows — waves 1-7 the same as wave 0 — so every wave runs one branch-free
+  // load sequence: index, row, then the fragments; wave 0's wait for the rows excludes them)
   Q4Frags<1, 2, Q4_NW> F1;
-  F1.load<true>(Ac.fwd(0), Ac.biasp(0), 16, 256, wave, lane);
   Q4Pair<16, Q4_NW> W2;
-  W2.load(Ac.fwd(1), 0, wave, lane);
-  if (wave == 0) {
+  {
     const int c = lane >> 4, f = lane & 15;
     const bool valid = s0 + c < B;
-    const double* rp = storage + (size_t)(valid ? idx[s0 + c] : 0) * cols;
-    S.st[c * 16 + f] = (valid && f < ns) ? (float)rp[f] : 0.f;
-    if (f == 0) S.term_s[c] = valid ? rp[3 * ns + 2] : 0.0;
+    const int sc = min(s0 + c, B - 1), fc = min(f, ns - 1);
+    const double* rp = storage + (size_t)idx[sc] * cols;
+    const double x = rp[fc], term = rp[3 * ns + 2];
+    // the system copy (branch-free: clamped index, duplicates write the same value), issued right
+    // after the rows so the first barrier's wait covers it and not the fragments
+    constexpr int SDW = sizeof(SysDevice) / sizeof(double);
+    const int k = min(tid, SDW - 1);
+    const double sv = reinterpret_cast<const double*>(sdp)[k];
+    F1.load<true>(Ac.fwd(0), Ac.biasp(0), 16, 256, wave, lane);
+    W2.load(Ac.fwd(1), 0, wave, lane);
+    reinterpret_cast<double*>(&S.sys)[k] = sv;
+    if (wave == 0) {
+      S.st[c * 16 + f] = (valid && f < ns) ? (float)x : 0.f;
+      if (f == 0) S.term_s[c] = valid ? term : 0.0;
+    }
   }
   __syncthreads();
   if (wave == 0) {  // input of layer 0 (normalised) -> LT_0
@@ -459,6 +573,7 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   Q4Split<2, Q4_NW> F3;  // the action layer (256 -> na)
   F3.load<true>(Ac.fwd(2), 16, Ac.biasp(2), na, wave, lane);
   __syncthreads();
+  CSTAMP(10);
   q4_layer_pairs<16, true, Q4_NW>(Ac.fwd(1), H, wave, lane, lepi(1), Ac.biasp(1), W2);
   // the critic's forward fragments at s', in flight during the action layer and the dynamics (for
   // the revolute chains after the dynamics: their float64 recursions need the registers)
@@ -466,6 +581,7 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   Q4CriticFwd<Q4_NW> CF;
   if (early_cf) CF.load<true>(C, wave, lane);
   __syncthreads();
+  CSTAMP(11);
   F3.run<true>(16, H + 16 * 64, red, wave, lane, [&](int, float v) {
     const int f = lane & 15;
     if (f < na) S.A[(lane >> 4) * na + f] = v;
@@ -473,7 +589,24 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   __syncthreads();
   CSTAMP(2);
   // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
-  if (tid < Q4_TILE) {
+  if constexpr (NJ >= 3) {
+    // revolute chains: spread over the workgroup; d reward / d a on wave 2 alongside
+    if (wave == 2 && lane < Q4_TILE) {
+      constexpr int NA = Dims<NJ>::NA;
+      const int c = lane;
+      float af[NA], g[NA];
+#pragma unroll
+      for (int i = 0; i < NA; ++i) af[i] = S.A[c * na + i];
+      const double tc = S.term_s[c];
+      const double w6 = 6 >= p.n_weights ? 0.0 : tc * p.w_terminal[6] + (1.0 - tc) * p.w_running[6];
+      (void)reward_batch_f32<NA>(p, w6, af, 0.0, g);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) S.dra[c * na + i] = g[i];
+    }
+    // (the 6-joint chain keeps its parameter reads on the scalar path: from LDS the compiler hoists
+    // them all and spills)
+    q4_chain_dynamics<NJ>(S, NJ <= 3 ? S.sys : sd, wave, lane);
+  } else if (tid < Q4_TILE) {
     constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
     const int c = tid;
     double s[NS], a[NA], sn[NS], F[NS * NA];
@@ -481,11 +614,12 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
     for (int f = 0; f < NS; ++f) s[f] = (double)S.st[c * 16 + f];
 #pragma unroll
     for (int i = 0; i < NA; ++i) a[i] = (double)S.A[c * na + i];
+    const SysDevice& sl = S.sys;
     if constexpr (NJ > 0 && NJ <= 3) {
-      if (p.const_dyn) env_simulate_derivative_const<NJ>(sd, s, a, true, sn, F);
-      else env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
+      if (p.const_dyn) env_simulate_derivative_const<NJ>(sl, s, a, true, sn, F);
+      else env_simulate_derivative<NJ>(sl, s, a, true, sn, F);
     } else {
-      env_simulate_derivative<NJ>(sd, s, a, true, sn, F);
+      env_simulate_derivative<NJ>(sl, s, a, true, sn, F);
     }
 #pragma unroll
     for (int f = 0; f < 16; ++f) S.stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
@@ -505,7 +639,7 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
 #pragma unroll
     for (int i = 0; i < NA; ++i) S.dra[c * na + i] = g[i];
   }
-  __syncthreads();
+  if constexpr (NJ < 3) __syncthreads();
   CSTAMP(3);
   if (!early_cf) CF.load<true>(C, wave, lane);
   if (wave == 0) {
@@ -518,7 +652,7 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   float* HC = H;             // 16 tiles
   float* ZB2 = H + 16 * 64;  // 16 tiles
   Q4CriticBwd CB;
-  q4_critic_forward_f<false, Q4_NW>(CF, XS, ZC, nullptr, HC, red, nullptr, wave, lane, [](int, int, float) {},
+  q4_critic_forward_f<false, Q4_NW>(CF, XS, ZC, nullptr, HC, red, nullptr, wave, lane, [](int, int, float, float) {},
                                     [&](int l) {
                                       if (l == 1) CB.load(C, wave, lane);
                                     });
@@ -527,10 +661,13 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   // middle of the critic's first backward through the dQ/da phase
   Q4Frags<1, 2, Q4_NW> B2;
   Q4Pair<16, Q4_NW> B1;
-  q4_critic_first_backward(CB, ZC, HC, nullptr, G0, red, wave, lane, [](int, int, float) {}, [&]() {
-    B2.load<false>(Ac.bwd(2), nullptr, 16, 256, wave, lane);
-    B1.load(Ac.bwd(1), 0, wave, lane);
-  });
+  q4_critic_first_backward(
+      CB, ZC, HC, nullptr, red, wave, lane, [](int, int, float) {},
+      [&]() {
+        B2.load<false>(Ac.bwd(2), nullptr, 16, 256, wave, lane);
+        B1.load(Ac.bwd(1), 0, wave, lane);
+      },
+      [&](int ln, float g) { G0[q4e(0, ln)] = g; });
   CSTAMP(6);
   // dQ/da = dV/ds' Fu + dr/da ; abar = -dQ/da / B  (NeuralNetwork.py:206-231)
   if (wave == 0) {  // d normalize / d s of every (state f, sample i) element at once
@@ -588,7 +725,9 @@ __global__ void __launch_bounds__(Q4_THREADS)
 }
 
 // the critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the rest)
-// in one grid, as k_chain_pair
+// in one grid, as k_chain_pair. (Measured and not kept: idle CUs of this grid reading the weight
+// images into their XCD's L2 ahead of the chains, +1 %: a CU's fragment stream is bounded by its
+// own L2-to-CU rate, ~20-30 B/clk, not by where the lines come from.)
 template <int NJ>
 __global__ void __launch_bounds__(Q4_THREADS)
     k_chain_pair_q4(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, NetView Ac, ChainScalars cs,

@@ -1093,7 +1093,6 @@ inline int q4_max_bp() {
   return v;
 }
 inline int chain_tile(int Bp) { return Bp <= q4_max_bp() ? Q4_TILE : CACTO_TILE; }
-
 template <int NJ>
 struct LaunchActorChain {
   static int run(const cacto_sys* sys, NetView Ac, NetView C, ChainScalars cs, const double* storage,
@@ -1777,7 +1776,10 @@ extern "C" int cacto_update_n_per(const cacto_sys* sys, const cacto_nets* nets, 
   const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
   const PerArgs per{sum_tree_d, min_tree_d, capacity, max_idx, beta, fresh_factor, eps, alpha, uniforms_d,
                     exp_counter_d, max_priority_d};
-  // with PER the sampling and the priority update sit between consecutive critic steps on one
-  // stream, so the two-stream pipeline (actor steps beside them) is the faster schedule here
+  // small batches: the paired single-stream schedule with the sampling and priority update between
+  // steps (car_park B = 64 with the q4 chains: 21.1 k vs 19.8 k updates/s two-stream); larger
+  // batches keep the two-stream pipeline (the actor step beside the sampling / priority update)
+  if (fused_adam(w.Bp))
+    return update_pipeline_pair(sys, nets, cfg, storage_d, nullptr, &per, K, B, w, as_stream(stream));
   return update_pipeline(sys, nets, cfg, storage_d, nullptr, &per, K, B, w, as_stream(stream));
 }

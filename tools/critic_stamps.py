@@ -58,6 +58,8 @@ def actor():
         print("actor B=%d total %.0f cycles: " % (B, t[9] - t[0]) + ", ".join("%s %.0f" % (n, x) for n, x in zip(names, np.diff(t))))
         if st[10] > st[1] and st[11] > st[10]:
             print("   actor forward: layer 1 %.0f, layer 2 %.0f, layer 3 %.0f" % (st[10] - st[1], st[11] - st[10], st[2] - st[11]))
+        if st[2] < st[12] < st[3]:
+            print("   dynamics: M / h %.0f, factor + solves %.0f" % (st[12] - st[2], st[3] - st[12]))
 
 
 def pair():
