@@ -92,6 +92,37 @@ def pmc_traffic(kernel="k_rollout<2,"):
     return (2.0 * fk + wk) * 1024.0, os.path.basename(fetch[-1]) + " + " + os.path.basename(write[-1])
 
 
+def pmc_update_traffic(B):
+    """HBM bytes per DI update at batch B from the committed learner PMC summaries
+    (profiles/rNN_pmc_learn_{fetch,write}_b<B>.csv: separate FETCH_SIZE / WRITE_SIZE passes over
+    the update kernels of a DI-only run). Bytes of every learner dispatch in the run ÷ the number of
+    updates (one critic gradient per update: the paired chain grid, or the standalone critic chain
+    that opens and the classic k_critic_grad). Same gfx950 corrections as pmc_traffic (FETCH_SIZE
+    x2, KiB). Returns (bytes, per-kernel bytes per update, source) or (None, None, None)."""
+    import csv
+    import glob
+    prof = os.path.join(ROOT, "profiles")
+    fetch = sorted(glob.glob(os.path.join(prof, "r*_pmc_learn_fetch_b%d.csv" % B)))
+    write = sorted(glob.glob(os.path.join(prof, "r*_pmc_learn_write_b%d.csv" % B)))
+    if not fetch or not write:
+        return None, None, None
+    tot, updates = {}, {}
+    for path, counter, scale in ((fetch[-1], "FETCH_SIZE", 2.0), (write[-1], "WRITE_SIZE", 1.0)):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["counter"] != counter:
+                    continue
+                k, n = row["kernel"], int(row["dispatches"])
+                tot[k] = tot.get(k, 0.0) + scale * float(row["mean"]) * 1024.0 * n
+                if k.startswith(("k_chain_pair", "k_critic_grad")):
+                    updates[(counter, k)] = n
+    nup = sum(n for (c, _), n in updates.items() if c == "FETCH_SIZE")
+    if not tot or nup == 0:
+        return None, None, None
+    per = {k: v / nup for k, v in tot.items()}
+    return sum(per.values()), per, os.path.basename(fetch[-1]) + " + " + os.path.basename(write[-1])
+
+
 def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -181,7 +212,9 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     def step():
         # one rollout batch = the sequential pass (k_rollout: actor + dynamics, S/A) and the parallel
         # reward / EE pass over the recorded steps (k_rollout_rewards), launched apart so each
-        # kernel gets its own HIP-event time; both run on torch's current stream
+        # kernel gets its own HIP-event time; both run on torch's current stream. (Rewards on the
+        # rollout's idle waves beside the dynamics measured slower: one f64 reward per lane is a
+        # 7.6 k-cycle chain on DI against wave 0's 2 k-cycle dynamics phase — DESIGN.md §3.)
         rl.rollout_batch(None, None, T, inputs=inputs, out=seq)
         ev[1].record()
         rl.rollout_rewards(out, n_d, T)
@@ -680,6 +713,25 @@ def main():
     if cpu is not None:
         cpu["host"] = host_info()
     traffic, traffic_src = pmc_traffic()
+    rw_traffic, _ = pmc_traffic("k_rollout_rewards<2>")
+    n_ep = len(roll["nsteps"])
+    roll_bytes = (roll["steps_per_call"] * (8 * ns + 4 * na + 8 + 24) + n_ep * (8 * ns + 24 + 8 * ns + 4)
+                  + 4 * rl.actor_model.P)
+    upd_roof = None
+    if updates:
+        # the update at the first batch (the reference's B = 128): SURVEY §8(d) algorithmic FLOP and
+        # bytes per update, against the measured rate and the PMC counter bytes of its kernels
+        Bu = [int(b) for b in args.batches.split(",") if b][0]
+        u = updates["B=%d" % Bu]
+        PA, PC = rl.actor_model.P, rl.critic_model.P
+        fl = Bu * world * (9 * fc_flops(ns) + 3 * fa_flops(ns, na)) + 12 * (PA + PC) + 3 * PC
+        by = Bu * world * ((3 * ns + 3) * 4 + 8) + 36 * (PA + PC) + 12 * PC
+        ctr, per, src = pmc_update_traffic(Bu)
+        upd_roof = {"batch": Bu, "flop_per_update": fl, "algorithmic_bytes_per_update": by,
+                    "ms_per_update": u["ms_per_update"], "achieved_tflops": fl / (u["ms_per_update"] * 1e-3) / 1e12,
+                    "mfma_frac": fl / (u["ms_per_update"] * 1e-3) / (FP32_MFMA_PEAK * world),
+                    "counter_bytes_per_update": ctr, "counter_bytes_by_kernel": per,
+                    "counter_over_algorithmic": (ctr / by) if ctr else None, "traffic_source": src}
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -707,7 +759,15 @@ def main():
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "kernel_ms": roll["seq_kernel_ms"], "flop_per_env_step": fa_flops(ns, na),
                          "rollout_batch_ms": roll["kernel_ms"], "rewards_kernel_ms": roll["rewards_kernel_ms"],
-                         "env_steps_per_launch": roll["steps_per_call"]},
+                         "env_steps_per_launch": roll["steps_per_call"],
+                         # bytes the batch (k_rollout + k_rollout_rewards) must move: per env step
+                         # s_{t+1} (8 ns), a_t (4 na), r_t (8), EE (24) written; per episode s_0 read
+                         # and written, EE_0, the length; the actor weights read once
+                         "batch_algorithmic_bytes": roll_bytes,
+                         "batch_traffic": (traffic + rw_traffic) if traffic and rw_traffic else None,
+                         "batch_traffic_over_algorithmic": ((traffic + rw_traffic) / roll_bytes
+                                                            if traffic and rw_traffic else None),
+                         "update": upd_roof},
             "critic_updates": updates,
             "episode_to_buffer": e2b,
             "ddp_labels": ddp,

@@ -80,6 +80,8 @@ _SIGS = {
                                      vp, C.c_double, C.c_double, C.c_double, vp, C.c_int, C.c_int, vp, sz, vp]),
     "cacto_update_pair_grads": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, vp, C.c_int, vp, vp,
                                           vp, vp, sz, vp]),
+    "cacto_update_pair_grads_stage": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, vp, C.c_int,
+                                                vp, vp, vp, vp, sz, C.c_int, vp]),
     "cacto_update_pair_apply": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, C.c_int, C.c_int, C.c_int,
                                           vp]),
     "cacto_rollout": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),

@@ -1528,16 +1528,25 @@ extern "C" int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const 
 // Data-parallel form of the paired schedule (update_pipeline_pair): per step, the gradients of the
 // critic step of update t and of the actor step of update t - 1 (either may be absent) go to one
 // flat buffer [critic P | actor P], the caller all-reduces it once (RCCL), then both Adam steps.
-extern "C" int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
-                                       const double* storage_d, const int32_t* idx_c_d, const float* is_w_d,
-                                       const int32_t* idx_a_d, int B, float* grad_d, float* y_d, float* V_d,
-                                       void* workspace_d, size_t workspace_bytes, void* stream) {
-  CACTO_REQUIRE(sys && cfg && storage_d && grad_d && B > 0 && (idx_c_d || idx_a_d),
-                "cacto_update_pair_grads: bad arguments");
-  if (int e = check_nets(nets)) return e;
+namespace {
+// stage bit 0: the chain(s) and the critic's weight gradient; bit 1: the actor's weight gradient
+// (which reads only the actor chain's panels in the workspace)
+int pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const double* storage_d,
+               const int32_t* idx_c_d, const float* is_w_d, const int32_t* idx_a_d, int B, float* grad_d, float* y_d,
+               float* V_d, void* workspace_d, size_t workspace_bytes, int stages, hipStream_t st) {
   CHECK_WS(workspace_d, workspace_bytes, B);
   const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
-  hipStream_t st = as_stream(stream);
+  const int Pc = sys->critic.params, Pa = sys->actor.params;
+  if (stages & 2) {
+    if (!idx_a_d) return CACTO_OK;
+    WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
+    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
+    CACTO_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, a.nch, Pa,
+                       grad_d + Pc);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
   float* yb = y_d ? y_d : w.scal;
   float* Vb = V_d ? V_d : w.scal + w.Bp;
   if (idx_c_d && idx_a_d) {
@@ -1552,7 +1561,6 @@ extern "C" int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* n
   } else {
     if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx_a_d, B, w, st)) return e;
   }
-  const int Pc = sys->critic.params, Pa = sys->actor.params;
   if (idx_c_d) {
     const bool sob = cfg->w_S != 0.0;
     WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
@@ -1561,15 +1569,33 @@ extern "C" int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* n
     hipLaunchKernelGGL(k_reduce, dim3(std::min((Pc + 255) / 256, 1024)), dim3(256), 0, st, w.slab, a.nch, Pc, grad_d);
     CACTO_CHECK_HIP(hipGetLastError());
   }
-  if (idx_a_d) {
-    WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
-    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
-    CACTO_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, a.nch, Pa,
-                       grad_d + Pc);
-    CACTO_CHECK_HIP(hipGetLastError());
-  }
+  if (stages & 2) return pair_grads(sys, nets, cfg, storage_d, idx_c_d, is_w_d, idx_a_d, B, grad_d, y_d, V_d,
+                                    workspace_d, workspace_bytes, 2, st);
   return CACTO_OK;
+}
+}  // namespace
+
+extern "C" int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                       const double* storage_d, const int32_t* idx_c_d, const float* is_w_d,
+                                       const int32_t* idx_a_d, int B, float* grad_d, float* y_d, float* V_d,
+                                       void* workspace_d, size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && grad_d && B > 0 && (idx_c_d || idx_a_d),
+                "cacto_update_pair_grads: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  return pair_grads(sys, nets, cfg, storage_d, idx_c_d, is_w_d, idx_a_d, B, grad_d, y_d, V_d, workspace_d,
+                    workspace_bytes, 1 | 2, as_stream(stream));
+}
+
+extern "C" int cacto_update_pair_grads_stage(const cacto_sys* sys, const cacto_nets* nets,
+                                             const cacto_update_cfg* cfg, const double* storage_d,
+                                             const int32_t* idx_c_d, const float* is_w_d, const int32_t* idx_a_d,
+                                             int B, float* grad_d, float* y_d, float* V_d, void* workspace_d,
+                                             size_t workspace_bytes, int stage, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && grad_d && B > 0 && (idx_c_d || idx_a_d) && (stage == 0 || stage == 1),
+                "cacto_update_pair_grads_stage: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  return pair_grads(sys, nets, cfg, storage_d, idx_c_d, is_w_d, idx_a_d, B, grad_d, y_d, V_d, workspace_d,
+                    workspace_bytes, stage == 0 ? 1 : 2, as_stream(stream));
 }
 
 extern "C" int cacto_update_pair_apply(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,

@@ -187,7 +187,7 @@ class PrioritizedReplayBuffer(ReplayBuffer):
             u = torch.as_tensor(np.asarray(uniforms, dtype=np.float64), device=DEVICE)
         idx = torch.empty(B, dtype=torch.int32, device=DEVICE)
         w = torch.empty(B, dtype=torch.float32, device=DEVICE)
-        if self.dp_world > 1:
+        if self.dp_world > 1 or self.dp_group is not None:
             stats = self.shard_stats()
             L.lib().call("cacto_per_sample_global", dptr(self.sum_tree), dptr(self.min_tree), self.cap,
                          self.max_idx(), self.beta, dptr(u), B, dptr(stats), self.dp_world, dptr(idx), dptr(w),

@@ -34,22 +34,40 @@ def dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update):
     apply("actor", ga, False)
 
 
-def dp_pipeline(K, grads, all_reduce, apply):
-    """K data-parallel updates (RL.py:101-118 each) with ONE gradient exchange per update.
+class _Done:
+    """The handle of an exchange that completed when it was issued (a synchronous all-reduce)."""
 
-    Step t = 0..K computes, into one flat buffer, the gradient of the critic step of update t
-    (c = t, absent at t = K) and of the actor step of update t - 1 (a = t - 1, absent at t = 0),
-    all-reduces it once, then applies both Adam steps. The critic step of update t never reads the
-    actor, and the actor step of update t - 1 sees the critic after its update t - 1 — the ordering
-    RL.py:104-109 prescribes — so the K updates equal the sequential loop. Gradients are normalised by
-    the GLOBAL batch, so the exchange is a plain sum. grads(c, a) -> tensor, apply(c, a, g).
+    def wait(self):
+        return True
+
+
+def dp_pipeline(K, stages, all_reduce, apply):
+    """K data-parallel updates (RL.py:101-118 each) with the gradient exchange off the critical path.
+
+    Step t = 0..K forms the gradient of the critic step of update t (c = t, absent at t = K) and of
+    the actor step of update t - 1 (a = t - 1, absent at t = 0), then applies both Adam steps. The
+    critic step of update t never reads the actor, and the actor step of update t - 1 sees the
+    critic after its update t - 1 — the ordering RL.py:104-109 prescribes — so the K updates equal
+    the sequential loop. Gradients are normalised by the GLOBAL batch, so the exchange is a plain
+    sum.
+
+    stages(c, a) is a generator that yields ("critic", g) / ("actor", g) as each part is formed
+    (critic first); each part's all-reduce is issued the moment it is yielded — all_reduce(g)
+    returns a handle with wait() (torch.distributed async work; RCCL runs it on its own stream
+    after the work already queued) — so the critic's exchange overlaps the forming of the actor
+    gradient, and the actor's exchange overlaps the critic Adam step. apply(which, step, g) runs
+    after that part's wait(), critic before actor, as the sequential loop has them.
     """
     for t in range(K + 1):
         c = t if t < K else None
         a = t - 1 if t > 0 else None
-        g = grads(c, a)
-        all_reduce(g)
-        apply(c, a, g)
+        pending = []
+        for which, g in stages(c, a):
+            h = all_reduce(g)
+            pending.append((which, g, h if h is not None else _Done()))
+        for which, g, h in pending:
+            h.wait()
+            apply(which, c if which == "critic" else a, g)
 
 
 class Adam:
@@ -167,12 +185,18 @@ class RL_AC:
     dp_group = None
 
     def set_data_parallel(self, world_size, group=None):
-        """Replicated weights, local minibatch per rank, RCCL all-reduce of the gradients: one
-        all-reduce per update of [critic gradient of update t | actor gradient of update t-1]
-        (dp_pipeline), which keeps RL.py:104-109's order (the actor gradient is taken against the
-        critic after its own update)."""
+        """Replicated weights, local minibatch per rank, RCCL all-reduce of the gradients: per
+        update [critic gradient of update t | actor gradient of update t-1] (dp_pipeline), the
+        critic part's all-reduce issued as soon as it is formed, which keeps RL.py:104-109's order
+        (the actor gradient is taken against the critic after its own update). An explicit `group`
+        selects the exchange path even for world_size 1 (a one-rank RCCL group: the path the
+        graph-capture test runs on a one-GPU box)."""
         self.dp_world = int(world_size)
         self.dp_group = group
+
+    @property
+    def _dp(self):
+        return self.dp_world > 1 or self.dp_group is not None
 
     # ---- gradient pieces (explicit rows; used by the DP path and the parity tests) ----
     def critic_grad_flat(self, rows, idx, w=None, y=None, V=None, Vt=None):
@@ -212,7 +236,7 @@ class RL_AC:
 
     # ---- RL.py:101-111 on replay rows ----
     def update_rows(self, storage, idx, is_w=None, y=None, V=None, Vt=None):
-        if self.dp_world > 1:
+        if self._dp:
             return self._update_rows_dp(storage, idx, is_w, y, V, Vt)
         B = idx.shape[0]
         ws = self.workspace(B)
@@ -227,7 +251,7 @@ class RL_AC:
         actor step of update t on a second stream (the critic step never reads the actor), with
         results bit-identical to K update_rows calls. Single rank (the data-parallel update
         all-reduces between the two steps)."""
-        if self.dp_world > 1:
+        if self._dp:
             return self._update_rows_n_dp(storage, idx_steps)
         K, B = int(idx_steps.shape[0]), int(idx_steps.shape[1])
         ws = self.workspace(B)
@@ -259,13 +283,27 @@ class RL_AC:
         is the same work as calling update_rows per step, without the per-launch host cost.
         idx_steps [K, B] int32 (device, kept alive by the caller). With `per_buffer` (a
         PrioritizedReplayBuffer) each step instead samples from `uniforms[k]` ([K, B] f64) and
-        updates the priorities (learn_and_update with PER, RL.py:122-137). Single rank only: the
-        data-parallel update all-reduces between the kernels."""
-        if self.dp_world > 1:
-            raise RuntimeError("capture_updates: the data-parallel update is not captured")
+        updates the priorities (learn_and_update with PER, RL.py:122-137).
+        Data parallel (RCCL process group): the graph holds the dp_pipeline loop — stage kernels,
+        the all-reduces on RCCL's stream and the Adam steps joined by stream waits — since nothing
+        in it waits on the host (gloo's collectives run on the host and cannot be captured)."""
         K = (uniforms if per_buffer is not None else idx_steps).shape[0]
         B = (uniforms if per_buffer is not None else idx_steps).shape[1]
         self.workspace(B)                       # allocated before the capture
+        if self._dp:
+            import torch.distributed as dist
+            if dist.get_backend(self.dp_group) != "nccl":
+                raise RuntimeError("capture_updates: a data-parallel loop is captured only over RCCL (backend "
+                                   "'nccl'), not %r" % dist.get_backend(self.dp_group))
+            self._dp_grad_buf(self.critic_model.P + self.actor_model.P)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                if per_buffer is None:
+                    self._update_rows_n_dp(storage, idx_steps)
+                else:
+                    self.update_rows_n_per_dp(per_buffer, uniforms)
+            return g
         y = torch.empty(B, dtype=torch.float32, device=DEVICE)
         V = torch.empty_like(y)
         torch.cuda.synchronize()
@@ -308,19 +346,32 @@ class RL_AC:
         g = self._dp_grad_buf(Pc + Pa)
         idx_steps = idx_steps.contiguous()
 
-        def grads(c, a):
+        def stages(c, a):
             ic = idx_steps[c] if c is not None else None
             ia = idx_steps[a] if a is not None else None
-            L.lib().call("cacto_update_pair_grads", self.sys.handle, C.byref(self.nets), C.byref(cfg),
-                         dptr(storage, torch.float64), dptr(ic, torch.int32), dptr(is_w if c is not None else None),
-                         dptr(ia, torch.int32), B, dptr(g), dptr(y if c is not None else None),
-                         dptr(V if c is not None else None), dptr(ws), ws.numel() * 4, stream())
-            return g[:Pc] if a is None else (g[Pc:] if c is None else g)
+            args = (self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(storage, torch.float64),
+                    dptr(ic, torch.int32), dptr(is_w if c is not None else None), dptr(ia, torch.int32), B, dptr(g),
+                    dptr(y if c is not None else None), dptr(V if c is not None else None), dptr(ws), ws.numel() * 4)
+            L.lib().call("cacto_update_pair_grads_stage", *args, 0, stream())
+            if c is not None:
+                yield "critic", g[:Pc]
+            if a is not None:
+                L.lib().call("cacto_update_pair_grads_stage", *args, 1, stream())
+                yield "actor", g[Pc:]
+        dp_pipeline(K, stages, self._all_reduce_async, self._dp_apply(g, cfg))
 
-        def apply(c, a, _):
+    def _all_reduce_async(self, t):
+        import torch.distributed as dist
+        return dist.all_reduce(t, group=self.dp_group, async_op=True)
+
+    def _dp_apply(self, g, cfg, after_critic=None):
+        def apply(which, step, _):
+            crit = which == "critic"
             L.lib().call("cacto_update_pair_apply", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(g),
-                         int(c is not None), int(a is not None), int(not self.conf.MC), stream())
-        dp_pipeline(K, grads, lambda t: dist.all_reduce(t, group=self.dp_group), apply)
+                         int(crit), int(not crit), int(crit and not self.conf.MC), stream())
+            if crit and after_critic is not None:
+                after_critic(step)
+        return apply
 
     def update_rows_n_per_dp(self, buffer, uniforms):
         """K data-parallel PER updates (RL.py:122-137 on every rank's replay shard, the sampling of
@@ -344,24 +395,23 @@ class RL_AC:
         V = torch.empty_like(y)
         drawn = {}
 
-        def grads(c, a):
+        def stages(c, a):
             if c is not None:
                 drawn[c] = buffer.sample_device(u[c])
                 drawn.pop(c - 2, None)
             ic, wc = drawn[c] if c is not None else (None, None)
             ia = drawn[a][0] if a is not None else None
-            L.lib().call("cacto_update_pair_grads", self.sys.handle, C.byref(self.nets), C.byref(cfg),
-                         dptr(buffer.storage, torch.float64), dptr(ic, torch.int32), dptr(wc), dptr(ia, torch.int32),
-                         B, dptr(g), dptr(y if c is not None else None), dptr(V if c is not None else None), dptr(ws),
-                         ws.numel() * 4, stream())
-            return g[:Pc] if a is None else (g[Pc:] if c is None else g)
-
-        def apply(c, a, _):
-            L.lib().call("cacto_update_pair_apply", self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(g),
-                         int(c is not None), int(a is not None), int(not self.conf.MC), stream())
+            args = (self.sys.handle, C.byref(self.nets), C.byref(cfg), dptr(buffer.storage, torch.float64),
+                    dptr(ic, torch.int32), dptr(wc), dptr(ia, torch.int32), B, dptr(g),
+                    dptr(y if c is not None else None), dptr(V if c is not None else None), dptr(ws), ws.numel() * 4)
+            L.lib().call("cacto_update_pair_grads_stage", *args, 0, stream())
             if c is not None:
-                buffer.update_priorities_device(drawn[c][0], y, V)
-        dp_pipeline(K, grads, lambda t: dist.all_reduce(t, group=self.dp_group), apply)
+                yield "critic", g[:Pc]
+            if a is not None:
+                L.lib().call("cacto_update_pair_grads_stage", *args, 1, stream())
+                yield "actor", g[Pc:]
+        dp_pipeline(K, stages, self._all_reduce_async,
+                    self._dp_apply(g, cfg, lambda c: buffer.update_priorities_device(drawn[c][0], y, V)))
 
     def _dp_grad_buf(self, n):
         if getattr(self, "_dp_g", None) is None or self._dp_g.numel() < n:
@@ -392,7 +442,7 @@ class RL_AC:
         B = self.conf.BATCH_SIZE
         per = getattr(buffer, "prioritized", False)
         if per:
-            if self.dp_world > 1 and buffer.dp_world != self.dp_world:
+            if self._dp and (buffer.dp_world, buffer.dp_group) != (self.dp_world, self.dp_group):
                 buffer.set_data_parallel(self.dp_world, self.dp_group)
             # the updates between two checkpoint saves as one pipelined call; the uniforms are the
             # per-step random.random() draws of the sequential loop, in the same order
@@ -400,7 +450,7 @@ class RL_AC:
             while i < n:
                 k = min(n - i, self.conf.save_interval - update_step_counter % self.conf.save_interval)
                 U = np.array([[buffer.random.random() for _ in range(B)] for _ in range(k)], dtype=np.float64)
-                if self.dp_world == 1:
+                if not self._dp:
                     self.update_rows_n_per(buffer, torch.as_tensor(U, device=DEVICE))
                 else:
                     self.update_rows_n_per_dp(buffer, torch.as_tensor(U, device=DEVICE))

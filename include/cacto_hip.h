@@ -266,6 +266,16 @@ int cacto_update_pair_grads(const cacto_sys* sys, const cacto_nets* nets, const 
                             const double* storage_d, const int32_t* idx_c_d, const float* is_w_d,
                             const int32_t* idx_a_d, int B, float* grad_d, float* y_d, float* V_d,
                             void* workspace_d, size_t workspace_bytes, void* stream);
+/* cacto_update_pair_grads in two stream-ordered stages, so the critic part's all-reduce can be
+ * issued while the actor part is still being formed: stage 0 runs the chain(s) and writes the
+ * critic gradient (when idx_c_d), stage 1 the actor's weight gradient into grad_d + P_critic (when
+ * idx_a_d; a no-op otherwise). Stage 1 reads the panels stage 0 left in the workspace, so the two
+ * calls take the same arguments, stage 0 first, on the same stream. Stage 0 + stage 1 = one
+ * cacto_update_pair_grads call, bit for bit. */
+int cacto_update_pair_grads_stage(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                  const double* storage_d, const int32_t* idx_c_d, const float* is_w_d,
+                                  const int32_t* idx_a_d, int B, float* grad_d, float* y_d, float* V_d,
+                                  void* workspace_d, size_t workspace_bytes, int stage, void* stream);
 int cacto_update_pair_apply(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                             const float* grad_d, int critic, int actor, int soft_update, void* stream);
 

@@ -85,18 +85,24 @@ def _run_update(rows, world, all_reduce, n_steps=3, pipelined=True):
         for _ in range(n_steps):
             dp_update_step(critic_grad, actor_grad, apply, all_reduce, soft_update=True)
         return {k: _flat(v).numpy() for k, v in st.items()}
-    nc = _flat(st["critic"]).numel()
 
-    def grads(c, a):
-        parts = ([critic_grad()] if c is not None else []) + ([actor_grad()] if a is not None else [])
-        return torch.cat(parts)
-
-    def apply_pair(c, a, g):
+    def stages(c, a):
+        # each part is exchanged as soon as it is formed (dp_pipeline issues the all-reduce at the
+        # yield), so the critic's exchange is in flight while the actor gradient is computed
         if c is not None:
-            apply("critic", g[:nc], True)
+            yield "critic", critic_grad()
         if a is not None:
-            apply("actor", g[nc:] if c is not None else g, False)
-    dp_pipeline(n_steps, grads, all_reduce, apply_pair)
+            yield "actor", actor_grad()
+
+    order = []
+
+    def apply_part(which, step, g):
+        order.append((which, step))
+        apply(which, g, which == "critic")
+    dp_pipeline(n_steps, stages, all_reduce, apply_part)
+    # RL.py:104-109 per update: critic(t) before actor(t); actor(t-1) after critic(t-1)
+    assert order == [("critic", 0)] + [x for t in range(1, n_steps) for x in (("critic", t), ("actor", t - 1))] + \
+        [("actor", n_steps - 1)]
     return {k: _flat(v).numpy() for k, v in st.items()}
 
 
@@ -106,7 +112,7 @@ def _worker(rank, world, port, rows, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         n = rows.shape[0] // world
-        out = _run_update(rows[rank * n:(rank + 1) * n], world, lambda t: dist.all_reduce(t))
+        out = _run_update(rows[rank * n:(rank + 1) * n], world, lambda t: dist.all_reduce(t, async_op=True))
         q.put((rank, out))
     finally:
         dist.destroy_process_group()

@@ -368,3 +368,61 @@ def test_dp_per_loop_pipelined_equals_sequential():
         assert np.array_equal(a, b)
     # the shards differ (each rank's own rows and priorities)
     assert not np.array_equal(res[0][0][1][2], res[1][0][1][2])
+
+
+def _rccl_worker(rank, port, rows, idx, q):
+    """One rank over RCCL (backend 'nccl'): the exchange path of RL_AC (an explicit process group
+    selects it at world size 1) run eagerly and captured into a HIP graph."""
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        storage = torch.as_tensor(rows, device="cuda")
+        ix = torch.as_tensor(idx.astype(np.int32), device="cuda")
+        single = _learner(1)
+        single.update_rows_n(storage, ix)                     # the one-rank pipeline (no exchange)
+        eager = _learner(1)
+        eager.set_data_parallel(1, dist.group.WORLD)
+        eager.update_rows_n(storage, ix)                      # dp_pipeline, RCCL all-reduces
+        graphed = _learner(1)
+        graphed.set_data_parallel(1, dist.group.WORLD)
+        g = graphed.capture_updates(storage, ix)
+        g.replay()
+        torch.cuda.synchronize()
+        first = (_state(single), _state(eager), _state(graphed), graphed.steps.cpu().tolist())
+        eager.update_rows_n(storage, ix)                      # a second replay continues from the new state
+        g.replay()
+        torch.cuda.synchronize()
+        q.put((0, first, _state(eager), _state(graphed), graphed.steps.cpu().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_loop_over_rccl_is_graph_capturable():
+    """The data-parallel K-step loop (dp_pipeline: staged gradients, the critic part's all-reduce
+    issued before the actor part is formed, Adam steps after each part lands) over RCCL, captured
+    into one HIP graph: replays equal the eager loop bit for bit, and at one rank (the exchange is
+    the identity) both equal the single-rank pipeline. The first RCCL communicator this package
+    runs; the multi-GPU driver runs the same code with world size N."""
+    import torch.multiprocessing as mp
+    rng = np.random.default_rng(91)
+    N = 4096
+    rows = _rows(N, 92)
+    idx = rng.integers(0, N, size=(6, 128))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(0, _free_port(), rows, idx, q))
+    p.start()
+    try:
+        _, first, eager2, graphed2, steps2 = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert p.exitcode == 0
+    single, eager, graphed, steps = first
+    assert steps == [6, 6] and steps2 == [12, 12]
+    for a, b, c in zip(single, eager, graphed):
+        assert np.array_equal(a, b) and np.array_equal(b, c)
+    for a, b in zip(eager2, graphed2):
+        assert np.array_equal(a, b)

@@ -280,23 +280,30 @@ def test_rollout_di_known_answer():
 
 
 @pytest.mark.parametrize("system", ["double_integrator", "manipulator", "car_park", "ur5"])
-def test_rollout_rewards_separate_launch(system):
+@pytest.mark.parametrize("ep,sched", [(1, (0, 0)), (1, (1, 3)), (0, (2, 2))])
+def test_rollout_rewards_separate_launch(system, ep, sched):
     """cacto_rollout_rewards over a recorded S/A-only rollout gives exactly the R / EE of the
-    combined cacto_rollout call (bench.py launches the two kernels apart)."""
+    combined cacto_rollout call (bench.py launches the two kernels apart) — under the automatic
+    schedule and a slot-refilling one (1 group, 3 workgroups), with the actor and with zero
+    controls (ep == 0), and with an episode of length 0 (EE_0 only)."""
     conf, genv, oe, nn, rl = _nets(system, None, seed=2)
     rng = random.Random(5)
     S0 = np.array([oe.reset(rng) for _ in range(37)])
     ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
+    ns_[3] = 0                                   # an episode of length 0: EE_0 only, from the refill
     T = max(ns_)
-    ref = rl.rollout_batch(S0, ns_, T)
-    got = rl.rollout_batch(S0, ns_, T, want=("S", "A"))
+    ref = rl.rollout_batch(S0, ns_, T, ep=ep, sched=sched)
+    got = rl.rollout_batch(S0, ns_, T, ep=ep, want=("S", "A"), sched=sched)
     got["R"] = torch.full_like(ref["R"], float("nan"))
     got["EE"] = torch.full_like(ref["EE"], float("nan"))
-    rl.rollout_rewards(got, torch.as_tensor(np.asarray(ns_, dtype=np.int32), device="cuda"), T)
+    rl.rollout_rewards(got, torch.as_tensor(np.asarray(ns_, dtype=np.int32), device="cuda"), T, ep=ep)
     torch.cuda.synchronize()
     for k, n in enumerate(ns_):
         np.testing.assert_array_equal(got["R"][k, :n].cpu().numpy(), ref["R"][k, :n].cpu().numpy())
         np.testing.assert_array_equal(got["EE"][k, :n + 1].cpu().numpy(), ref["EE"][k, :n + 1].cpu().numpy())
+        assert not np.isnan(ref["EE"][k, :n + 1].cpu().numpy()).any()
+    if ep == 0:
+        return
     w = conf.cost_weights_running
     S, A, R = got["S"].cpu().numpy(), got["A"].cpu().numpy(), got["R"].cpu().numpy()
     for k in range(0, len(S0), 6):

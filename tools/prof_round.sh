@@ -1,8 +1,9 @@
-# Round profile set (see profiles/README.md). Usage: bash tools/prof_round.sh r02
+# Round profile set (see profiles/README.md). Usage: bash tools/prof_round.sh r03
 #  1. kernel trace of the default bench (every system), and of the DI update loop at B = 128 and at
 #     B = 4096 in runs of their own (so per-batch learner kernel times are readable);
 #  2. PMC passes, one counter group per run (TCC slot limits): FETCH_SIZE, WRITE_SIZE of the
-#     rollout; MFMA busy cycles / MFMA MOPS / GRBM_GUI_ACTIVE of the rollout and learner kernels.
+#     rollout; MFMA busy cycles / MFMA MOPS / GRBM_GUI_ACTIVE of the rollout and learner kernels;
+#     FETCH_SIZE, WRITE_SIZE of the learner kernels at B = 128 and B = 4096 (DI only).
 set -e
 export TMPDIR=/tmp
 R=$1
@@ -24,3 +25,13 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "k_rollout|k_critic_grad|k_actor_grad|k_wgrad|k_chain_pair" -d $D/mfma4096 -o run -- python3 bench.py $PMCARGS --batches 4096 > $D/mfma4096.json 2> $D/mfma4096.err
 python3 tools/prof_summary.py pmc $D/mfma128/run_results.db > $D/pmc_mfma_b128.csv
 python3 tools/prof_summary.py pmc $D/mfma4096/run_results.db > $D/pmc_mfma_b4096.csv
+LEARN="k_chain_pair|k_critic_grad|k_actor_grad|k_wgrad|k_adam"
+for B in 128 4096; do
+  for C in FETCH_SIZE WRITE_SIZE; do
+    c=$(echo $C | cut -d_ -f1 | tr A-Z a-z)
+    timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex "$LEARN" -d $D/l${c}$B -o run -- python3 bench.py $PMCARGS --batches $B > $D/l${c}$B.json 2> $D/l${c}$B.err
+    python3 tools/prof_summary.py pmc $D/l${c}$B/run_results.db > $D/pmc_learn_${c}_b$B.csv
+  done
+done
+# keep the summaries only (the raw rocprofv3 databases would overflow the copy-back)
+for d in trace b128 b4096 fetch write mfma128 mfma4096 lfetch128 lwrite128 lfetch4096 lwrite4096; do rm -rf $D/$d; done

@@ -40,6 +40,9 @@ def main():
         print("   chain dynamics after the actor: RNEA (wave 0) %.0f, CRBA columns (waves 1-3) %s"
               % (float(st[9]) - t[1], ", ".join("%.0f" % (float(st[9 + w]) - t[1]) if st[9 + w] > st[1] else "-"
                                                    for w in (1, 2, 3))))
+    if st[13] > st[2] or st[14] > st[2]:
+        print("   reward waves after the actor / dynamics phase: r_t (wave 1) %s, EE(s_t) (wave 2) %s, EE(s_n) (wave 3) %s"
+              % tuple("%.0f" % (float(st[k]) - t[2]) if st[k] > st[2] else "-" for k in (13, 14, 15)))
     print("   wave 0 after the dynamics phase: s' %.0f, advance/stores %.0f, refill+ballot %.0f, barrier %.0f"
           % (float(st[6]) - t[2], float(st[7]) - float(st[6]), float(st[8]) - float(st[7]), t[3] - float(st[8])))
 
