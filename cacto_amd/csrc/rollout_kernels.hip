@@ -513,13 +513,42 @@ __device__ __forceinline__ void ro_refill(bool need, int c, int& head, RoShared<
   }
 }
 
+// A slot's state as wave 0's lane c keeps it in registers: active flag, episode, step, s_t and, for
+// prismatic chains, the episode's Cholesky factor and bias forces (loaded from the slot's LDS copy
+// after the lane (re)fills it).
+template <int NJ, int NG>
+struct RoSlotRegs {
+  static constexpr int ns = Dims<NJ>::NS, SL = RoCfg<NG>::SL;
+  bool act = false;
+  int b = 0, t = 0, n = 0;
+  double s[ns];
+  ConstDyn<NJ> cd;
+  __device__ __forceinline__ void load(const RoShared<NJ, NG>& Sh, int c, bool cdyn) {
+    if (c >= SL) return;
+    act = Sh.sact[c] != 0;
+    b = Sh.sb[c];
+    t = Sh.st[c];
+    n = Sh.sn[c];
+#pragma unroll
+    for (int i = 0; i < ns; ++i) s[i] = Sh.sS[c * ns + i];
+    if constexpr (NJ > 0) {
+      if (cdyn) {
+#pragma unroll
+        for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = Sh.MS[k * SL + c];
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) cd.h[i] = Sh.hS[i * SL + c];
+      }
+    }
+  }
+};
+
 // Wave 0, lane c (< SL): after s' = f(s, a) of slot c: state + next actor input, the trajectory
 // stores of (a_t, s_{t+1}), and the end of the episode (status, slot refill).
 template <int NJ, int NG>
 __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* sn, const float* a,
                                            RoShared<NJ, NG>& Sh, const SysDevice& sd, int T,
                                            double* __restrict__ Straj, float* __restrict__ Atraj,
-                                           int32_t* __restrict__ status, const RoNorm<Dims<NJ>::NS>& nrm) {
+                                           int32_t* __restrict__ status, const RoNorm<Dims<NJ>::NS>& nrm, int n) {
   constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
   const cacto_sys_params& p = sd.p;
   bool bad = false;
@@ -534,7 +563,6 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
   if (Straj)
 #pragma unroll
     for (int i = 0; i < ns; ++i) Straj[((size_t)b * (T + 1) + tc + 1) * ns + i] = sn[i];
-  const int n = Sh.sn[c];
   if (bad && Straj) {
     // RL.py:229-231 drops the episode; the rest of its trajectory is NaN (the reward / EE pass
     // skips NaN states)
@@ -594,6 +622,12 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   __syncthreads();
   const int c = L.lane % SL;  // slot of this lane
   const RoX0Lane<ns, SL> x0l(nrm, L.lane);
+  // wave 0, lane c < SL: its slot's state in registers for the whole launch (the lane is the only
+  // writer of the slot's LDS copy: ro_advance and ro_refill run on it), so the dynamics phase waits
+  // only for the action, not for LDS reads of s_t and the episode's factored mass matrix
+  const bool cdyn = RoConstDyn<NJ>::ok && !split_dyn && NJ > 0;
+  RoSlotRegs<NJ, NG> sr;
+  if (L.wave == 0) sr.load(Sh, c, cdyn);
   for (int it = 0; Sh.anyact; ++it) {
     RSTAMP(0);
     // joint placements of s_t (published by the actor's first barrier)
@@ -605,7 +639,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
     }
     if (use_actor) ro_actor<NG, ns, na, REGK, LDSK>(R, Sh.W, W2g, L, it);
     RSTAMP(1);
-    const bool active = L.lane < SL && Sh.sact[c] != 0;
+    const bool active = L.lane < SL && (L.wave == 0 ? sr.act : Sh.sact[c] != 0);
     if (split_dyn) {
       if constexpr (NJ > 0) {
         if (L.wave == 0 && active) {
@@ -624,11 +658,10 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
     if (L.wave == 0) {
       bool fin = false;
       if (active) {
-        const int b = Sh.sb[c], tc = Sh.st[c];
-        double s[ns], ad[na], sn[ns];
+        const int b = sr.b, tc = sr.t;
+        double ad[na], sn[ns];
+        const double* s = sr.s;
         float a[na];
-#pragma unroll
-        for (int i = 0; i < ns; ++i) s[i] = Sh.sS[c * ns + i];
 #pragma unroll
         for (int i = 0; i < na; ++i) {
           a[i] = use_actor ? Sh.W.a[c * na + i] : 0.f;
@@ -643,21 +676,20 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
             for (int i = 0; i < NJ; ++i) h[i] = Sh.hS[i * SL + c];
             chain_step<NJ>(sd, s, ad, M, h, sn);
           } else {
-            ConstDyn<NJ> cd;
-#pragma unroll
-            for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = Sh.MS[k * SL + c];
-#pragma unroll
-            for (int i = 0; i < NJ; ++i) cd.h[i] = Sh.hS[i * SL + c];
-            env_simulate_const<NJ>(sd, cd, s, ad, sn);
+            env_simulate_const<NJ>(sd, sr.cd, s, ad, sn);
           }
         } else {
           env_simulate<NJ>(sd, s, ad, false, sn);
         }
         RSTAMP(6);
-        fin = ro_advance<NJ, NG>(c, b, tc, sn, a, Sh, sd, T, Straj, Atraj, status, nrm);
+        fin = ro_advance<NJ, NG>(c, b, tc, sn, a, Sh, sd, T, Straj, Atraj, status, nrm, sr.n);
+#pragma unroll
+        for (int i = 0; i < ns; ++i) sr.s[i] = sn[i];
+        sr.t = tc + 1;
         RSTAMP(7);
       }
       ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L);
+      if (fin) sr.load(Sh, c, cdyn);  // the slot's next episode (or none), written by this lane
       // next actor input from s_{t+1} (or a refilled s_0): the slots' lanes wrote sS above; LDS
       // operations of one wave complete in order, so after this wave-scope fence every lane reads them
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
