@@ -1215,6 +1215,16 @@ WgArgs wg_args(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int
   return a;
 }
 
+// the weight-gradient GEMM of one network into its slabs; returns the chunk count k_adam sums
+int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int bias_r0, float* slab,
+                 hipStream_t st, int* nch) {
+  const WgArgs a = wg_args(t, gb, r_begin, r_end, bias_r0);
+  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, slab);
+  CACTO_CHECK_HIP(hipGetLastError());
+  *nch = a.nch;
+  return CACTO_OK;
+}
+
 ChainScalars chain_scalars(const cacto_update_cfg* cfg, int B) {
   ChainScalars cs;
   cs.w_S = (float)cfg->w_S;
@@ -1270,11 +1280,7 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
   if (int e = launch_critic_chain(sys, nets, cfg, storage, idx, isw, B, y, V, Vt, w, st)) return e;
   const ChainScalars cs = chain_scalars(cfg, B);
   const bool sob = cs.w_S != 0.f;
-  WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
-  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
-  CACTO_CHECK_HIP(hipGetLastError());
-  *nch_out = a.nch;
-  return CACTO_OK;
+  return launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, nch_out);
 }
 
 int launch_actor_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
@@ -1289,11 +1295,7 @@ int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, c
                                  const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
                                  int* nch_out) {
   if (int e = launch_actor_chain(sys, nets, cfg, storage, idx, B, w, st)) return e;
-  WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
-  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
-  CACTO_CHECK_HIP(hipGetLastError());
-  *nch_out = a.nch;
-  return CACTO_OK;
+  return launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, st, nch_out);
 }
 
 // src: the weights the step starts from (nullptr = in place; cacto_update_n steps the critic from one
@@ -1378,21 +1380,19 @@ int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_u
   if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 0, critic_adam_net(sys, nets, cfg, w, soft, src, nb), nullptr,
                                                  nets->step_d, st);
   const bool sob = cfg->w_S != 0.0;
-  WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
-  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
-  CACTO_CHECK_HIP(hipGetLastError());
+  int nch = 0;
+  if (int e = launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, &nch)) return e;
   cacto_nets dst = *nets;
   dst.critic_d = nb;
-  return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, a.nch, soft, st, src);
+  return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, nch, soft, st, src);
 }
 
 int actor_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
                     hipStream_t st) {
   if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 1, actor_adam_net(sys, nets, cfg, w), nullptr, nets->step_d, st);
-  WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
-  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
-  CACTO_CHECK_HIP(hipGetLastError());
-  return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, a.nch, 0, st);
+  int nch = 0;
+  if (int e = launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, st, &nch)) return e;
+  return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, nch, 0, st);
 }
 
 }  // namespace
@@ -1539,10 +1539,9 @@ int pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_
   const int Pc = sys->critic.params, Pa = sys->actor.params;
   if (stages & 2) {
     if (!idx_a_d) return CACTO_OK;
-    WgArgs a = wg_args(sys->actor, w.act, 0, w.Bp, 0);
-    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab_a);
-    CACTO_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, a.nch, Pa,
+    int nch = 0;
+    if (int e = launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, st, &nch)) return e;
+    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, nch, Pa,
                        grad_d + Pc);
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
@@ -1563,10 +1562,9 @@ int pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_
   }
   if (idx_c_d) {
     const bool sob = cfg->w_S != 0.0;
-    WgArgs a = wg_args(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp);
-    hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, w.slab);
-    CACTO_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pc + 255) / 256, 1024)), dim3(256), 0, st, w.slab, a.nch, Pc, grad_d);
+    int nch = 0;
+    if (int e = launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, &nch)) return e;
+    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pc + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, Pc, grad_d);
     CACTO_CHECK_HIP(hipGetLastError());
   }
   if (stages & 2) return pair_grads(sys, nets, cfg, storage_d, idx_c_d, is_w_d, idx_a_d, B, grad_d, y_d, V_d,

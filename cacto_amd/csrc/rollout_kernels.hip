@@ -165,23 +165,39 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[g][0] = acc[g][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int rd = (L.lane >> 2) * 20 + 4 * (L.lane & 3);
+    // LDS operands one step ahead (the next 64-k block's activations, the next 16-row block of
+    // LDS-resident weights), so their latency hides behind the current block's MFMAs
+    auto lds_w = [&](int k0, float4* wl) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) wl[qq] = W.w2[(((k0 - REGK) / 4 + qq) * 4 + L.wave) * 64 + L.lane];
+    };
+    auto in_lds = [](int k0) { return k0 >= REGK && k0 < REGK + LDSK; };
+    float4 xn[NG], wn[4];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4) * C::H1B + rd]);
+    if (in_lds(0)) lds_w(0, wn);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       float4 xv[NG];
 #pragma unroll
-      for (int g = 0; g < NG; ++g) xv[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb) * C::H1B + rd]);
+      for (int g = 0; g < NG; ++g) xv[g] = xn[g];
+      if (kb + 1 < 4)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb + 1) * C::H1B + rd]);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int k0 = 64 * kb + 16 * v;  // a 16-row block lies in one residence region
         float4 wl[4];
         float wg[16];
-        if (k0 >= REGK && k0 < REGK + LDSK) {
+        if (in_lds(k0)) {
 #pragma unroll
-          for (int qq = 0; qq < 4; ++qq) wl[qq] = W.w2[(((k0 - REGK) / 4 + qq) * 4 + L.wave) * 64 + L.lane];
+          for (int qq = 0; qq < 4; ++qq) wl[qq] = wn[qq];
+          if (in_lds(k0 + 16)) lds_w(k0 + 16, wn);
         } else if (k0 >= REGK + LDSK) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) wg[q] = W2g[(k0 + q) * 256 + 64 * L.wave + L.lane];
         }
+        if (!in_lds(k0) && in_lds(k0 + 16)) lds_w(k0 + 16, wn);
         static_for<16>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
           const int k = k0 + q;
@@ -542,8 +558,8 @@ struct RoSlotRegs {
   }
 };
 
-// Wave 0, lane c (< SL): after s' = f(s, a) of slot c: state + next actor input, the trajectory
-// stores of (a_t, s_{t+1}), and the end of the episode (status, slot refill).
+// Wave 0, lane c (< SL): after s' = f(s, a) of slot c (already in the slot's LDS state): the
+// trajectory stores of (a_t, s_{t+1}) and the end of the episode (status; the caller refills).
 template <int NJ, int NG>
 __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* sn, const float* a,
                                            RoShared<NJ, NG>& Sh, const SysDevice& sd, int T,
@@ -553,10 +569,7 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
   const cacto_sys_params& p = sd.p;
   bool bad = false;
 #pragma unroll
-  for (int i = 0; i < ns; ++i) {
-    Sh.sS[c * ns + i] = sn[i];
-    bad |= isnan(sn[i]);
-  }
+  for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
   if (Atraj)
 #pragma unroll
     for (int i = 0; i < na; ++i) Atraj[((size_t)b * T + tc) * na + i] = a[i];
@@ -571,11 +584,7 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
       for (int i = 0; i < ns; ++i) Straj[((size_t)b * (T + 1) + t) * ns + i] = __builtin_nan("");
   }
   const bool fin = bad || tc + 1 >= n;
-  if (fin) {
-    if (status) status[b] = bad ? 1 : 0;
-  } else {
-    Sh.st[c] = tc + 1;
-  }
+  if (fin && status) status[b] = bad ? 1 : 0;
   return fin;
 }
 
@@ -657,11 +666,10 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
     RSTAMP(2);
     if (L.wave == 0) {
       bool fin = false;
+      float a[na];
       if (active) {
-        const int b = sr.b, tc = sr.t;
         double ad[na], sn[ns];
         const double* s = sr.s;
-        float a[na];
 #pragma unroll
         for (int i = 0; i < na; ++i) {
           a[i] = use_actor ? Sh.W.a[c * na + i] : 0.f;
@@ -682,18 +690,25 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
           env_simulate<NJ>(sd, s, ad, false, sn);
         }
         RSTAMP(6);
-        fin = ro_advance<NJ, NG>(c, b, tc, sn, a, Sh, sd, T, Straj, Atraj, status, nrm, sr.n);
 #pragma unroll
-        for (int i = 0; i < ns; ++i) sr.s[i] = sn[i];
-        sr.t = tc + 1;
+        for (int i = 0; i < ns; ++i) {
+          Sh.sS[c * ns + i] = sn[i];
+          sr.s[i] = sn[i];
+        }
+      }
+      // next actor input from s_{t+1}, first: the slots' lanes wrote sS above, and LDS operations of
+      // one wave complete in order, so after this wave-scope fence every lane reads them. The
+      // stores and the bookkeeping below overlap its latency; a slot that ends and is refilled gets
+      // its new s_0 row from ro_refill afterwards (same wave, later in program order).
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      x0l.write(Sh, nrm, L.lane);
+      if (active) {
+        fin = ro_advance<NJ, NG>(c, sr.b, sr.t, sr.s, a, Sh, sd, T, Straj, Atraj, status, nrm, sr.n);
+        sr.t += 1;
         RSTAMP(7);
       }
       ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L);
       if (fin) sr.load(Sh, c, cdyn);  // the slot's next episode (or none), written by this lane
-      // next actor input from s_{t+1} (or a refilled s_0): the slots' lanes wrote sS above; LDS
-      // operations of one wave complete in order, so after this wave-scope fence every lane reads them
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      x0l.write(Sh, nrm, L.lane);
       const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
       if (L.lane == 0) Sh.anyact = m != 0;
       RSTAMP(8);
