@@ -66,7 +66,7 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic(kernel="k_rollout<2,"):
+def pmc_traffic(kernel=("k_rollout_tt<2>", "k_rollout<2,")):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summaries
     (profiles/rNN_pmc_{fetch,write}.csv, made by tools/prof_summary.py from separate --pmc
     FETCH_SIZE / WRITE_SIZE passes). gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE
@@ -79,11 +79,16 @@ def pmc_traffic(kernel="k_rollout<2,"):
     if not fetch or not write:
         return None, None
 
+    kernels = (kernel,) if isinstance(kernel, str) else kernel
+
     def mean(path, counter):
+        # the first of `kernels` the summary holds: the double integrator's sequential pass at its
+        # bench schedule (k_rollout_tt<2> since round 3, k_rollout<2, 2> before)
         with open(path) as f:
-            for row in csv.DictReader(f):
-                # k_rollout<NJ, NG>: the double integrator's sequential pass at its bench schedule
-                if row["kernel"].replace(" ", "").startswith(kernel) and row["counter"] == counter:
+            rows = list(csv.DictReader(f))
+        for k in kernels:
+            for row in rows:
+                if row["kernel"].replace(" ", "").startswith(k) and row["counter"] == counter:
                     return float(row["mean"])
         return None
     fk, wk = mean(fetch[-1], "FETCH_SIZE"), mean(write[-1], "WRITE_SIZE")
@@ -754,7 +759,8 @@ def main():
                        "parallelism": "dp%d" % world},
             "segments": roll["segments"],
             "long_region": roll["long_region"],
-            "roofline": {"kernel": "k_rollout", "bound": "mfma", "achieved": achieved / 1e12,
+            "roofline": {"kernel": "k_rollout (k_rollout_tt<2>: two 4-slot teams per workgroup at this schedule)",
+                         "bound": "mfma", "achieved": achieved / 1e12,
                          "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                          "kernel_ms": roll["seq_kernel_ms"], "flop_per_env_step": fa_flops(ns, na),

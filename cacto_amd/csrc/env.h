@@ -806,9 +806,8 @@ __device__ __forceinline__ double soft_term(double alpha, double e) { return log
 // u_cost = a.a (the bound term only enters reward_batch's float32 part).
 template <int NJ>
 __device__ inline double ur5_reward(const SysDevice& sd, const double* w, const double* s, const double* a,
-                                    bool f32state) {
+                                    bool f32state, const V3& e) {
   const cacto_sys_params& p = sd.p;
-  const V3 e = env_ee<NJ>(sd, s);
   const double* o = p.obs;
   double ell[3];
   for (int k = 0; k < 3; ++k) {
@@ -864,13 +863,14 @@ __device__ inline double carpark_reward(const cacto_sys_params& p, const double*
   return p.scale * r;
 }
 
+// Env.reward with the end-effector position e = EE(s) already evaluated (a caller that also
+// records EE(s) computes the forward kinematics once).
 template <int NJ>
-__device__ inline double env_reward(const SysDevice& sd, const double* w, const double* s, const double* a,
-                                    bool f32state) {
+__device__ inline double env_reward_at(const SysDevice& sd, const double* w, const double* s, const double* a,
+                                       bool f32state, const V3& e) {
   constexpr int NA = NJ > 0 ? NJ : 2;
   const cacto_sys_params& p = sd.p;
-  if (p.reward_kind == CACTO_REW_UR5) return ur5_reward<NJ>(sd, w, s, a, f32state);
-  const V3 e = env_ee<NJ>(sd, s);
+  if (p.reward_kind == CACTO_REW_UR5) return ur5_reward<NJ>(sd, w, s, a, f32state, e);
   const double x = e.x, y = e.y;
   const double* o = p.obs;
   const double ell1 = ell_cost(p, x, y, o[0], o[1], o[6], o[7]);
@@ -912,6 +912,12 @@ __device__ inline double env_reward(const SysDevice& sd, const double* w, const 
   }
   r = r - w[3] * ell1 - w[4] * ell2 - w[5] * ell3 - w[6] * u_cost + p.offset;
   return p.scale * r;
+}
+
+template <int NJ>
+__device__ inline double env_reward(const SysDevice& sd, const double* w, const double* s, const double* a,
+                                    bool f32state) {
+  return env_reward_at<NJ>(sd, w, s, a, f32state, env_ee<NJ>(sd, s));
 }
 
 // reward_batch's TF float32 part and its tape gradient (environment.py:282-286 and the dr_da tape

@@ -19,6 +19,7 @@
 // 4 accumulator registers. Layer-2 rows stay in registers for the whole launch (weight
 // stationary) or in LDS (RoSplit); the 256 -> na output layer is a VALU dot product + lane
 // reduction. Numerics: every dot product is an f32 FMA chain (MFMA) — F32 tolerance as before.
+#include <cstdlib>
 #include <utility>
 
 #include "net_common.h"
@@ -132,9 +133,9 @@ __device__ __forceinline__ float add_from_above(float v, int off) {
 
 // Actor forward of the workgroup's SL slots: x0 -> h1 -> h2 -> a. Contains 3 barriers (the last
 // one publishes W.a).
-template <int NG, int NS, int NA, int REGK, int LDSK>
-__device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActorLds<NG, NA, LDSK>& W,
-                                         const float* __restrict__ W2g, const Lane& L, int it) {
+template <int NG, int NS, int NA, int REGK, int LDSK, bool PF, typename WT, typename Bar>
+__device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, WT& W, const float* __restrict__ W2g,
+                                         const Lane& L, int it, Bar&& bar) {
   using C = RoCfg<NG>;
   // ---- layer 1 (K = NS): one activation VGPR per group covers every k
   {
@@ -157,7 +158,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
 #pragma unroll
       for (int i = 0; i < 4; ++i) W.h1[(g * 4 + L.wave) * C::H1B + q * 20 + 4 * i + v] = lrelu(fadd(acc[g][i], R.b1));
   }
-  __syncthreads();
+  bar();
   RSTAMP(4);
   // ---- layer 2 (K = 256): k = 64 kb + 16 v + q; lane 4q+i reads {x[i][64kb + 16v + q], v = 0..3}
   {
@@ -165,39 +166,53 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[g][0] = acc[g][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int rd = (L.lane >> 2) * 20 + 4 * (L.lane & 3);
-    // LDS operands one step ahead (the next 64-k block's activations, the next 16-row block of
-    // LDS-resident weights), so their latency hides behind the current block's MFMAs
+    // PF: LDS operands one step ahead (the next 64-k block's activations, the next 16-row block of
+    // LDS-resident weights), so their latency hides behind the current block's MFMAs. Measured per
+    // system (r03): DI +2.5 %, car_park +2 %, manipulator -3 %, UR5 -20 % (its streamed rows and
+    // chain dynamics need the registers), so only the systems without streamed rows take it.
     auto lds_w = [&](int k0, float4* wl) {
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) wl[qq] = W.w2[(((k0 - REGK) / 4 + qq) * 4 + L.wave) * 64 + L.lane];
     };
     auto in_lds = [](int k0) { return k0 >= REGK && k0 < REGK + LDSK; };
     float4 xn[NG], wn[4];
+    if constexpr (PF) {
 #pragma unroll
-    for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4) * C::H1B + rd]);
-    if (in_lds(0)) lds_w(0, wn);
+      for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4) * C::H1B + rd]);
+      if (in_lds(0)) lds_w(0, wn);
+    }
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       float4 xv[NG];
+      if constexpr (PF) {
 #pragma unroll
-      for (int g = 0; g < NG; ++g) xv[g] = xn[g];
-      if (kb + 1 < 4)
+        for (int g = 0; g < NG; ++g) xv[g] = xn[g];
+        if (kb + 1 < 4)
 #pragma unroll
-        for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb + 1) * C::H1B + rd]);
+          for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb + 1) * C::H1B + rd]);
+      } else {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) xv[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb) * C::H1B + rd]);
+      }
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int k0 = 64 * kb + 16 * v;  // a 16-row block lies in one residence region
         float4 wl[4];
         float wg[16];
         if (in_lds(k0)) {
+          if constexpr (PF) {
 #pragma unroll
-          for (int qq = 0; qq < 4; ++qq) wl[qq] = wn[qq];
-          if (in_lds(k0 + 16)) lds_w(k0 + 16, wn);
+            for (int qq = 0; qq < 4; ++qq) wl[qq] = wn[qq];
+            if (in_lds(k0 + 16)) lds_w(k0 + 16, wn);
+          } else {
+            lds_w(k0, wl);
+          }
         } else if (k0 >= REGK + LDSK) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) wg[q] = W2g[(k0 + q) * 256 + 64 * L.wave + L.lane];
         }
-        if (!in_lds(k0) && in_lds(k0 + 16)) lds_w(k0 + 16, wn);
+        if constexpr (PF)
+          if (!in_lds(k0) && in_lds(k0 + 16)) lds_w(k0 + 16, wn);
         static_for<16>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
           const int k = k0 + q;
@@ -214,7 +229,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
       for (int i = 0; i < 4; ++i)
         W.h2[(4 * g + i) * C::H2S + f] = lrelu(fadd(fadd(acc[g][0][i], acc[g][1][i]), R.b2));
   }
-  __syncthreads();
+  bar();
   RSTAMP(5);
   // ---- layer 3 (256 -> NA): one summation order for every NG (so the schedule never changes a
   //      result): 64 partial chains, chain j = features j, j + 64, j + 128, j + 192 (FMA in that
@@ -250,7 +265,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, RoActor
 #pragma unroll
       for (int a = 0; a < NA; ++a) W.a[s * NA + a] = fadd(pa[a][0], W.b3[a]);
   }
-  __syncthreads();
+  bar();
 }
 
 // Chain dynamics workspace of the rollout, structure of arrays [joint][component][slot] (slot
@@ -472,12 +487,12 @@ struct RoX0Lane {
 // Slot refill (wave 0; every lane calls it, lanes with `need` take the next queue entries in lane
 // order). A new episode's s_0 goes to the slot's state and the actor input; episodes of length 0
 // are completed on the spot (status 0: RL.py never rolls out NSTEPS_SH == 0).
-template <int NJ, int NG>
-__device__ __forceinline__ void ro_refill(bool need, int c, int& head, RoShared<NJ, NG>& Sh, const SysDevice& sd,
+template <int NJ, int NG, typename ShT, bool INIT_CD = true>
+__device__ __forceinline__ void ro_refill(bool need, int c, int& head, ShT& Sh, const SysDevice& sd,
                                           const double* __restrict__ S0,
                                           const int32_t* __restrict__ nsteps, const int32_t* __restrict__ order, int T,
                                           int B, int G, double* __restrict__ Straj, int32_t* __restrict__ status,
-                                          const RoNorm<Dims<NJ>::NS>& nrm, const Lane& L) {
+                                          const RoNorm<Dims<NJ>::NS>& nrm, const Lane& L, int vb) {
   constexpr int ns = Dims<NJ>::NS, SL = RoCfg<NG>::SL;
   const cacto_sys_params& p = sd.p;
   while (true) {
@@ -487,7 +502,7 @@ __device__ __forceinline__ void ro_refill(bool need, int c, int& head, RoShared<
     const int k = head + rank;
     head += __popcll(m);
     if (need) {
-      const int r = k * G + ((k & 1) ? G - 1 - (int)blockIdx.x : (int)blockIdx.x);
+      const int r = k * G + ((k & 1) ? G - 1 - vb : vb);
       if (r >= B) {
         need = false;
         Sh.sact[c] = 0;
@@ -512,7 +527,7 @@ __device__ __forceinline__ void ro_refill(bool need, int c, int& head, RoShared<
           for (int i = 0; i < ns; ++i) Sh.sS[c * ns + i] = s[i];
 #pragma unroll
           for (int q = 0; q < ns; ++q) Sh.W.x0[(c >> 2) * 64 + 4 * q + (c & 3)] = nrm(q, (float)s[q]);
-          if constexpr (RoConstDyn<NJ>::ok) {
+          if constexpr (RoConstDyn<NJ>::ok && INIT_CD) {
             if (p.const_dyn) {
               // prismatic chain: M factored once per episode, kept in the slot's MS / hS
               ConstDyn<NJ> cd;
@@ -539,7 +554,8 @@ struct RoSlotRegs {
   int b = 0, t = 0, n = 0;
   double s[ns];
   ConstDyn<NJ> cd;
-  __device__ __forceinline__ void load(const RoShared<NJ, NG>& Sh, int c, bool cdyn) {
+  template <typename ShT>
+  __device__ __forceinline__ void load(const ShT& Sh, int c, bool cdyn) {
     if (c >= SL) return;
     act = Sh.sact[c] != 0;
     b = Sh.sb[c];
@@ -562,7 +578,7 @@ struct RoSlotRegs {
 // trajectory stores of (a_t, s_{t+1}) and the end of the episode (status; the caller refills).
 template <int NJ, int NG>
 __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* sn, const float* a,
-                                           RoShared<NJ, NG>& Sh, const SysDevice& sd, int T,
+                                           const SysDevice& sd, int T,
                                            double* __restrict__ Straj, float* __restrict__ Atraj,
                                            int32_t* __restrict__ status, const RoNorm<Dims<NJ>::NS>& nrm, int n) {
   constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
@@ -624,7 +640,8 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   int head = 0;  // queue position (wave 0, uniform)
   const RoNorm<ns> nrm(p);
   if (L.wave == 0) {
-    ro_refill<NJ, NG>(L.lane < SL, L.lane, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L);
+    ro_refill<NJ, NG>(L.lane < SL, L.lane, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L,
+                      (int)blockIdx.x);
     const uint64_t m = __ballot(L.lane < SL && Sh.sact[L.lane]);
     if (L.lane == 0) Sh.anyact = m != 0;
   }
@@ -646,7 +663,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (!use_actor) __syncthreads();
       }
     }
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK>(R, Sh.W, W2g, L, it);
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
     RSTAMP(1);
     const bool active = L.lane < SL && (L.wave == 0 ? sr.act : Sh.sact[c] != 0);
     if (split_dyn) {
@@ -696,19 +713,28 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
           sr.s[i] = sn[i];
         }
       }
-      // next actor input from s_{t+1}, first: the slots' lanes wrote sS above, and LDS operations of
-      // one wave complete in order, so after this wave-scope fence every lane reads them. The
-      // stores and the bookkeeping below overlap its latency; a slot that ends and is refilled gets
-      // its new s_0 row from ro_refill afterwards (same wave, later in program order).
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      x0l.write(Sh, nrm, L.lane);
+      // The next actor input from s_{t+1}: the slots' lanes wrote sS above, and LDS operations of
+      // one wave complete in order, so after the wave-scope fence every lane reads them. EARLY
+      // (revolute chains): written before the trajectory stores and the bookkeeping, which then
+      // overlap its latency; a slot that ends and is refilled gets its new s_0 row from ro_refill
+      // afterwards (same wave, later in program order). Measured per system (r03): UR5 +2.7 %,
+      // manipulator neutral, car_park -4.5 %, DI neutral — the others write it last.
+      constexpr bool EARLY = NJ >= 3;
+      if constexpr (EARLY) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        x0l.write(Sh, nrm, L.lane);
+      }
       if (active) {
-        fin = ro_advance<NJ, NG>(c, sr.b, sr.t, sr.s, a, Sh, sd, T, Straj, Atraj, status, nrm, sr.n);
+        fin = ro_advance<NJ, NG>(c, sr.b, sr.t, sr.s, a, sd, T, Straj, Atraj, status, nrm, sr.n);
         sr.t += 1;
         RSTAMP(7);
       }
-      ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L);
+      ro_refill<NJ, NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L, (int)blockIdx.x);
       if (fin) sr.load(Sh, c, cdyn);  // the slot's next episode (or none), written by this lane
+      if constexpr (!EARLY) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        x0l.write(Sh, nrm, L.lane);
+      }
       const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
       if (L.lane == 0) Sh.anyact = m != 0;
       RSTAMP(8);
@@ -718,12 +744,203 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   }
 }
 
+// ---------------------------------------------------------------- two teams per workgroup
+// The same per-step pipeline for the systems whose dynamics need no workgroup (no chain with
+// configuration-dependent M: SI, car, car_park, the prismatic DI) run as TWO independent teams of
+// 4 waves (4 episode slots each) in one 8-wave workgroup: two waves per SIMD, so while one team is
+// in its non-MFMA phases (layer 1's epilogue, layer 3, the dynamics on its wave 0, the stores and
+// refill) the other team's layer-2 MFMAs keep the matrix cores busy. The teams share the LDS-resident
+// layer-2 weight rows (RoSplitTT: 128 rows in registers — a wave has 256 of them at two waves per
+// SIMD — and 128 in LDS) and synchronise with team barriers (an LDS arrival counter), never with
+// the workgroup barrier. Each team is a "virtual workgroup" of the snake dealing (vb = 2 b + team,
+// G = 2 x workgroups); per-slot arithmetic is the single-team kernel's, so results are identical.
+struct RoSplitTT {
+  static constexpr int REGK = 128, LDSK = 128;
+};
+
+template <int NA>
+struct RoTeamActorLds {
+  static constexpr int SL = 4;
+  float h1[4 * RoCfg<1>::H1B];
+  float h2[SL * RoCfg<1>::H2S];
+  float x0[64];
+  float a[SL * NA];
+};
+
+template <int NJ>
+struct RoTeamShared {
+  static constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA, SL = 4;
+  RoTeamActorLds<na> W;
+  double sS[SL * ns];
+  double MS[NJ > 0 ? SL * NJ * NJ : 1], hS[NJ > 0 ? SL * NJ : 1];
+  int sb[SL], sn[SL], st[SL], sact[SL];
+  int anyact;
+  int bar;  // team barrier: arrivals
+};
+
+template <int NJ>
+struct RoTTShared {
+  static constexpr int na = Dims<NJ>::NA;
+  float4 w2[RoSplitTT::LDSK / 4 * 4 * 64];
+  float w3[na * 256];
+  float b3[8];
+  RoTeamShared<NJ> team[2];
+};
+
+// ro_actor's view of a team: the shared weights + the team's activations
+template <int NA>
+struct RoTeamView {
+  const float4* w2;
+  const float* w3;
+  const float* b3;
+  float* h1;
+  float* h2;
+  float* x0;
+  float* a;
+};
+
+// Barrier of the 4 waves of a team: each wave's lane 0 adds one arrival (release: the wave's LDS
+// writes are complete), the wave then waits for 4 arrivals per barrier so far (acquire).
+struct RoTeamBar {
+  int* ctr;
+  int target;
+  int lane;
+  __device__ __forceinline__ void operator()() {
+    target += 4;
+    if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+      __builtin_amdgcn_s_sleep(1);
+  }
+};
+
+template <int NJ>
+__global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
+    k_rollout_tt(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
+                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
+                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA, NG = 1, SL = 4;
+  constexpr int REGK = RoSplitTT::REGK, LDSK = RoSplitTT::LDSK;
+  __shared__ RoTTShared<NJ> Sh;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const int team = threadIdx.x >> 8;
+  Lane L;
+  // team-local wave (team 1's wave 0 is the workgroup's wave 7: the two teams' dynamics waves sit
+  // on different SIMDs) and thread index
+  L.wave = (L.wave + team) & 3;
+  L.tid = L.wave * 64 + L.lane;
+  RoTeamShared<NJ>& S = Sh.team[team];
+  RoActorRegs<ns, REGK> R;
+  if (use_actor) {
+    const float* W1 = N.flat + N.t.woff[0];
+    const float* W2 = N.flat + N.t.woff[1];
+    const float* W3 = N.flat + N.t.woff[2];
+    const int f = 64 * L.wave + L.lane;
+#pragma unroll
+    for (int k = 0; k < REGK; ++k) R.w2[k] = W2[k * 256 + f];
+#pragma unroll
+    for (int q = 0; q < ns; ++q) R.w1[q] = W1[q * 256 + f];
+    R.b1 = N.bias(0, f);
+    R.b2 = N.bias(1, f);
+    for (int e = threadIdx.x; e < LDSK * 64; e += 2 * CACTO_THREADS) {
+      const int lane = e & 63, w = (e >> 6) & 3, kq = e >> 8;
+      const int k = REGK + 4 * kq, col = 64 * w + lane;
+      Sh.w2[e] = make_float4(W2[k * 256 + col], W2[(k + 1) * 256 + col], W2[(k + 2) * 256 + col],
+                             W2[(k + 3) * 256 + col]);
+    }
+    for (int e = threadIdx.x; e < na * 256; e += 2 * CACTO_THREADS) Sh.w3[e] = W3[(e & 255) * na + (e >> 8)];
+    if (threadIdx.x < 8) Sh.b3[threadIdx.x] = threadIdx.x < na ? N.bias(2, threadIdx.x) : 0.f;
+  }
+  if (L.tid < 64) S.W.x0[L.tid] = 0.f;
+  for (int e = L.tid; e < SL * ns; e += CACTO_THREADS) S.sS[e] = 0.0;
+  if (L.tid < SL) S.sact[L.tid] = 0;
+  if (L.tid == 0) S.bar = 0;
+  __syncthreads();  // the only workgroup barrier: weights and team state in place
+  RoTeamBar tbar{&S.bar, 0, L.lane};
+  const int vb = 2 * (int)blockIdx.x + team, G = 2 * (int)gridDim.x;
+  int head = 0;
+  const RoNorm<ns> nrm(p);
+  const int c = L.lane % SL;
+  // prismatic chains (the host runs this kernel for const_dyn chains only): M's Cholesky factor
+  // and h do not depend on (q, v) — the values k_const_dyn_init tabled in SysDevice, computed by
+  // the same chain_terms -> cholesky the single-team kernel runs per episode
+  ConstDyn<NJ> cd;
+  if constexpr (NJ > 0) {
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = sd.cd_L[k];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) cd.h[i] = sd.cd_h[i];
+  }
+  RoSlotRegs<NJ, NG> sr;
+  if (L.wave == 0) {
+    ro_refill<NJ, NG, RoTeamShared<NJ>, false>(L.lane < SL, L.lane, head, S, sd, S0, nsteps, order, T, B, G, Straj,
+                                                status, nrm, L, vb);
+    const uint64_t m = __ballot(L.lane < SL && S.sact[L.lane]);
+    if (L.lane == 0) S.anyact = m != 0;
+    sr.load(S, c, false);
+  }
+  tbar();
+  const RoX0Lane<ns, SL> x0l(nrm, L.lane);
+  RoTeamView<na> V{Sh.w2, Sh.w3, Sh.b3, S.W.h1, S.W.h2, S.W.x0, S.W.a};
+  const float* W2g = N.flat + N.t.woff[1];
+#ifdef CACTO_STAMPS
+#define TSTAMP(k)                                                                                          \
+  do {                                                                                                     \
+    if (blockIdx.x == 0 && L.wave == 0 && L.lane == 0 && it == 20) g_rstamps[8 * team + k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+  for (int it = 0; S.anyact; ++it) {
+    TSTAMP(0);
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true>(R, V, W2g, L, it, tbar);
+    TSTAMP(1);
+    if (L.wave == 0) {
+      const bool active = L.lane < SL && sr.act;
+      bool fin = false;
+      float a[na];
+      if (active) {
+        double ad[na], sn[ns];
+#pragma unroll
+        for (int i = 0; i < na; ++i) {
+          a[i] = use_actor ? S.W.a[c * na + i] : 0.f;
+          ad[i] = (double)a[i];
+        }
+        if constexpr (NJ > 0)
+          env_simulate_const<NJ>(sd, cd, sr.s, ad, sn);
+        else
+          env_simulate<NJ>(sd, sr.s, ad, false, sn);
+#pragma unroll
+        for (int i = 0; i < ns; ++i) {
+          S.sS[c * ns + i] = sn[i];
+          sr.s[i] = sn[i];
+        }
+        fin = ro_advance<NJ, NG>(c, sr.b, sr.t, sr.s, a, sd, T, Straj, Atraj, status, nrm, sr.n);
+        sr.t += 1;
+      }
+      ro_refill<NJ, NG, RoTeamShared<NJ>, false>(fin, c, head, S, sd, S0, nsteps, order, T, B, G, Straj, status, nrm,
+                                                  L, vb);
+      if (fin) sr.load(S, c, false);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      x0l.write(S, nrm, L.lane);
+      const uint64_t m = __ballot(L.lane < SL && S.sact[c]);
+      if (L.lane == 0) S.anyact = m != 0;
+      TSTAMP(2);
+    }
+    tbar();
+    TSTAMP(3);
+  }
+#undef TSTAMP
+}
+
 // Rewards and end-effector positions of every recorded step (Env.step's reward and
 // get_end_effector_position, environment.py:70-78, :146-156): one thread per (episode, t),
 // r_t = reward(w, s_t, a_t) for t < n, EE_t = EE(s_t) for t <= n; NaN states (a dropped episode)
 // are skipped.
 template <int NJ>
-__global__ void __launch_bounds__(256) k_rollout_rewards(const SysDevice* __restrict__ sdp, const double* __restrict__ Straj,
+__global__ void __launch_bounds__(256, 4) k_rollout_rewards(const SysDevice* __restrict__ sdp, const double* __restrict__ Straj,
                                                          const float* __restrict__ Atraj, const int32_t* __restrict__ nsteps,
                                                          int T, int use_actor, const double* __restrict__ Wext,
                                                          double* __restrict__ Rtraj, double* __restrict__ EEtraj, int B) {
@@ -745,8 +962,8 @@ __global__ void __launch_bounds__(256) k_rollout_rewards(const SysDevice* __rest
       bad |= isnan(s[i]);
     }
     if (bad) continue;
+    const V3 v = env_ee<NJ>(sd, s);  // once, for the EE row and the reward
     if (EEtraj) {
-      const V3 v = env_ee<NJ>(sd, s);
       EEtraj[(size_t)e * 3 + 0] = v.x;
       EEtraj[(size_t)e * 3 + 1] = v.y;
       EEtraj[(size_t)e * 3 + 2] = v.z;
@@ -755,7 +972,7 @@ __global__ void __launch_bounds__(256) k_rollout_rewards(const SysDevice* __rest
       double a[na];
 #pragma unroll
       for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)Atraj[((size_t)b * T + t) * na + i] : 0.0;
-      Rtraj[(size_t)b * T + t] = env_reward<NJ>(sd, w, s, a, false);
+      Rtraj[(size_t)b * T + t] = env_reward_at<NJ>(sd, w, s, a, false, v);
     }
   }
 }
@@ -798,6 +1015,28 @@ struct LaunchRollout {
                  const double* W, double* S, float* A, double* R, double* EE, int32_t* status, const int32_t* order,
                  int B, int groups, int wgs, hipStream_t st) {
     const int cus = ro_cus();
+    // two teams of 4 slots per workgroup (k_rollout_tt) for the systems whose step needs no
+    // workgroup-wide dynamics: automatically where the single-team kernel would take 2 groups,
+    // or on request (groups == -1)
+    constexpr bool tt_ok = NJ <= 2 && !(NJ > 0 && !RoConstDyn<NJ>::ok);
+    const bool tt_sys = tt_ok && (NJ <= 0 || sys->host.p.const_dyn);
+    // automatic only where it measured faster: the prismatic chain (DI 0.75 -> 0.72 ms at 4096
+    // episodes); car_park's step was slower on two teams (0.42 -> 0.50 ms)
+    const bool tt_auto = tt_sys && NJ > 0;
+    if (groups == -1 && !tt_sys) {
+      set_error("cacto_rollout_sched: groups -1 (two teams) needs a system without configuration-dependent M");
+      return CACTO_EINVAL;
+    }
+    if (tt_sys && (groups == -1 || (tt_auto && groups == 0 && B / (2 * 4 * cus) == 2))) {
+      if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
+      wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
+      if constexpr (tt_ok)
+        hipLaunchKernelGGL(k_rollout_tt<NJ>, dim3(wgs), dim3(2 * CACTO_THREADS), 0, st, sys->dev, v, S0, n, T,
+                           use_actor, S, A, status, order, B);
+      CACTO_CHECK_HIP(hipGetLastError());
+      if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
+      return CACTO_OK;
+    }
     // the float64 6-joint chain dynamics need the registers that more slots would take
     constexpr int gmax = 4;
     if (groups <= 0) {
@@ -850,7 +1089,8 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
                                    const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
-  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4, "cacto_rollout_sched: groups must be 0, 1, 2 or 4");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1,
+                "cacto_rollout_sched: groups must be 0, 1, 2, 4 or -1 (two teams)");
   CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
   CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
                 "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");

@@ -171,9 +171,14 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         self.random = py_random or random  # replay_buffer.py:150 uses the global `random`
 
     def _rows_added(self, start, n):
-        # leaves = max_priority ** alpha (replay_buffer.py:133-135), max_priority read on the device
-        L.lib().call("cacto_per_set_range_max", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.N, start, n,
-                     dptr(self.max_priority, torch.float64), self.alpha, stream())
+        # leaves = max_priority ** alpha (replay_buffer.py:133-135) with the host's Python float
+        # power, as the reference: the device pow can differ from libm's by an ulp once max_priority
+        # != 1, and the leaves feed the stratified sampling. One 8-byte read per add (adds happen
+        # once per episode batch, outside the update loop); cacto_per_set_range_max is the
+        # sync-free variant.
+        leaf = float(self.max_priority.item()) ** self.alpha
+        L.lib().call("cacto_per_set_range", dptr(self.sum_tree), dptr(self.min_tree), self.cap, self.N, start, n,
+                     leaf, stream())
 
     def sample_device(self, uniforms=None):
         """_sample_proportional + IS weights + exp_counter (replay_buffer.py:139-188)."""

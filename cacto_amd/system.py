@@ -44,15 +44,73 @@ _SHARED = {}
 
 
 def shared_system(conf):
-    """The System of a conf module, created once: the reference constructs `Environment(conf)`,
+    """The System of a conf module: the reference constructs `Environment(conf)`,
     `ReplayBuffer(conf)`, `NN(env, conf)` ... from the same conf (main.py:145-150), and they all
-    address one device copy of it (one `cacto_sys` handle)."""
+    address one device copy of it (one `cacto_sys` handle). The cache holds the System weakly (its
+    handle is destroyed once no Env / buffer / net uses it) and keys it by the conf's packed
+    numeric content as well as its identity: a conf module changed after a System was made from it
+    (dt, weights, norms, ...) gets a new System instead of silently reusing the stale one."""
+    import weakref
     key = id(conf)
+    fp = fingerprint(conf)
     hit = _SHARED.get(key)
-    if hit is None or hit[0] is not conf:
-        hit = (conf, System(conf))
-        _SHARED[key] = hit
-    return hit[1]
+    sysobj = hit[1]() if hit is not None and hit[0] is conf and hit[2] == fp else None
+    if sysobj is None:
+        sysobj = System(conf)
+        _SHARED[key] = (conf, weakref.ref(sysobj), fp)
+    return sysobj
+
+
+def fingerprint(conf):
+    """The bytes System(conf) hands the device: the packed parameters and the joint table."""
+    p, table = pack_params(conf)
+    return bytes(p) + (table.tobytes() if table is not None else b"")
+
+
+def pack_params(conf):
+    """conf module -> (cacto_sys_params, joint table or None), host only."""
+    p = L.SysParams()
+    sid = conf.system_id
+    robot = getattr(conf, "robot", None)
+    if sid == "single_integrator":
+        p.dyn_kind, p.reward_kind = L.CACTO_DYN_SINGLE_INTEGRATOR, L.CACTO_REW_PLANAR
+    elif sid == "car":
+        p.dyn_kind, p.reward_kind = L.CACTO_DYN_CAR, L.CACTO_REW_PLANAR
+    elif sid == "car_park":
+        p.dyn_kind, p.reward_kind = L.CACTO_DYN_CAR_PARK, L.CACTO_REW_CAR_PARK
+        p.L_delta, p.tau_delta, p.k_db = float(conf.L_delta), float(conf.tau_delta), float(conf.k_db)
+        cp = np.asarray(conf.check_points_BF, dtype=np.float64)
+        p.n_check = cp.shape[0]
+        _fill(p.check_points, cp.reshape(-1))
+    elif robot is not None and sid in ("double_integrator", "manipulator", "ur5"):
+        p.dyn_kind = L.CACTO_DYN_CHAIN
+        p.reward_kind = {"manipulator": L.CACTO_REW_MANIPULATOR, "ur5": L.CACTO_REW_UR5}.get(sid, L.CACTO_REW_PLANAR)
+    else:
+        raise NotImplementedError("system %r is not in this build's hot path" % sid)
+    p.nb_state, p.nb_action = conf.nb_state, conf.nb_action
+    p.nq = conf.nq or 0
+    p.nv = conf.nv or 0
+    p.normalize = int(conf.NORMALIZE_INPUTS)
+    p.n_weights = len(conf.cost_weights_running)
+    p.dt = conf.dt
+    _fill(p.state_norm, conf.state_norm_arr)
+    _fill(p.u_max, conf.u_max)
+    p.w_b = conf.w_b
+    p.offset, p.scale = float(conf.cost_funct_param[0]), float(conf.cost_funct_param[1])
+    p.alpha, p.alpha2 = float(conf.soft_max_param[0]), float(conf.soft_max_param[1])
+    _fill(p.obs, conf.obs_param)
+    _fill(p.target, conf.TARGET_STATE)
+    _fill(p.w_running, conf.cost_weights_running)
+    _fill(p.w_terminal, conf.cost_weights_terminal)
+    table = None
+    if robot is not None:
+        p.n_joints = robot.nq
+        p.ee_parent = robot.ee_parent
+        _fill(p.ee_R, np.asarray(robot.ee_R).reshape(-1))
+        _fill(p.ee_p, robot.ee_p)
+        _fill(p.gravity, robot.gravity)
+        table = np.ascontiguousarray(robot.table(), dtype=np.float64)
+    return p, table
 
 
 class System:
@@ -61,47 +119,7 @@ class System:
     def __init__(self, conf):
         require_gpu()
         self.conf = conf
-        p = L.SysParams()
-        sid = conf.system_id
-        robot = getattr(conf, "robot", None)
-        if sid == "single_integrator":
-            p.dyn_kind, p.reward_kind = L.CACTO_DYN_SINGLE_INTEGRATOR, L.CACTO_REW_PLANAR
-        elif sid == "car":
-            p.dyn_kind, p.reward_kind = L.CACTO_DYN_CAR, L.CACTO_REW_PLANAR
-        elif sid == "car_park":
-            p.dyn_kind, p.reward_kind = L.CACTO_DYN_CAR_PARK, L.CACTO_REW_CAR_PARK
-            p.L_delta, p.tau_delta, p.k_db = float(conf.L_delta), float(conf.tau_delta), float(conf.k_db)
-            cp = np.asarray(conf.check_points_BF, dtype=np.float64)
-            p.n_check = cp.shape[0]
-            _fill(p.check_points, cp.reshape(-1))
-        elif robot is not None and sid in ("double_integrator", "manipulator", "ur5"):
-            p.dyn_kind = L.CACTO_DYN_CHAIN
-            p.reward_kind = {"manipulator": L.CACTO_REW_MANIPULATOR, "ur5": L.CACTO_REW_UR5}.get(sid, L.CACTO_REW_PLANAR)
-        else:
-            raise NotImplementedError("system %r is not in this build's hot path" % sid)
-        p.nb_state, p.nb_action = conf.nb_state, conf.nb_action
-        p.nq = conf.nq or 0
-        p.nv = conf.nv or 0
-        p.normalize = int(conf.NORMALIZE_INPUTS)
-        p.n_weights = len(conf.cost_weights_running)
-        p.dt = conf.dt
-        _fill(p.state_norm, conf.state_norm_arr)
-        _fill(p.u_max, conf.u_max)
-        p.w_b = conf.w_b
-        p.offset, p.scale = float(conf.cost_funct_param[0]), float(conf.cost_funct_param[1])
-        p.alpha, p.alpha2 = float(conf.soft_max_param[0]), float(conf.soft_max_param[1])
-        _fill(p.obs, conf.obs_param)
-        _fill(p.target, conf.TARGET_STATE)
-        _fill(p.w_running, conf.cost_weights_running)
-        _fill(p.w_terminal, conf.cost_weights_terminal)
-        table = None
-        if robot is not None:
-            p.n_joints = robot.nq
-            p.ee_parent = robot.ee_parent
-            _fill(p.ee_R, np.asarray(robot.ee_R).reshape(-1))
-            _fill(p.ee_p, robot.ee_p)
-            _fill(p.gravity, robot.gravity)
-            table = np.ascontiguousarray(robot.table(), dtype=np.float64)
+        p, table = pack_params(conf)
         self.params = p
         self._table = table
         h = C.c_void_p()

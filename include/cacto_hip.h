@@ -299,8 +299,11 @@ int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const doubl
                   int32_t* status_d, const int32_t* order_d, int B, void* stream);
 
 /* cacto_rollout with an explicit schedule: `groups` 4-episode groups per workgroup (1, 2 or 4;
- * 0 = automatic: about two episodes per slot) and `workgroups` (0 = one per CU, capped by B).
- * Same outputs as cacto_rollout for any schedule (tests use it to force slot refills). */
+ * 0 = automatic: about two episodes per slot; -1 = two independent 4-slot teams per 8-wave
+ * workgroup, for systems whose step needs no workgroup-wide dynamics — SI, car, car_park and the
+ * prismatic DI — chosen automatically for DI where it would take 2 groups) and `workgroups`
+ * (0 = one per CU, capped by B). Same outputs as cacto_rollout for any schedule (tests use it to
+ * force slot refills and to compare the kernels). */
 int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
                         const int32_t* nsteps_d, int T, int use_actor, const double* W_d,
                         double* S_traj_d, float* A_traj_d, double* R_traj_d, double* EE_traj_d,
@@ -367,7 +370,9 @@ int cacto_per_init(double* sum_tree_d, double* min_tree_d, int64_t capacity, voi
 int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
                         int64_t start, int64_t n, double value, void* stream);
 /* The same with the value max_priority_d[0] ** alpha read on the device (what ReplayBuffer.add sets new
- * leaves to, replay_buffer.py:133-135), so adding episodes needs no host read of max_priority. */
+ * leaves to, replay_buffer.py:133-135), so adding episodes needs no host read of max_priority. The
+ * device pow may differ from the host libm pow the reference uses by an ulp; the Python layer
+ * computes the power on the host and calls cacto_per_set_range. */
 int cacto_per_set_range_max(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
                             int64_t start, int64_t n, const double* max_priority_d, double alpha, void* stream);
 /* Stratified proportional sampling (replay_buffer.py:139-188). uniforms_d [B] = random.random()

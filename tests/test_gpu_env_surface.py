@@ -71,3 +71,24 @@ def test_bound_control_cost(system):
     ref = np.array([oe.bound_control_cost(a) for a in A])
     np.testing.assert_allclose(got, ref, rtol=1e-14, atol=0)
     assert env.bound_control_cost(A[5]) == got[5]
+
+
+def test_shared_system_follows_conf_changes():
+    """Objects built from one conf module share one System (one device copy); a conf changed after
+    that (here dt) gets a fresh System for the objects built afterwards, and the cache does not keep
+    a System alive on its own."""
+    import gc
+    import weakref
+    from cacto_amd.confs import load_conf
+    from cacto_amd.system import shared_system
+    conf = load_conf("double_integrator", fresh=True)
+    a = shared_system(conf)
+    assert shared_system(conf) is a
+    conf.dt = conf.dt * 0.5
+    b = shared_system(conf)
+    assert b is not a and b.params.dt == conf.dt and a.params.dt == 2 * conf.dt
+    assert shared_system(conf) is b
+    ref = weakref.ref(b)
+    del b
+    gc.collect()
+    assert ref() is None

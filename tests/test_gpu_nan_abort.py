@@ -86,11 +86,12 @@ def setup():
     return conf, genv, oe, rl, S0, fail, stable
 
 
-def test_status_matches_oracle_under_refill(setup):
+@pytest.mark.parametrize("sched", [(1, 3), (-1, 2)])
+def test_status_matches_oracle_under_refill(setup, sched):
     conf, genv, oe, rl, S0, fail, stable = setup
     ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
     T = max(ns_)
-    got = rl.rollout_batch(S0, ns_, T, ep=1, sched=(1, 3))
+    got = rl.rollout_batch(S0, ns_, T, ep=1, sched=sched)
     st = got["status"].cpu().numpy()
     pinned = [k for k in range(len(S0)) if stable[k]]
     assert sum(fail[k] is not None for k in pinned) >= 6, "the construction must drop several episodes"
@@ -105,11 +106,12 @@ def test_status_matches_oracle_under_refill(setup):
             assert np.isnan(S[k, ns_[k]]).any()
 
 
-def test_kept_episodes_equal_a_clean_run(setup):
+@pytest.mark.parametrize("sched", [(1, 3), (-1, 2)])
+def test_kept_episodes_equal_a_clean_run(setup, sched):
     conf, genv, oe, rl, S0, fail, stable = setup
     ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
     T = max(ns_)
-    got = rl.rollout_batch(S0, ns_, T, ep=1, sched=(1, 3))
+    got = rl.rollout_batch(S0, ns_, T, ep=1, sched=sched)
     st = got["status"].cpu().numpy()
     keep = np.where(st == 0)[0]
     assert len(keep) >= 30

@@ -383,11 +383,15 @@ def test_rollout_per_step_consistency(system):
 
 
 @pytest.mark.parametrize("system,sched", [("double_integrator", (1, 3)), ("double_integrator", (2, 2)),
-                                          ("manipulator", (4, 1)), ("car_park", (1, 2)), ("ur5", (2, 1))])
+                                          ("manipulator", (4, 1)), ("car_park", (1, 2)), ("ur5", (2, 1)),
+                                          ("double_integrator", (-1, 2)), ("double_integrator", (-1, 1)),
+                                          ("car_park", (-1, 3))])
 def test_rollout_slot_refill_matches_one_episode_per_slot(system, sched):
     """Few workgroups force every slot to run several episodes back to back (refill at the step
     boundary, zero-length episodes completed on the spot); every episode must come out exactly as
-    in a schedule with one episode per slot, and agree with the oracle's step-by-step semantics."""
+    in a schedule with one episode per slot, and agree with the oracle's step-by-step semantics.
+    groups = -1: the two-team kernel (k_rollout_tt, two 4-slot teams per workgroup on team
+    barriers), against the single-team kernel's one-episode-per-slot schedule."""
     conf, genv, oe, nn, rl = _nets(system, None, seed=4)
     rng = random.Random(11)
     n_ep = 45
@@ -559,3 +563,43 @@ def test_per_update_priorities_matches_oracle():
         st = per.sum_tree.cpu().numpy()
         np.testing.assert_allclose(st[65536:65536 + 3000], o.it_sum.value[65536:65536 + 3000], rtol=1e-6)
         np.testing.assert_allclose(st[1], o.it_sum.value[1], rtol=1e-6)
+
+
+def test_per_new_leaves_after_priority_updates_match_host_pow():
+    """Rows added after priority updates (max_priority != 1) get leaves max_priority ** alpha
+    (replay_buffer.py:133-135, the host Python float power). The device computes the power in
+    float64: the leaves must equal the host's bit for bit, and the stratified indices drawn over
+    them must equal the oracle's."""
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    from cacto_amd.system import System
+    conf = load_conf("car_park")
+    per = PrioritizedReplayBuffer(conf, System(conf))
+    per.alpha = 0.6
+    o = obuf.PrioritizedReplayBuffer(conf.REPLAY_SIZE, conf.nb_state, 0.6, 0.6, conf.prioritized_replay_eps,
+                                     conf.fresh_factor, conf.BATCH_SIZE)
+    rng = np.random.default_rng(23)
+    cols = 3 * conf.nb_state + 3
+    rows = rng.normal(size=(2000, cols))
+    per.add_rows(rows)
+    o.add_rows(rows)
+    for it in range(4):
+        u = list(rng.uniform(size=conf.BATCH_SIZE))
+        idx, _ = per.sample_device(u)
+        oidx = o.sample_proportional(u)
+        np.testing.assert_array_equal(idx.cpu().numpy(), oidx)
+        o.sample_weights(oidx)                     # the IS weights step advances exp_counter
+        y = (rng.normal(size=(conf.BATCH_SIZE, 1)) * (3 + it)).astype(np.float32)
+        V = rng.normal(size=(conf.BATCH_SIZE, 1)).astype(np.float32)
+        per.update_priorities_device(idx, torch.as_tensor(y, device="cuda"), torch.as_tensor(V, device="cuda"))
+        o.update_priorities(oidx, y, V)
+        more = rng.normal(size=(300, cols))
+        n0 = per.next_idx
+        per.add_rows(more)
+        o.add_rows(more)
+        torch.cuda.synchronize()
+        maxp = float(per.max_priority.item())
+        assert maxp == o.max_priority and maxp != 1.0
+        leaves = per.sum_tree.cpu().numpy()[per.cap + n0:per.cap + n0 + 300]
+        assert (leaves == maxp ** 0.6).all(), (leaves[0], maxp ** 0.6)
+    u = list(rng.uniform(size=conf.BATCH_SIZE))
+    np.testing.assert_array_equal(per.sample_device(u)[0].cpu().numpy(), o.sample_proportional(u))

@@ -123,3 +123,47 @@ def test_rl_solve_add_per_leaves_get_max_priority():
     m = float(per.max_priority.item()) ** 0.6
     np.testing.assert_array_equal(leaves[:32], m)
     np.testing.assert_array_equal(leaves[32:], 0.0)
+
+
+@pytest.mark.parametrize("system", ["double_integrator", "manipulator", "car_park"])
+def test_rl_solve_env_rl_resimulates_on_device(system):
+    """RL_Solve with env_RL = 1 (RL.py:157-165): the episode is re-simulated from TO_controls —
+    s_{i+1}, r_i = Env.step(cost_weights_running, s_i, u_i), ee_{i+1} = EE(s_{i+1}),
+    r_T = reward(cost_weights_terminal, s_T) with action None — against the oracle env's step /
+    reward / EE loop (a closed-form chain, a revolute chain, car_park's check-point rewards); the
+    n-step targets then follow from those rewards as the reference computes them."""
+    import random
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.rl import RL_AC
+    from oracle import env as oenv
+    conf = load_conf(system, fresh=True)
+    conf.env_RL = 1
+    env = make_env(conf)
+    rl = RL_AC(env, NN(env, conf, w_S=0.0, seed=5), conf)
+    rl.setup_model()
+    oe = oenv.make_env(conf)
+    ICS = np.asarray(oe.reset(random.Random(3)), dtype=np.float64)
+    init, S_to, U_to, T, ok = rl.create_TO_init(1, ICS)
+    assert ok == 1 and T > 3
+    rng = np.random.default_rng(4)
+    U = rng.normal(size=U_to.shape) * 0.5 * np.asarray(conf.u_max, dtype=np.float64)[:U_to.shape[1]]
+    state_arr, partial, total, s_next, done, rwrd, term, ep_return, ee = rl.RL_Solve(U, S_to, np.zeros(T + 1))
+    s = ICS.copy()
+    S_ref, R_ref, EE_ref = [s], [], [oe.get_end_effector_position(s)]
+    for i in range(T):
+        s, r = oe.step(conf.cost_weights_running, s, U[i])
+        S_ref.append(s)
+        R_ref.append(r)
+        EE_ref.append(oe.get_end_effector_position(s))
+    R_ref.append(oe.reward(conf.cost_weights_terminal, s))
+    S_ref, R_ref, EE_ref = np.array(S_ref), np.array(R_ref), np.array(EE_ref)
+    np.testing.assert_allclose(state_arr, S_ref, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(rwrd, R_ref, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(ee, EE_ref, rtol=1e-12, atol=1e-12)
+    p, t, sn, d, tm = obuf.rl_solve(state_arr, -rwrd, conf.nsteps_TD_N, MC=bool(conf.MC))
+    np.testing.assert_array_equal(partial, p)
+    np.testing.assert_array_equal(total, t)
+    np.testing.assert_array_equal(s_next, sn)
+    np.testing.assert_array_equal(done, d)
+    assert ep_return == sum(rwrd)

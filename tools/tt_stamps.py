@@ -1,0 +1,36 @@
+"""Diagnostic: per-phase cycles of one step (step 20, workgroup 0) of each team of k_rollout_tt
+(CACTO_STAMPS build). Not part of the product path.
+    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/tt_stamps.py [system]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cacto_amd import _lib as L  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    system = sys.argv[1] if len(sys.argv) > 1 else "double_integrator"
+    conf, env, rl = bench.make_learner(system)
+    S0, n = bench.initial_states(env, conf, 4096, seed=0)
+    T = int(n.max())
+    inputs = rl.rollout_inputs(S0, n)
+    for _ in range(3):
+        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(-1, 0))
+    torch.cuda.synchronize()
+    st = (ctypes.c_ulonglong * 16)()
+    L.lib().dll.cacto_debug_rollout_stamps(st)
+    v = np.array(st[:16], dtype=np.float64)
+    for team in (0, 1):
+        t = v[8 * team: 8 * team + 4]
+        print(system, "team", team, "step %.0f: actor %.0f, dynamics+stores+refill %.0f, barrier %.0f"
+              % (t[3] - t[0], t[1] - t[0], t[2] - t[1], t[3] - t[2]), "(start offset vs team 0: %.0f)" % (t[0] - v[0]))
+    print("   team 0 actor: layer 1 %.0f, layer 2 %.0f, layer 3 %.0f" % (v[4] - v[0], v[5] - v[4], v[1] - v[5]))
+
+
+if __name__ == "__main__":
+    main()
