@@ -690,10 +690,70 @@ __device__ __forceinline__ void write_packed(float4* pk4, const NetTopo& t, int 
      (o & 3)] = val;
 }
 
+struct AdamScalars {
+  float alpha, c1, c2, eps, tau, omt;
+};
+
+__device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int32_t* step) {
+  const int it = step[a.which];  // = Keras iterations + 1
+  const int iters = it - 1;
+  double lr = a.lr[4];
+  for (int k = 0; k < 4; ++k)
+    if ((double)iters <= a.bounds[k]) {
+      lr = a.lr[k];
+      break;
+    }
+  const float tf = (float)it;
+  const float b1p = powf((float)a.beta1, tf), b2p = powf((float)a.beta2, tf);
+  AdamScalars s;
+  s.alpha = fdiv(fmul((float)lr, __fsqrt_rn(fsub(1.f, b2p))), fsub(1.f, b1p));
+  s.c1 = (float)(1.0 - a.beta1);
+  s.c2 = (float)(1.0 - a.beta2);
+  s.eps = (float)a.eps;
+  s.tau = (float)a.tau;
+  s.omt = (float)(1.0 - a.tau);
+  return s;
+}
+
+// NCH > 0: every chunk partial of a parameter is loaded at once (clamped, branch-free) together with
+// m, v, the weight and the target value, so a thread waits for one memory latency instead of one per
+// group of 8 chunks plus one per leftover chunk (B = 4096: 32 chunks, ~11 dependent rounds, 11 us);
+// the partials are still summed in chunk order (bit-identical). NCH = 0: any chunk count.
+template <int NCH>
 __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, int nch, NetTopo t, const float* src,
                                               float* netbuf, float4* packed, float* __restrict__ m, float* __restrict__ v,
                                               const int32_t* __restrict__ step, AdamArgs a, float* target,
                                               float4* target_packed) {
+  if constexpr (NCH > 0) {
+    const int p0 = blockIdx.x * blockDim.x + threadIdx.x;
+    float q[NCH], mm = 0.f, vv = 0.f, th0 = 0.f, tg0 = 0.f;
+    const int pc = min(p0, t.params - 1);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) q[k] = slab[(size_t)min(k, nch - 1) * t.params + pc];
+    mm = m[pc];
+    vv = v[pc];
+    th0 = src[pc];
+    if (a.soft) tg0 = target[pc];
+    const AdamScalars s = adam_scalars(a, step);
+    if (p0 >= t.params) return;
+    float g = q[0];
+#pragma unroll
+    for (int k = 1; k < NCH; ++k)
+      if (k < nch) g += q[k];
+    mm = fadd(mm, fmul(fsub(g, mm), s.c1));
+    vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
+    const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
+    m[p0] = mm;
+    v[p0] = vv;
+    netbuf[p0] = th;
+    write_packed(packed, t, p0, th);
+    if (a.soft) {
+      const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
+      target[p0] = tg;
+      write_packed(target_packed, t, p0, tg);
+    }
+    return;
+  }
   const int it = step[a.which];  // = Keras iterations + 1
   const int iters = it - 1;
   double lr = a.lr[4];
@@ -775,31 +835,6 @@ struct AdamNet {
   int items;                    // weight tiles + bias tiles, all layers
   int ioff[MAX_LAYERS + 1];     // first item of layer l: KT*OT weight tiles then OT bias tiles
 };
-
-struct AdamScalars {
-  float alpha, c1, c2, eps, tau, omt;
-};
-
-__device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int32_t* step) {
-  const int it = step[a.which];  // = Keras iterations + 1
-  const int iters = it - 1;
-  double lr = a.lr[4];
-  for (int k = 0; k < 4; ++k)
-    if ((double)iters <= a.bounds[k]) {
-      lr = a.lr[k];
-      break;
-    }
-  const float tf = (float)it;
-  const float b1p = powf((float)a.beta1, tf), b2p = powf((float)a.beta2, tf);
-  AdamScalars s;
-  s.alpha = fdiv(fmul((float)lr, __fsqrt_rn(fsub(1.f, b2p))), fsub(1.f, b1p));
-  s.c1 = (float)(1.0 - a.beta1);
-  s.c2 = (float)(1.0 - a.beta2);
-  s.eps = (float)a.eps;
-  s.tau = (float)a.tau;
-  s.omt = (float)(1.0 - a.tau);
-  return s;
-}
 
 // k_adam's per-parameter arithmetic (same ops, same order), values only
 __device__ __forceinline__ void adam_math(const AdamScalars& s, float g, float& mm, float& vv, float& th, float& tg) {
@@ -1132,7 +1167,19 @@ struct LaunchChainPair {
 
 // Rows per weight-gradient chunk (one slab each): small batches use short chunks so the grid
 // still fills the chip; large ones long chunks so Adam sums few slabs.
-inline int wg_chunk(int rows) { return rows <= 1024 ? 64 : rows <= 4096 ? 128 : 256; }
+// Row chunk of the split-K weight-gradient GEMM. CACTO_WG_CHUNK overrides it above 1024 rows
+// (read once; benchmarks) — the fused small-batch path always takes 64-row chunks.
+inline int wg_chunk_big() {
+  static const int v = [] {
+    const char* e = std::getenv("CACTO_WG_CHUNK");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+inline int wg_chunk(int rows) {
+  if (rows > 1024 && wg_chunk_big() > 0) return wg_chunk_big();
+  return rows <= 1024 ? 64 : rows <= 4096 ? 128 : 256;
+}
 
 struct Workspace {
   GradBufs crit, act;
@@ -1308,9 +1355,19 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
   float* v = which == CACTO_NET_CRITIC ? nets->critic_v_d : nets->actor_v_d;
   float4* pk = reinterpret_cast<float4*>(nb + flat_span(t));
   float4* tpk = reinterpret_cast<float4*>(nets->target_d + flat_span(t));
-  const int grid = std::min((t.params + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, st, slab, nch, t, src ? src : nb, nb, pk, m, v, nets->step_d,
-                     adam_args(cfg, which, soft && which == CACTO_NET_CRITIC), nets->target_d, tpk);
+  const AdamArgs aa = adam_args(cfg, which, soft && which == CACTO_NET_CRITIC);
+  const float* s0 = src ? src : nb;
+  // one parameter per thread with all chunk partials in flight (k_adam<NCH>), else the looped kernel
+  const int full = (t.params + 255) / 256;
+  auto go = [&](auto kern, int grid) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, slab, nch, t, s0, nb, pk, m, v, nets->step_d, aa,
+                       nets->target_d, tpk);
+  };
+  if (nch <= 8) go(k_adam<8>, full);
+  else if (nch <= 16) go(k_adam<16>, full);
+  else if (nch <= 32) go(k_adam<32>, full);
+  else if (nch <= 64) go(k_adam<64>, full);
+  else go(k_adam<0>, std::min(full, 1024));
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }
@@ -1690,8 +1747,18 @@ int ensure_side_stream(cacto_sys* ms) {
   if (ms->side) return CACTO_OK;
   hipStream_t side = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  hipError_t e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
-  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+  // CACTO_SIDE_PRIO=hi|lo: the side (actor) stream at the device's greatest / least priority
+  // (read once; benchmarks). Default: normal priority.
+  int prio = 0, least = 0, greatest = 0;
+  if (const char* pe = std::getenv("CACTO_SIDE_PRIO")) {
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      prio = pe[0] == 'h' ? greatest : pe[0] == 'l' ? least : 0;
+  }
+  hipError_t e = hipStreamCreateWithPriority(&side, hipStreamNonBlocking, prio);
+  // device-scope events (CACTO_EVENT_SYSFENCE=1 restores the system-scope fence): every
+  // producer and consumer of these dependencies is a kernel on this device
+  const unsigned evf = hipEventDisableTiming | (std::getenv("CACTO_EVENT_SYSFENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], evf);
   if (e != hipSuccess) {
     for (hipEvent_t x : ev)
       if (x) (void)hipEventDestroy(x);
