@@ -66,7 +66,7 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic(kernel=("k_rollout_tt<2>", "k_rollout<2,")):
+def pmc_traffic(kernel=("k_rollout_tt<2", "k_rollout<2,")):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summaries
     (profiles/rNN_pmc_{fetch,write}.csv, made by tools/prof_summary.py from separate --pmc
     FETCH_SIZE / WRITE_SIZE passes). gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE

@@ -977,6 +977,94 @@ __global__ void __launch_bounds__(256, 4) k_rollout_rewards(const SysDevice* __r
   }
 }
 
+// The same per-element work over the COMPACTED element space: element e of [0, sum_b (n_b + 1))
+// is step t = e - off[b] of episode b (off = exclusive prefix of n_b + 1, n_b = min(nsteps[b], T)),
+// so every lane of a wave has a recorded step. The per-element code is f64-issue bound (~1.5 k f64
+// instructions for DI), and in the [b][t] grid about 40 % of the waves that had any work straddled
+// an episode's end with part of their lanes idle. Each workgroup scans the B lengths into LDS
+// itself (B <= CACTO_REW_SCAN_MAX; the L2-resident lengths are read once per workgroup) and finds
+// an element's episode by binary search there. Same values written (bit-identical).
+#define CACTO_REW_SCAN_MAX 16000  // (B + 1) ints within the 64 KiB of dynamic LDS
+template <int NJ>
+__global__ void __launch_bounds__(256, 4) k_rollout_rewards_c(const SysDevice* __restrict__ sdp,
+                                                           const double* __restrict__ Straj,
+                                                           const float* __restrict__ Atraj,
+                                                           const int32_t* __restrict__ nsteps, int T, int use_actor,
+                                                           const double* __restrict__ Wext, double* __restrict__ Rtraj,
+                                                           double* __restrict__ EEtraj, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  extern __shared__ int offs[];  // B + 1
+  __shared__ int wsum[4];
+  const SysDevice& sd = *sdp;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // block exclusive scan of the element counts: thread tid owns episodes [tid*per, tid*per + per)
+  const int per = (B + 255) / 256, b0 = tid * per;
+  int loc = 0;
+  for (int k = 0; k < per; ++k) {
+    const int b = b0 + k;
+    if (b < B) {
+      const int n = min(nsteps[b], T);
+      loc += n >= 0 ? n + 1 : 0;
+    }
+  }
+  int inc = loc;  // inclusive scan over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wv; ++w) base += wsum[w];
+  int run = base + inc - loc;
+  for (int k = 0; k < per; ++k) {
+    const int b = b0 + k;
+    if (b < B) {
+      offs[b] = run;
+      const int n = min(nsteps[b], T);
+      run += n >= 0 ? n + 1 : 0;
+    }
+  }
+  if (tid == 255) offs[B] = base + inc;
+  __syncthreads();
+  const int total = offs[B];
+  double w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = k >= sd.p.n_weights ? 0.0 : Wext ? Wext[k] : sd.p.w_running[k];
+  for (int e = blockIdx.x * 256 + tid; e < total; e += gridDim.x * 256) {
+    int lo = 0, hi = B;  // the last b with offs[b] <= e (empty episodes are skipped over)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (offs[mid] <= e) lo = mid;
+      else hi = mid;
+    }
+    const int b = lo, t = e - offs[b];
+    const int n = min(nsteps[b], T);
+    const size_t row = (size_t)b * (T + 1) + t;
+    double s[ns];
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < ns; ++i) {
+      s[i] = Straj[row * ns + i];
+      bad |= isnan(s[i]);
+    }
+    if (bad) continue;
+    const V3 v = env_ee<NJ>(sd, s);
+    if (EEtraj) {
+      EEtraj[row * 3 + 0] = v.x;
+      EEtraj[row * 3 + 1] = v.y;
+      EEtraj[row * 3 + 2] = v.z;
+    }
+    if (Rtraj && t < n) {
+      double a[na];
+#pragma unroll
+      for (int i = 0; i < na; ++i) a[i] = use_actor ? (double)Atraj[((size_t)b * T + t) * na + i] : 0.0;
+      Rtraj[(size_t)b * T + t] = env_reward_at<NJ>(sd, w, s, a, false, v);
+    }
+  }
+}
+
 // Episode slots per workgroup and workgroup count for B episodes: about two episodes per slot
 // (their lengths pair up long + short), one workgroup per CU.
 inline int ro_cus() {
@@ -1001,9 +1089,22 @@ struct LaunchRolloutRewards {
   static int run(const cacto_sys* sys, const double* S, const float* A, const int32_t* n, int T, int use_actor,
                  const double* W, double* R, double* EE, int B, hipStream_t st) {
     const int64_t total = (int64_t)B * (T + 1);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8 * ro_cus()));
-    hipLaunchKernelGGL(k_rollout_rewards<NJ>, dim3(grid), dim3(256), 0, st, sys->dev, S, A, n, T, use_actor, W, R,
-                       EE, B);
+    // compacted elements where the per-element reward is long enough to pay for the per-workgroup
+    // scan and the per-element search (measured r03: car_park's 30 smooth boxes 410 -> 428 M
+    // env-steps/s; DI's rewards 29.9 -> 34.5 us, the chains unchanged). CACTO_REW_GRID=bt|c forces
+    // one (benchmarks).
+    static const char* force = std::getenv("CACTO_REW_GRID");
+    const bool compact = force ? force[0] == 'c' : NJ == -2;
+    if (B <= CACTO_REW_SCAN_MAX && compact) {
+      // compacted elements: at most 4 workgroups per CU (each scans the lengths once)
+      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4 * ro_cus()));
+      hipLaunchKernelGGL(k_rollout_rewards_c<NJ>, dim3(grid), dim3(256), (size_t)(B + 1) * sizeof(int), st, sys->dev,
+                         S, A, n, T, use_actor, W, R, EE, B);
+    } else {
+      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8 * ro_cus()));
+      hipLaunchKernelGGL(k_rollout_rewards<NJ>, dim3(grid), dim3(256), 0, st, sys->dev, S, A, n, T, use_actor, W, R,
+                         EE, B);
+    }
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
   }
