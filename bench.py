@@ -224,6 +224,28 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
         ev[1].record()
         rl.rollout_rewards(out, n_d, T)
 
+    # robustness check beside the contract's K-step region (the driver runs K = 20, ~16 ms): a long
+    # region of max(K, LONG_STEPS) rollout batches, as 5 consecutive segments, median reported. It runs
+    # BEFORE the contract's W warmup + K timed batches, so those are taken at settled GPU clocks (the
+    # first ~100 batches of a fresh process ran 5-10 % slower while the clocks ramped, r02 / r03).
+    steps_per_call = int(nsteps.sum())
+    long_k = max(K, LONG_STEPS) if LONG_STEPS > 0 else 0
+    long_region = None
+    if long_k >= 5:
+        lev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        cuts = [j * long_k // 5 for j in range(6)]
+        barrier(world)
+        lev[0].record()
+        for j in range(5):
+            for _ in range(cuts[j + 1] - cuts[j]):
+                rl.rollout_batch(None, None, T, inputs=inputs, out=seq)
+                rl.rollout_rewards(out, n_d, T)
+            lev[j + 1].record()
+        torch.cuda.synchronize()
+        rates = [steps_per_call * (cuts[j + 1] - cuts[j]) / (lev[j].elapsed_time(lev[j + 1]) * 1e-3) for j in range(5)]
+        long_region = dict(batches=long_k, seconds=lev[0].elapsed_time(lev[5]) * 1e-3, segment_rates=rates,
+                           median=sum_over_ranks(float(np.median(rates)), world),
+                           spread=float((max(rates) - min(rates)) / np.median(rates)))
     ev = [None, torch.cuda.Event(enable_timing=True)]
     for _ in range(W):
         step()
@@ -242,32 +264,9 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     wall = max_over_ranks(t1 - t0, world)
     kern_ms = sum(e[0].elapsed_time(e[2]) for e in evs) / K
     seq_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / K
-    steps_per_call = int(nsteps.sum())
     # the timed region in 5 consecutive segments (HIP events at their boundaries): per-segment rate
     # and the median of the 5, beside the whole-region value
     seg = segments([(e[0], e[2]) for e in evs], steps_per_call)
-    # robustness check beside the contract's K-step region (the driver runs K = 20, ~16 ms): a long
-    # region of max(K, LONG_STEPS) rollout batches, as 5 consecutive segments, median reported
-    long_k = max(K, LONG_STEPS) if LONG_STEPS > 0 else 0
-    if long_k < 5:
-        return dict(out=out, S0=S0, nsteps=nsteps, T=T, wall=wall, kernel_ms=kern_ms, seq_kernel_ms=seq_ms,
-                    seq_kernel_ms_median=float(np.median([e[0].elapsed_time(e[1]) for e in evs])),
-                    rewards_kernel_ms=kern_ms - seq_ms, steps_per_call=steps_per_call,
-                    total_steps=sum_over_ranks(steps_per_call * K, world), segments=seg, long_region=None)
-    lev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    cuts = [j * long_k // 5 for j in range(6)]
-    barrier(world)
-    lev[0].record()
-    for j in range(5):
-        for _ in range(cuts[j + 1] - cuts[j]):
-            rl.rollout_batch(None, None, T, inputs=inputs, out=seq)
-            rl.rollout_rewards(out, n_d, T)
-        lev[j + 1].record()
-    torch.cuda.synchronize()
-    rates = [steps_per_call * (cuts[j + 1] - cuts[j]) / (lev[j].elapsed_time(lev[j + 1]) * 1e-3) for j in range(5)]
-    long_region = dict(batches=long_k, seconds=lev[0].elapsed_time(lev[5]) * 1e-3, segment_rates=rates,
-                       median=sum_over_ranks(float(np.median(rates)), world),
-                       spread=float((max(rates) - min(rates)) / np.median(rates)))
     return dict(out=out, S0=S0, nsteps=nsteps, T=T, wall=wall, kernel_ms=kern_ms, seq_kernel_ms=seq_ms,
                 seq_kernel_ms_median=float(np.median([e[0].elapsed_time(e[1]) for e in evs])),
                 rewards_kernel_ms=kern_ms - seq_ms, steps_per_call=steps_per_call,
