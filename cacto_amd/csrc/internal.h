@@ -30,3 +30,8 @@ inline int64_t flat_span(const NetTopo& t) { return ((int64_t)t.params + 63) / 6
 cacto::NetView cacto_make_view(const cacto_sys* sys, int net, const float* netbuf);
 int cacto_const_dyn_init(cacto_sys* sys);  // SysDevice::cd_* of a prismatic-only chain (env_kernels.hip)
 int cacto_build_wgrad_adam_items(cacto_sys* sys);  // learn_kernels.hip
+// replay_kernels.hip: batches from this size on take the multi-workgroup PER kernels; the update
+// pipelines then issue the sample's exp_counter increment just before the priority update (its only
+// reader), off the sample -> critic chain path
+int cacto_per_mw_min();
+int cacto_per_count_launch(const int32_t* idx_d, int B, double* exp_counter_d, hipStream_t st);

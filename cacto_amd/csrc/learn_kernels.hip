@@ -1705,6 +1705,7 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
   const NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
   const AdamNet cn = critic_adam_net(sys, nets, cfg, w, soft, nullptr, nets->critic_d);
   const AdamNet an = actor_adam_net(sys, nets, cfg, w);
+  const bool late_count = per && B >= cacto_per_mw_min();  // exp_counter += 1 just before the priority update
   const int32_t* idx_prev = nullptr;
   for (int t = 0; t <= K; ++t) {
     const int32_t* idx = nullptr;
@@ -1714,7 +1715,7 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
       if (per) {
         int32_t* pi = w.pidx + (size_t)(t & 1) * w.Bp;
         if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
-                                     per->uniforms + (size_t)t * B, B, pi, w.pisw, per->exp_counter, st))
+                                     per->uniforms + (size_t)t * B, B, pi, w.pisw, late_count ? nullptr : per->exp_counter, st))
           return e;
         idx = pi;
         isw = w.pisw;
@@ -1733,6 +1734,8 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
       if (int e = launch_wgrad_adam(sys, 1, an, nullptr, nets->step_d, st)) return e;
     }
     if (per && t < K) {
+      if (late_count)
+        if (int e = cacto_per_count_launch(idx, B, per->exp_counter, st)) return e;
       if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
                                    per->eps, per->alpha, per->max_priority, B, st))
         return e;
@@ -1804,6 +1807,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   float* const buf[2] = {nets->critic_d, w.cshadow};
   float* const y = w.scal;
   float* const V = w.scal + w.Bp;
+  const bool late_count = per && B >= cacto_per_mw_min();  // exp_counter += 1 just before the priority update
   for (int t = 0; t < K; ++t) {
     // actor chain(t-2) read the critic buffer Adam(t) writes and (PER) the index buffer of update t
     if (t >= 2) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t & 1], 0));
@@ -1812,7 +1816,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     if (per) {
       int32_t* pi = w.pidx + (size_t)(t & 1) * w.Bp;
       if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
-                                   per->uniforms + (size_t)t * B, B, pi, w.pisw, per->exp_counter, st))
+                                   per->uniforms + (size_t)t * B, B, pi, w.pisw, late_count ? nullptr : per->exp_counter, st))
         return e;
       idx = pi;
       isw = w.pisw;
@@ -1825,6 +1829,8 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     *cbuf = (t + 1) & 1;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
     if (per) {
+      if (late_count)
+        if (int e = cacto_per_count_launch(idx, B, per->exp_counter, st)) return e;
       if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
                                    per->eps, per->alpha, per->max_priority, B, st))
         return e;

@@ -2,6 +2,8 @@
 // combination order of segment_tree.py (so sampled indices are bit-exact), stratified proportional
 // sampling, IS weights, the duplicate-once exp_counter update and last-write-wins priority updates
 // (replay_buffer.py:87-218).
+#include <cstdlib>
+
 #include "internal.h"
 
 namespace cacto {
@@ -90,7 +92,11 @@ __device__ double prefix_reduce(const double* tree, const double* top, int64_t n
   return r;
 }
 
-__global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __restrict__ sum_tree,
+// SPT samples per thread, PG of them in lock-step: the one-workgroup launch (1024 threads) takes
+// SPT = 8, PG = 4; the multi-workgroup launch one sample per thread (64-thread workgroups), so each
+// thread's serial work is one descent and one IS-weight pow
+template <int SPT, int PG>
+__global__ void __launch_bounds__(SPT == 1 ? 64 : PER_THREADS) k_per_sample(const double* __restrict__ sum_tree,
                                                            const double* __restrict__ min_tree, int64_t cap,
                                                            int64_t max_idx, double beta,
                                                            const double* __restrict__ uniforms, int B,
@@ -101,10 +107,15 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
   __shared__ int32_t idx_s[PER_MAX_B];
   __shared__ double top_s[TOP_NODES];
   const int64_t ntop = cap < TOP_NODES ? cap : TOP_NODES;
-  for (int k = threadIdx.x; k < ntop; k += blockDim.x) top_s[k] = k ? sum_tree[k] : 0.0;
-  __syncthreads();
+  // multi-workgroup launches: workgroup b takes samples [b * PER_MAX_B/PER_THREADS * blockDim.x, ...)
+  // (each stages the top and forms the batch scalars itself; exp_counter then goes to k_per_count)
+  const int base = blockIdx.x * SPT * blockDim.x;
+  // thread 0 forms the batch scalars from global memory while the others stage the top (the same
+  // node values either way), so the two memory latencies overlap
+  if (threadIdx.x > 0)  // threads 1.. stage the top
+    for (int k = threadIdx.x - 1; k < ntop; k += blockDim.x - 1) top_s[k] = k ? sum_tree[k] : 0.0;
   if (threadIdx.x == 0) {
-    const double p_total = prefix_reduce(sum_tree, top_s, ntop, cap, max_idx - 2);  // sum(0, max_idx - 1)
+    const double p_total = prefix_reduce(sum_tree, top_s, 0, cap, max_idx - 2);  // sum(0, max_idx - 1)
     seg_s = p_total / B;
     total_s = sum_tree[1];
     if (shards) {
@@ -131,12 +142,11 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
   // levels whose seven candidate left children are loaded together (one memory latency per round
   // instead of per level). The comparisons and subtractions are the reference's, in its order. The
   // (up to 8) descents of a thread advance in lock-step so their loads overlap too.
-  constexpr int PT = PER_MAX_B / PER_THREADS;
-  constexpr int PG = 4;  // descents in lock-step per group (register budget at 1024 threads)
+  constexpr int PT = SPT;
   int64_t node[PT];
 #pragma unroll
   for (int g = 0; g < PT; g += PG) {
-    if (threadIdx.x + g * blockDim.x >= (unsigned)B) {
+    if (base + threadIdx.x + g * blockDim.x >= (unsigned)B) {
 #pragma unroll
       for (int j = g; j < g + PG; ++j) node[j] = cap;
       continue;
@@ -145,7 +155,7 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
     int64_t nd[PG];
 #pragma unroll
     for (int jj = 0; jj < PG; ++jj) {
-      const int i = threadIdx.x + (g + jj) * blockDim.x;
+      const int i = base + threadIdx.x + (g + jj) * blockDim.x;
       p[jj] = i < B ? uniforms[i] * seg + i * seg : 0.0;
       nd[jj] = 1;
       if (i < B) {
@@ -163,13 +173,13 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
     while (true) {
       bool any = false;
 #pragma unroll
-      for (int jj = 0; jj < PG; ++jj) any |= (threadIdx.x + (g + jj) * blockDim.x < (unsigned)B) && nd[jj] < cap;
+      for (int jj = 0; jj < PG; ++jj) any |= (base + threadIdx.x + (g + jj) * blockDim.x < (unsigned)B) && nd[jj] < cap;
       if (!any) break;
       double a[PG], b0[PG], b1[PG], c[PG][4];
 #pragma unroll
       for (int jj = 0; jj < PG; ++jj) {
         const int64_t n = nd[jj];
-        const bool live = threadIdx.x + (g + jj) * blockDim.x < (unsigned)B && n < cap;
+        const bool live = base + threadIdx.x + (g + jj) * blockDim.x < (unsigned)B && n < cap;
         a[jj] = live ? tree_at(sum_tree, top_s, ntop, 2 * n) : 0.0;
         const bool two = live && 2 * n < cap, three = live && 4 * n < cap;
         b0[jj] = two ? sum_tree[4 * n] : 0.0;
@@ -180,7 +190,7 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
 #pragma unroll
       for (int jj = 0; jj < PG; ++jj) {
         const int64_t n = nd[jj];
-        if (threadIdx.x + (g + jj) * blockDim.x >= (unsigned)B || n >= cap) continue;
+        if (base + threadIdx.x + (g + jj) * blockDim.x >= (unsigned)B || n >= cap) continue;
         int64_t m;
         if (a[jj] > p[jj]) {
           m = 2 * n;
@@ -215,15 +225,16 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
   }
 #pragma unroll
   for (int j = 0; j < PT; ++j) {
-    const int i = threadIdx.x + j * blockDim.x;
+    const int i = base + threadIdx.x + j * blockDim.x;
     if (i < B) {
       const int32_t id = (int32_t)(node[j] - cap);
-      idx_s[i] = id;
+      idx_s[i - base] = id;
       idx_out[i] = id;
       const double pr = sum_tree[node[j]] / total;
       w_out[i] = (float)(pow(pr * scale, -beta) / maxw);
     }
   }
+  if (gridDim.x > 1) return;  // k_per_count follows
   __syncthreads();
   // exp_counter[idxes] += 1: numpy fancy-index increment counts each distinct index once.
   double old[PER_MAX_B / PER_THREADS];
@@ -234,6 +245,134 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_sample(const double* __rest
   for (int i = threadIdx.x; i < B; i += blockDim.x) {
     if (exp_counter) exp_counter[idx_s[i]] = old[k] + 1.0;
     ++k;
+  }
+}
+
+// The leaf writes of k_per_set over many workgroups, one leaf per thread (the two f64 pows of a
+// priority are the serial work): every workgroup checks the whole index list for order itself (so
+// "last occurrence" is the neighbour test for sorted lists, a scan otherwise, as in k_per_set), and
+// max_priority = max(max_priority, max p) by an atomic max on the bit pattern — the priorities are
+// positive (p >= eps > 0), where the IEEE order and the integer order agree; NaN is skipped as fmax
+// skips it. Same leaf values, same last-write-wins, same max (bit-identical).
+__global__ void __launch_bounds__(256) k_per_leaves_mw(double* sum_tree, double* min_tree, int64_t cap,
+                                                      const int32_t* __restrict__ idx, const double* __restrict__ vals,
+                                                      int n, const float* __restrict__ y, const float* __restrict__ V,
+                                                      const double* __restrict__ exp_counter, double fresh, double eps,
+                                                      double alpha, double* max_priority) {
+  bool unsorted = false;
+  for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) unsorted |= idx[i + 1] < idx[i];
+  const bool sorted = !__syncthreads_or(unsorted);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  double my_max = -__builtin_inf();
+  if (i < n) {
+    const int32_t id = idx[i];
+    double leaf;
+    if (vals) {
+      leaf = vals[i];
+    } else {
+      const float td = fabsf(__fsub_rn(y[i], V[i]));
+      const float fd = (float)pow(fresh, exp_counter[id]);
+      const float p = __fadd_rn(__fmul_rn(fd, td), (float)eps);
+      my_max = fmax(my_max, (double)p);
+      leaf = pow((double)p, alpha);
+    }
+    bool last = true;
+    if (sorted) {
+      last = i + 1 == n || idx[i + 1] != id;
+    } else {
+      for (int j = i + 1; j < n; ++j)
+        if (idx[j] == id) {
+          last = false;
+          break;
+        }
+    }
+    if (last) {
+      sum_tree[cap + id] = leaf;
+      min_tree[cap + id] = leaf;
+    }
+  }
+  if (max_priority) {
+    double m = my_max;
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0 && m > 0.0)  // false for -inf (no leaf) and NaN
+      atomicMax(reinterpret_cast<unsigned long long*>(max_priority), (unsigned long long)__double_as_longlong(m));
+  }
+}
+
+// exp_counter[idxes] += 1 after a multi-workgroup k_per_sample (numpy's fancy-index increment counts
+// each distinct index once). With a sorted index list (the stratified sampler's output) each distinct
+// index is incremented by the thread of its first occurrence alone, so no thread reads a counter
+// another one writes; an unsorted list (checked by every workgroup) is counted by workgroup 0 with
+// every read before any write. Same counters either way.
+__global__ void __launch_bounds__(256) k_per_count(const int32_t* __restrict__ idx, int B,
+                                                     double* __restrict__ exp_counter) {
+  bool unsorted = false;
+  for (int i = threadIdx.x; i + 1 < B; i += blockDim.x) unsorted |= idx[i + 1] < idx[i];
+  const bool sorted = !__syncthreads_or(unsorted);
+  if (sorted) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < B && (i == 0 || idx[i - 1] != idx[i])) exp_counter[idx[i]] += 1.0;
+    return;
+  }
+  if (blockIdx.x != 0) return;
+  double old[PER_MAX_B / 256];
+  int k = 0;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) old[k++] = exp_counter[idx[i]];
+  __syncthreads();
+  k = 0;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) exp_counter[idx[i]] = old[k++] + 1.0;
+}
+
+// Ancestor refresh of a priority update as whole subtrees in LDS: workgroup s loads the SUB leaves
+// [cap + s SUB, cap + (s + 1) SUB) of both trees, rebuilds the subtree's levels in LDS and writes
+// every internal node back. The tree is consistent (each node = op(children), set by these kernels
+// and k_per_level), so nodes over untouched leaves come out unchanged and the touched ones get
+// op(final children) — the value the reference's leaf-by-leaf updates leave (see k_per_fill_leaves).
+// One memory latency per workgroup instead of one barrier-separated global round per level.
+constexpr int PER_SUB = 1024;
+__global__ void __launch_bounds__(256) k_per_subtrees(double* __restrict__ sum_tree, double* __restrict__ min_tree,
+                                                     int64_t cap, int sub) {
+  __shared__ double ts[2 * PER_SUB], tm[2 * PER_SUB];  // local node j (1-based heap of the subtree)
+  const int64_t leaf0 = cap + (int64_t)blockIdx.x * sub;
+  for (int k = threadIdx.x; k < sub; k += blockDim.x) {
+    ts[sub + k] = sum_tree[leaf0 + k];
+    tm[sub + k] = min_tree[leaf0 + k];
+  }
+  __syncthreads();
+  int lvl = 0;
+  for (int lo = sub / 2; lo >= 1; lo /= 2) {
+    ++lvl;
+    for (int k = lo + threadIdx.x; k < 2 * lo; k += blockDim.x) {
+      ts[k] = ts[2 * k] + ts[2 * k + 1];
+      tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
+      // local node k of level lvl is global node (leaf0 >> lvl) + (k - lo)
+      const int64_t g = (leaf0 >> lvl) + (k - lo);
+      sum_tree[g] = ts[k];
+      min_tree[g] = tm[k];
+    }
+    __syncthreads();
+  }
+}
+
+// The nodes above the subtree roots, [1, cap / sub), from the roots (one workgroup, LDS).
+__global__ void __launch_bounds__(PER_THREADS) k_per_top(double* __restrict__ sum_tree, double* __restrict__ min_tree,
+                                                        int64_t nroot) {
+  extern __shared__ double sh[];  // 2 nroot sums, then 2 nroot mins
+  double* ts = sh;
+  double* tm = sh + 2 * nroot;
+  for (int64_t k = nroot + threadIdx.x; k < 2 * nroot; k += blockDim.x) {
+    ts[k] = sum_tree[k];
+    tm[k] = min_tree[k];
+  }
+  __syncthreads();
+  for (int64_t lo = nroot / 2; lo >= 1; lo /= 2) {
+    for (int64_t k = lo + threadIdx.x; k < 2 * lo; k += blockDim.x) {
+      ts[k] = ts[2 * k] + ts[2 * k + 1];
+      tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
+      sum_tree[k] = ts[k];
+      min_tree[k] = tm[k];
+    }
+    __syncthreads();
   }
 }
 
@@ -252,7 +391,7 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, doubl
                                                         const int32_t* __restrict__ idx, const double* __restrict__ vals,
                                                         int n, const float* __restrict__ y, const float* __restrict__ V,
                                                         const double* __restrict__ exp_counter, double fresh, double eps,
-                                                        double alpha, double* max_priority) {
+                                                        double alpha, double* max_priority, int leaves_only) {
   __shared__ int32_t id_s[PER_MAX_B];
   __shared__ double maxp_s[PER_THREADS / 64];
   __shared__ double top_sum[TOP_NODES], top_min[TOP_NODES];
@@ -302,6 +441,7 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, doubl
       max_priority[0] = fmax(max_priority[0], mm);
     }
   }
+  if (leaves_only) return;  // k_per_subtrees + k_per_top refresh the ancestors
   __syncthreads();
   // Ancestors below the LDS-staged top, one level per barrier. With sorted indices a node is
   // refreshed only by the first sample below it (the others would rewrite the same value). Each
@@ -400,6 +540,72 @@ int per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int6
 }
 }  // namespace
 
+namespace {
+// Batches of at least PER_MW_MIN samples take the multi-workgroup paths: the descents spread over
+// 64-thread workgroups (+ k_per_count), and the priority update's ancestor refresh as whole subtrees
+// in LDS (k_per_subtrees + k_per_top) after the leaf writes. Smaller batches keep the one-workgroup
+// kernels (fewer launches). Every path forms the same values (bit-identical indices, weights, trees).
+// CACTO_PER_MW_MIN overrides the bound (read once; benchmarks).
+int per_mw_min() {
+  static const int v = [] {
+    const char* e = std::getenv("CACTO_PER_MW_MIN");
+    return e ? std::atoi(e) : 512;
+  }();
+  return v;
+}
+
+int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
+                      double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
+                      double* exp_counter_d, const double* shards_d, int n_shards, hipStream_t st) {
+  if (B >= per_mw_min()) {
+    constexpr int TPB = 64;  // one sample per thread
+    hipLaunchKernelGGL((k_per_sample<1, 1>), dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sum_tree_d, min_tree_d, capacity,
+                       max_idx, beta, uniforms_d, B, idx_d, is_w_d, nullptr, shards_d, n_shards);
+    CACTO_CHECK_HIP(hipGetLastError());
+    if (exp_counter_d) {
+      hipLaunchKernelGGL(k_per_count, dim3((B + 255) / 256), dim3(256), 0, st, idx_d, B, exp_counter_d);
+      CACTO_CHECK_HIP(hipGetLastError());
+    }
+    return CACTO_OK;
+  }
+  hipLaunchKernelGGL((k_per_sample<PER_MAX_B / PER_THREADS, 4>), dim3(1), dim3(PER_THREADS), 0, st, sum_tree_d, min_tree_d, capacity, max_idx, beta,
+                     uniforms_d, B, idx_d, is_w_d, exp_counter_d, shards_d, n_shards);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+int launch_per_set(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                   const double* values_d, int n, const float* y_d, const float* V_d, const double* exp_counter_d,
+                   double fresh, double eps, double alpha, double* max_priority_d, hipStream_t st) {
+  const int64_t sub = std::min<int64_t>(PER_SUB, capacity), nroot = capacity / sub;
+  const bool mw = n >= per_mw_min() && nroot <= 2048;
+  if (!mw) {
+    hipLaunchKernelGGL(k_per_set, dim3(1), dim3(PER_THREADS), 0, st, sum_tree_d, min_tree_d, capacity, idx_d, values_d,
+                       n, y_d, V_d, exp_counter_d, fresh, eps, alpha, max_priority_d, 0);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
+  hipLaunchKernelGGL(k_per_leaves_mw, dim3((n + 255) / 256), dim3(256), 0, st, sum_tree_d, min_tree_d, capacity, idx_d,
+                     values_d, n, y_d, V_d, exp_counter_d, fresh, eps, alpha, max_priority_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_per_subtrees, dim3((unsigned)nroot), dim3(256), 0, st, sum_tree_d, min_tree_d, capacity, (int)sub);
+  CACTO_CHECK_HIP(hipGetLastError());
+  if (nroot > 1) {
+    hipLaunchKernelGGL(k_per_top, dim3(1), dim3(PER_THREADS), (size_t)4 * nroot * sizeof(double), st, sum_tree_d,
+                       min_tree_d, nroot);
+    CACTO_CHECK_HIP(hipGetLastError());
+  }
+  return CACTO_OK;
+}
+}  // namespace
+
+int cacto_per_mw_min() { return per_mw_min(); }
+int cacto_per_count_launch(const int32_t* idx_d, int B, double* exp_counter_d, hipStream_t st) {
+  hipLaunchKernelGGL(k_per_count, dim3((B + 255) / 256), dim3(256), 0, st, idx_d, B, exp_counter_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
 extern "C" int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
                                    int64_t start, int64_t n, double value, void* stream) {
   return per_set_range(sum_tree_d, min_tree_d, capacity, ring_size, start, n, value, nullptr, 0.0, as_stream(stream));
@@ -421,10 +627,8 @@ extern "C" int cacto_per_sample(const double* sum_tree_d, const double* min_tree
   CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_sample: 0 < B <= 8192");
   // max_idx <= 1 makes the reference's sum(0, max_idx - 1) recurse past the leaves (segment_tree.py:36-49)
   CACTO_REQUIRE(max_idx >= 2 && max_idx <= capacity, "cacto_per_sample: need 2 <= max_idx <= capacity");
-  hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
-                     max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d, nullptr, 0);
-  CACTO_CHECK_HIP(hipGetLastError());
-  return CACTO_OK;
+  return launch_per_sample(sum_tree_d, min_tree_d, capacity, max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d,
+                           nullptr, 0, as_stream(stream));
 }
 
 extern "C" int cacto_per_shard_stats(const double* sum_tree_d, const double* min_tree_d, int64_t max_idx,
@@ -445,10 +649,8 @@ extern "C" int cacto_per_sample_global(const double* sum_tree_d, const double* m
                 "cacto_per_sample_global: bad arguments");
   CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_sample_global: 0 < B <= 8192");
   CACTO_REQUIRE(max_idx >= 2 && max_idx <= capacity, "cacto_per_sample_global: need 2 <= max_idx <= capacity");
-  hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
-                     max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d, shard_stats_d, n_shards);
-  CACTO_CHECK_HIP(hipGetLastError());
-  return CACTO_OK;
+  return launch_per_sample(sum_tree_d, min_tree_d, capacity, max_idx, beta, uniforms_d, B, idx_d, is_w_d, exp_counter_d,
+                           shard_stats_d, n_shards, as_stream(stream));
 }
 
 extern "C" int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
@@ -457,18 +659,14 @@ extern "C" int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t 
   CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && y_d && V_d && exp_counter_d && max_priority_d && pow2(capacity),
                 "cacto_per_update: bad arguments");
   CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_update: 0 < B <= 8192");
-  hipLaunchKernelGGL(k_per_set, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
-                     idx_d, nullptr, B, y_d, V_d, exp_counter_d, fresh_factor, eps, alpha, max_priority_d);
-  CACTO_CHECK_HIP(hipGetLastError());
-  return CACTO_OK;
+  return launch_per_set(sum_tree_d, min_tree_d, capacity, idx_d, nullptr, B, y_d, V_d, exp_counter_d, fresh_factor, eps,
+                        alpha, max_priority_d, as_stream(stream));
 }
 
 extern "C" int cacto_per_set_leaves(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
                                     const double* values_d, int n, void* stream) {
   CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && values_d && pow2(capacity), "cacto_per_set_leaves: bad arguments");
   CACTO_REQUIRE(n > 0 && n <= PER_MAX_B, "cacto_per_set_leaves: 0 < n <= 8192");
-  hipLaunchKernelGGL(k_per_set, dim3(1), dim3(PER_THREADS), 0, as_stream(stream), sum_tree_d, min_tree_d, capacity,
-                     idx_d, values_d, n, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0, nullptr);
-  CACTO_CHECK_HIP(hipGetLastError());
-  return CACTO_OK;
+  return launch_per_set(sum_tree_d, min_tree_d, capacity, idx_d, values_d, n, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0,
+                        nullptr, as_stream(stream));
 }
