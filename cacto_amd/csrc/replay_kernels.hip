@@ -96,7 +96,7 @@ __device__ double prefix_reduce(const double* tree, const double* top, int64_t n
 // SPT = 8, PG = 4; the multi-workgroup launch one sample per thread (64-thread workgroups), so each
 // thread's serial work is one descent and one IS-weight pow
 template <int SPT, int PG>
-__global__ void __launch_bounds__(SPT == 1 ? 64 : PER_THREADS) k_per_sample(const double* __restrict__ sum_tree,
+__global__ void __launch_bounds__(SPT == 1 ? 256 : PER_THREADS) k_per_sample(const double* __restrict__ sum_tree,
                                                            const double* __restrict__ min_tree, int64_t cap,
                                                            int64_t max_idx, double beta,
                                                            const double* __restrict__ uniforms, int B,
@@ -104,9 +104,12 @@ __global__ void __launch_bounds__(SPT == 1 ? 64 : PER_THREADS) k_per_sample(cons
                                                            double* __restrict__ exp_counter,
                                                            const double* __restrict__ shards, int n_shards) {
   __shared__ double seg_s, total_s, maxw_s, scale_s;
-  __shared__ int32_t idx_s[PER_MAX_B];
-  __shared__ double top_s[TOP_NODES];
-  const int64_t ntop = cap < TOP_NODES ? cap : TOP_NODES;
+  // the multi-workgroup launch (SPT = 1) stages a deeper top (4,096 nodes: two rounds of global
+  // levels instead of three below it) and needs no index copy
+  constexpr int TOPN = SPT == 1 ? 4 * TOP_NODES : TOP_NODES;
+  __shared__ int32_t idx_s[SPT == 1 ? 1 : PER_MAX_B];
+  __shared__ double top_s[TOPN];
+  const int64_t ntop = cap < TOPN ? cap : TOPN;
   // multi-workgroup launches: workgroup b takes samples [b * PER_MAX_B/PER_THREADS * blockDim.x, ...)
   // (each stages the top and forms the batch scalars itself; exp_counter then goes to k_per_count)
   const int base = blockIdx.x * SPT * blockDim.x;
@@ -228,13 +231,13 @@ __global__ void __launch_bounds__(SPT == 1 ? 64 : PER_THREADS) k_per_sample(cons
     const int i = base + threadIdx.x + j * blockDim.x;
     if (i < B) {
       const int32_t id = (int32_t)(node[j] - cap);
-      idx_s[i - base] = id;
+      if constexpr (SPT > 1) idx_s[i - base] = id;
       idx_out[i] = id;
       const double pr = sum_tree[node[j]] / total;
       w_out[i] = (float)(pow(pr * scale, -beta) / maxw);
     }
   }
-  if (gridDim.x > 1) return;  // k_per_count follows
+  if (SPT == 1 || gridDim.x > 1) return;  // the multi-workgroup launch: k_per_count follows
   __syncthreads();
   // exp_counter[idxes] += 1: numpy fancy-index increment counts each distinct index once.
   double old[PER_MAX_B / PER_THREADS];
@@ -558,7 +561,7 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
                       double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
                       double* exp_counter_d, const double* shards_d, int n_shards, hipStream_t st) {
   if (B >= per_mw_min()) {
-    constexpr int TPB = 64;  // one sample per thread
+    constexpr int TPB = 256;  // one sample per thread
     hipLaunchKernelGGL((k_per_sample<1, 1>), dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sum_tree_d, min_tree_d, capacity,
                        max_idx, beta, uniforms_d, B, idx_d, is_w_d, nullptr, shards_d, n_shards);
     CACTO_CHECK_HIP(hipGetLastError());
