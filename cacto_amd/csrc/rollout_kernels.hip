@@ -801,6 +801,9 @@ struct RoTeamView {
 
 // Barrier of the 4 waves of a team: each wave's lane 0 adds one arrival (release: the wave's LDS
 // writes are complete), the wave then waits for 4 arrivals per barrier so far (acquire).
+#ifndef RO_TBAR_SLEEP
+#define RO_TBAR_SLEEP 1  // s_sleep between polls of a team barrier
+#endif
 struct RoTeamBar {
   int* ctr;
   int target;
@@ -809,7 +812,7 @@ struct RoTeamBar {
     target += 4;
     if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(RO_TBAR_SLEEP);
   }
 };
 
