@@ -63,7 +63,91 @@ def parse():
                    help="skip the rollout variants (profiling runs: every k_rollout dispatch is a full rollout)")
     p.add_argument("--long-steps", type=int, default=1000,
                    help="rollout batches of the long robustness region reported beside the K-step value")
+    p.add_argument("--dry-run", action="store_true",
+                   help="rank plumbing only: launch / rendezvous (gloo on the CPU) and print each rank's "
+                        "RANK / LOCAL_RANK / WORLD_SIZE and the device it would use; no GPU call")
+    p.add_argument("--launch-timeout", type=float, default=1800.0,
+                   help="seconds the --gpus N launcher waits for its ranks before killing them")
     return p.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) run directly, without a torch.distributed launcher: start N
+    fresh rank processes of this script — one per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    rendezvous on 127.0.0.1 — before this process makes any GPU call (it makes none), wait for
+    them, and exit with the first failing rank's code. Rank 0 writes the JSON line to this
+    process's stdout; the other ranks' stdout goes to stderr. Replaces the reference's
+    multiprocessing.Pool (main.py:219-225) as the node-level parallelism: one process per GPU."""
+    import signal
+    import subprocess
+    n = args.gpus
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise SystemExit(143)
+    signal.signal(signal.SIGTERM, stop)
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                          stdout=None if r == 0 else sys.stderr.fileno()))
+        t0, last = time.time(), time.time()
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print("bench launcher: rank %d exited with %d; stopping the other ranks" % (r, c), file=sys.stderr)
+                return c
+            if all(c == 0 for c in codes):
+                return 0
+            if time.time() - t0 > args.launch_timeout:
+                print("bench launcher: ranks still running after %.0f s; killing them" % args.launch_timeout,
+                      file=sys.stderr)
+                return 124
+            if time.time() - last > 60:
+                last = time.time()
+                print("bench launcher: %d of %d ranks running, %.0f s" % (sum(c is None for c in codes), n,
+                                                                          last - t0), file=sys.stderr, flush=True)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            p.wait()
+
+
+def dry_run(args):
+    """The rank plumbing without the GPU: rendezvous over gloo (CPU) as the real run would over
+    RCCL, all-gather what every rank sees, rank 0 prints one JSON line."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    me = dict(rank=rank, local_rank=local, world_size=world, device="cuda:%d" % local,
+              master="%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")))
+    ranks = [me]
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_requested": args.gpus, "ranks": ranks,
+                          "backend": os.environ.get("CACTO_DIST_BACKEND", "nccl")}))
 
 
 def pmc_traffic(kernel=("k_rollout_tt<2", "k_rollout<2,")):
@@ -138,6 +222,7 @@ def init_dist():
     if backend != "nccl":
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    DIST["backend"] = backend if world > 1 else None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -145,7 +230,16 @@ def init_dist():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
+        DIST["ranks"] = dist.get_world_size()
+        # the physical devices the ranks run on (a gloo rehearsal may put several ranks on one GPU)
+        devs = [None] * world
+        props = torch.cuda.get_device_properties(local)
+        dist.all_gather_object(devs, str(getattr(props, "uuid", local)))
+        DIST["devices"] = len(set(devs))
     return world, rank
+
+
+DIST = {"backend": None, "ranks": 1, "devices": 1}
 
 
 def barrier(world):
@@ -673,6 +767,29 @@ def config0(args, rank, cpu_updates):
     return out
 
 
+def flat_summary(updates, upd_roof, extra, world):
+    """Top-level scalar copies of the nested results (a record that keeps only the line's
+    top-level scalars still carries the update rates, the update roofline and the configs[2..4]
+    figures), plus what the distributed run actually was."""
+    out = {"rccl_ranks": DIST["ranks"] if DIST["backend"] == "nccl" else None,
+           "dist_backend": DIST["backend"], "devices": DIST["devices"] if world > 1 else 1}
+    for k, u in (updates or {}).items():
+        b = k.split("=")[1]
+        out["di_updates_per_s_b%s" % b] = u["value"]
+        out["di_update_mfma_frac_b%s" % b] = u["mfma_frac"]
+    if upd_roof:
+        out["update_mfma_frac"] = upd_roof["mfma_frac"]
+        out["update_counter_over_algorithmic"] = upd_roof["counter_over_algorithmic"]
+    for name, e in (extra or {}).items():
+        out["%s_env_steps_per_s" % name] = e["env_steps_per_s"]
+        out["%s_rollout_mfma_frac" % name] = e["rollout_mfma_frac"]
+        for k, u in e["critic_updates"].items():
+            b = k.split("=")[1]
+            out["%s_updates_per_s_b%s" % (name, b)] = u["value"]
+            out["%s_update_mfma_frac_b%s" % (name, b)] = u["mfma_frac"]
+    return out
+
+
 USE_GRAPH = False
 LONG_STEPS = 1000
 
@@ -680,6 +797,14 @@ LONG_STEPS = 1000
 def main():
     global USE_GRAPH, LONG_STEPS
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args))       # N rank processes of this script, one per GPU
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s (a launcher started a different number of ranks)"
+                 % (args.gpus, os.environ["WORLD_SIZE"]))
+    if args.dry_run:
+        return dry_run(args)
     USE_GRAPH = args.graph
     LONG_STEPS = args.long_steps
     world, rank = init_dist()
@@ -781,6 +906,7 @@ def main():
             "extra_systems": extra,
             "config0": c0,
         }
+        line.update(flat_summary(updates, upd_roof, extra, world))
         print(json.dumps(line))
     if world > 1:
         import torch.distributed as dist

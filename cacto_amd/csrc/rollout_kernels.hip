@@ -898,6 +898,11 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
 #endif
   for (int it = 0; S.anyact; ++it) {
     TSTAMP(0);
+    // Every wave must have read S.anyact (the loop test) before wave 0 rewrites it below. With the
+    // actor, its first team barrier orders that; without it (ep == 0, zero controls) this barrier
+    // does: a counter barrier, unlike s_barrier, would wait forever for waves that left the loop on
+    // an anyact they read too late.
+    if (!use_actor) tbar();
     if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true>(R, V, W2g, L, it, tbar);
     TSTAMP(1);
     if (L.wave == 0) {

@@ -430,16 +430,22 @@ def test_rollout_slot_refill_matches_one_episode_per_slot(system, sched):
         np.testing.assert_allclose(EE[k, n], oe.get_end_effector_position(S[k, n]), rtol=1e-12, atol=1e-12)
 
 
-def test_rollout_zero_controls_ep0_exact():
+@pytest.mark.parametrize("sched", [(0, 0), (-1, 2), (-1, 1), (1, 3)])
+def test_rollout_zero_controls_ep0_exact(sched):
+    """ep == 0 (zero warm-start controls, no actor) on the default schedule, on the two-team kernel
+    (groups = -1: its loop has no actor barriers, so the team barrier that orders the loop test
+    before wave 0 rewrites `anyact` is the only one per step) and on a refilling single-team one."""
     conf, genv, oe, nn, rl = _nets("double_integrator", None)
     rng = random.Random(6)
     S0 = np.array([oe.reset(rng) for _ in range(20)])
     ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
-    out = rl.rollout_batch(S0, ns_, max(ns_), ep=0)
+    out = rl.rollout_batch(S0, ns_, max(ns_), ep=0, sched=sched)
+    torch.cuda.synchronize()
     S = out["S"].cpu().numpy()
     for k in range(20):
         rS, rU, rT = oroll.to_init_rollout(oe, None, S0[k], 0)
         np.testing.assert_array_equal(S[k, :rT + 1], rS)
+    assert (out["status"].cpu().numpy() == 0).all()
 
 
 # ------------------------------------------------------------------ replay
