@@ -202,3 +202,262 @@ def test_per_shard_exchange_gives_union_weights():
     o, idx = _per_shard(0)
     o2, _ = _per_shard(0)
     np.testing.assert_array_equal(o.sample_weights_global(idx, o.shard_stats()[None]), o2.sample_weights(idx))
+
+
+# ------------------------------------------------------------------ the configs' rank counts
+# configs[3]: car_park with PER on 4 ranks (a replay shard per rank, IS weights over the union of
+# the shards); configs[4]: UR5 with the Sobolev term (w_S = 1e-2) on 8 ranks at a global batch of
+# 16,384 (2,048 per rank). Each rank runs the schedule RL_AC runs over RCCL (dp_pipeline: the
+# critic gradient of update t beside the actor gradient of update t-1, each part all-reduced as
+# soon as it is formed; with PER the stratified sample of update t after the priority update of
+# t-1, as update_rows_n_per_dp orders it) on oracle gradients; a single process running the
+# sequential loop (RL.py:101-137) at the global batch over all the shards is the reference.
+CP_B, CP_K, CP_WORLD = 8, 3, 4
+UR5_B, UR5_K, UR5_WORLD = 2048, 2, 8
+
+
+def _init_params(conf, seed):
+    rng = np.random.default_rng(seed)
+    ns, na = conf.nb_state, conf.nb_action
+
+    def lin(i, o, s):
+        return [rng.uniform(-s, s, (i, o)), rng.uniform(-0.05, 0.05, o)]
+    actor = lin(ns, 256, np.sqrt(6.0 / ns)) + lin(256, 256, np.sqrt(6.0 / 256)) + lin(256, na, 0.1 * np.sqrt(6.0 / 256))
+    critic = (lin(ns, 64, 1.0 / ns) + lin(64, 64, np.sqrt(6.0 / 64)) + lin(64, 128, np.sqrt(6.0 / 64)) +
+              lin(128, 128, np.sqrt(6.0 / 128)) + lin(128, 1, np.sqrt(6.0 / 128)))
+    return actor, critic
+
+
+class _Learner:
+    """Replicated actor / critic / target on oracle gradients and the Keras Adam restatement."""
+
+    def __init__(self, system, w_S, B_global):
+        from cacto_amd.confs import load_conf
+        self.conf = conf = load_conf(system)
+        self.oe = oenv.make_env(conf)
+        a, c = _init_params(conf, 5)
+        self.st = {"actor": a, "critic": c, "target": [p.copy() for p in c]}
+        self.adam = {"critic": onn.KerasAdam(conf.CRITIC_LEARNING_RATE), "actor": onn.KerasAdam(conf.ACTOR_LEARNING_RATE)}
+        self.norm = conf.state_norm_arr.astype(np.float64)
+        self.w_S, self.Bg = w_S, B_global
+
+    def _split(self, rows):
+        ns = self.conf.nb_state
+        return (rows[:, :ns], rows[:, ns:ns + 1], rows[:, ns + 1:2 * ns + 1], rows[:, 2 * ns + 1:3 * ns + 1],
+                rows[:, 3 * ns + 1:3 * ns + 2], rows[:, 3 * ns + 2:])
+
+    def critic_grad(self, rows, w):
+        S, R, Sn, dVdx, d, _ = self._split(rows)
+        g, y, V, _, _ = onn.compute_critic_grad(self.st["critic"], self.st["target"], S, Sn, R, dVdx, d,
+                                                np.asarray(w).reshape(-1, 1), self.w_S, self.norm)
+        return _flat(g) * (rows.shape[0] / self.Bg), y, V       # local mean -> share of the global mean
+
+    def actor_grad(self, rows):
+        S, _, _, _, _, term = self._split(rows)
+        g = onn.compute_actor_grad(self.oe, self.st["actor"], self.st["critic"], S.astype(np.float32), term, self.norm)
+        return _flat(g) * (rows.shape[0] / self.Bg)
+
+    def apply(self, which, g):
+        self.st[which] = self.adam[which].apply(self.st[which], _unflat(g, self.st[which]))
+        if which == "critic":
+            self.st["target"] = onn.soft_update(self.st["target"], self.st["critic"], self.conf.UPDATE_RATE)
+
+    def weights(self):
+        return {k: _flat(v).numpy() for k, v in self.st.items()}
+
+
+def _shard_rows(conf, n, seed):
+    ns = conf.nb_state
+    rng = np.random.default_rng(seed)
+    lo = np.asarray(conf.x_init_min, dtype=np.float64)
+    hi = np.asarray(conf.x_init_max, dtype=np.float64)
+    S = lo + (hi - lo) * rng.uniform(size=(n, ns))
+    Sn = lo + (hi - lo) * rng.uniform(size=(n, ns))
+    return np.concatenate([S, rng.normal(size=(n, 1)) * 0.5, Sn, rng.normal(size=(n, ns)) * 0.3,
+                           (rng.uniform(size=(n, 1)) < 0.3).astype(float),
+                           (rng.uniform(size=(n, 1)) < 0.2).astype(float)], axis=1)
+
+
+def _cp_shard(conf, rank):
+    """Rank `rank`'s car_park replay shard: rows of a different fill per rank, leaves of assorted
+    priorities (as after some updates), and the rank's own random.random() draws."""
+    from oracle import buffer as obuf
+    o = obuf.PrioritizedReplayBuffer(256, conf.nb_state, 0.6, 0.6, 1e-2, 0.95, CP_B)
+    n = 90 + 40 * rank
+    o.add_rows(_shard_rows(conf, n, 300 + rank))
+    rng = np.random.default_rng(400 + rank)
+    for i, p in enumerate(rng.uniform(0.05, 3.0, size=n)):
+        o.it_sum[i] = float(p) ** 0.6
+        o.it_min[i] = float(p) ** 0.6
+    o.max_priority = 3.0
+    return o, rng.uniform(size=(CP_K, CP_B))
+
+
+def _shard_state(o):
+    cap = o.it_sum.cap
+    return dict(sum=np.array(o.it_sum.value[cap:]), min=np.array(o.it_min.value[cap:]),
+                exp=o.exp_counter.copy(), maxp=o.max_priority)
+
+
+def _per_rank(rank, world, all_gather, all_reduce):
+    """update_rows_n_per_dp's schedule on one rank (car_park, PER)."""
+    from cacto_amd.rl import dp_pipeline
+    from cacto_amd.replay_buffer import exchange_shard_stats
+    L = _Learner("car_park", 0.0, CP_B * world)
+    o, U = _cp_shard(L.conf, rank)
+    drawn, yv, idxs = {}, {}, []
+
+    def stages(c, a):
+        if c is not None:
+            stats = exchange_shard_stats(torch.from_numpy(o.shard_stats()), world, all_gather).numpy()
+            idx = o.sample_proportional(U[c])
+            w = o.sample_weights_global(idx, stats)
+            drawn[c] = idx
+            idxs.append(idx.copy())
+            g, y, V = L.critic_grad(o.storage[idx], w)
+            yv[c] = (y, V)
+            yield "critic", g
+        if a is not None:
+            yield "actor", L.actor_grad(o.storage[drawn[a]])
+
+    def apply(which, step, g):
+        L.apply(which, g)
+        if which == "critic":                      # the priority update after the critic's Adam
+            o.update_priorities(drawn[step], *yv[step])
+    dp_pipeline(CP_K, stages, all_reduce, apply)
+    return dict(weights=L.weights(), shard=_shard_state(o), idx=np.array(idxs))
+
+
+def _per_reference(world):
+    """One process, the sequential loop: per update every shard samples its B_local from its own
+    tree with weights against the union, one update at the global batch, then the priorities."""
+    L = _Learner("car_park", 0.0, CP_B * world)
+    sh = [_cp_shard(L.conf, r) for r in range(world)]
+    idxs = [[] for _ in range(world)]
+    for t in range(CP_K):
+        stats = np.stack([o.shard_stats() for o, _ in sh])
+        parts = []
+        for r, (o, U) in enumerate(sh):
+            idx = o.sample_proportional(U[t])
+            parts.append((idx, o.sample_weights_global(idx, stats)))
+            idxs[r].append(idx.copy())
+        rows = np.concatenate([o.storage[idx] for (o, _), (idx, _) in zip(sh, parts)])
+        g, y, V = L.critic_grad(rows, np.concatenate([w for _, w in parts]))
+        L.apply("critic", g)
+        L.apply("actor", L.actor_grad(rows))
+        for r, ((o, _), (idx, _)) in enumerate(zip(sh, parts)):
+            o.update_priorities(idx, y[r * CP_B:(r + 1) * CP_B], V[r * CP_B:(r + 1) * CP_B])
+    return L.weights(), [_shard_state(o) for o, _ in sh], [np.array(i) for i in idxs]
+
+
+def _ur5_rank(rank, world, all_gather, all_reduce):
+    """update_rows_n's data-parallel schedule on one rank (UR5, w_S = 1e-2, no PER)."""
+    from cacto_amd.rl import dp_pipeline
+    L = _Learner("ur5", 1e-2, UR5_B * world)
+    rows = _shard_rows(L.conf, UR5_B * world, 77)[rank * UR5_B:(rank + 1) * UR5_B]
+    w = np.ones(UR5_B)
+
+    def stages(c, a):
+        if c is not None:
+            yield "critic", L.critic_grad(rows, w)[0]
+        if a is not None:
+            yield "actor", L.actor_grad(rows)
+    dp_pipeline(UR5_K, stages, all_reduce, lambda which, step, g: L.apply(which, g))
+    return dict(weights=L.weights())
+
+
+def _ur5_reference(world):
+    L = _Learner("ur5", 1e-2, UR5_B * world)
+    rows = _shard_rows(L.conf, UR5_B * world, 77)
+    for _ in range(UR5_K):
+        L.apply("critic", L.critic_grad(rows, np.ones(len(rows)))[0])
+        L.apply("actor", L.actor_grad(rows))
+    return L.weights()
+
+
+_RANK_FNS = {"per": _per_rank, "ur5": _ur5_rank}
+
+
+def _generic_worker(rank, world, port, kind, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = _RANK_FNS[kind](rank, world, lambda out, t: dist.all_gather(out, t),
+                              lambda t: dist.all_reduce(t, async_op=True))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(kind, world):
+    """Start `world` gloo ranks of `kind`; returns a function that collects their results (the
+    caller computes its reference meanwhile)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    old = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    os.environ.update(OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    try:
+        procs = [ctx.Process(target=_generic_worker, args=(r, world, port, kind, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+    def collect():
+        try:
+            res = dict(q.get(timeout=600) for _ in procs)
+            for p in procs:
+                p.join(timeout=60)
+                assert p.exitcode == 0
+            return res
+        finally:
+            for p in procs:
+                if p.is_alive():
+                    p.kill()
+    return collect
+
+
+def _assert_weights(res, ref, world):
+    for k in ("actor", "critic", "target"):
+        for r in range(1, world):
+            assert np.array_equal(res[r]["weights"][k], res[0]["weights"][k]), (k, r)   # replicas identical
+        np.testing.assert_allclose(res[0]["weights"][k], ref[k], rtol=1e-9, atol=1e-12, err_msg=k)
+
+
+def test_dp_per_car_park_ws4_equals_global_sampler():
+    """configs[3] at its rank count: 4 ranks, one PER shard each (different fills), union IS
+    weights, the pipelined DP schedule. Against the single-process global sampler: the same indices
+    on every shard, the same exp_counter, trees and max_priority, and the same weights."""
+    collect = _spawn("per", CP_WORLD)
+    ref_w, ref_sh, ref_idx = _per_reference(CP_WORLD)
+    res = collect()
+    _assert_weights(res, ref_w, CP_WORLD)
+    for r in range(CP_WORLD):
+        np.testing.assert_array_equal(res[r]["idx"], ref_idx[r])
+        got, exp = res[r]["shard"], ref_sh[r]
+        np.testing.assert_array_equal(got["exp"], exp["exp"])
+        # leaves float(p)**alpha of p = f32(fresh^n |y - V|) + eps: y, V differ from the reference
+        # by the reassociated all-reduce sums only
+        np.testing.assert_allclose(got["sum"], exp["sum"], rtol=1e-6)
+        np.testing.assert_allclose(got["min"], exp["min"], rtol=1e-6)
+        assert abs(got["maxp"] - exp["maxp"]) <= 1e-6 * exp["maxp"]
+    # the priorities did move away from the initial leaves, and the shards drew different rows
+    assert not np.allclose(ref_sh[0]["sum"], _shard_state(_cp_shard(_Learner("car_park", 0.0, 1).conf, 0)[0])["sum"])
+    assert sum(s["exp"].sum() for s in ref_sh) == CP_WORLD * CP_K * CP_B - sum(
+        len(i) - len(np.unique(i)) for idx in ref_idx for i in idx)
+
+
+def test_dp_ur5_ws8_global_16384_equals_single_process():
+    """configs[4] at its rank count: 8 ranks x 2,048 rows = the global batch of 16,384, UR5 with the
+    Sobolev term, two pipelined DP updates against the single-process sequential loop."""
+    collect = _spawn("ur5", UR5_WORLD)
+    ref = _ur5_reference(UR5_WORLD)
+    res = collect()
+    _assert_weights(res, ref, UR5_WORLD)
