@@ -30,11 +30,12 @@ def main():
             rl.rollout_batch(None, None, T, inputs=inputs, out=out, sched=sc)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(5):
+        reps = int(os.environ.get("RO_REPS", "50"))
+        for _ in range(reps):
             rl.rollout_batch(None, None, T, inputs=inputs, out=out, sched=sc)
         e1.record()
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 5
+        ms = e0.elapsed_time(e1) / reps
         print("%s R=%d sched=%s: %.3f ms  %.1fM env-steps/s" % (system, R, sc, ms, steps / ms / 1e3), flush=True)
 
 

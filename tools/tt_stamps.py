@@ -30,7 +30,41 @@ def main():
         print(system, "team", team, "step %.0f: actor %.0f, dynamics+stores+refill %.0f, barrier %.0f"
               % (t[3] - t[0], t[1] - t[0], t[2] - t[1], t[3] - t[2]), "(start offset vs team 0: %.0f)" % (t[0] - v[0]))
     print("   team 0 actor: layer 1 %.0f, layer 2 %.0f, layer 3 %.0f" % (v[4] - v[0], v[5] - v[4], v[1] - v[5]))
+    # every step of every team of the last launch, accumulated in-kernel (wave 0 and wave 1 of each team)
+    acc = (ctypes.c_ulonglong * (1024 * 2 * 2 * 10))()
+    L.lib().dll.cacto_debug_rollout_tt_acc(acc)
+    a = np.array(acc[:], dtype=np.float64).reshape(1024, 2, 2, 10)
+    names = ["layer 1 + bar", "layer 2 + bar", "layer 3 + bar", "dynamics/stores/refill", "end barrier",
+             "(wave 0: a + s'=f(s,a)", "stores", "refill", "next input + ballot)"]
+    for w in (0, 1):
+        steps = a[:, :, w, 9].sum()
+        tot = a[:, :, w, :9].sum(axis=(0, 1))
+        per = tot / max(steps, 1)
+        print("   all teams, wave %d, %d team-steps: cycles per step %.0f = " % (w, steps, per[:5].sum()) +
+              ", ".join("%s %.0f" % (n, x) for n, x in zip(names, per)))
+
+
+def ws(system):
+    """k_rollout_ws (groups -2): per-phase cycles per step, every wave of every team."""
+    conf, env, rl = bench.make_learner(system)
+    S0, n = bench.initial_states(env, conf, 4096, seed=0)
+    T = int(n.max())
+    inputs = rl.rollout_inputs(S0, n)
+    for _ in range(3):
+        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(-2, 0))
+    torch.cuda.synchronize()
+    acc = (ctypes.c_ulonglong * (1024 * 2 * 4 * 7))()
+    L.lib().dll.cacto_debug_rollout_ws_acc(acc)
+    a = np.array(acc[:], dtype=np.float64).reshape(1024, 2, 4, 7)
+    names = ["loop test + layer 2 + bar", "layer 3", "s'=f(s,a) + stores", "refill", "layer 1", "end barrier"]
+    steps = a[..., 6].sum()
+    per = a[..., :6].sum(axis=(0, 1, 2)) / max(steps, 1)
+    print(system, "k_rollout_ws, %d wave-steps: cycles per step %.0f = " % (steps, per.sum()) +
+          ", ".join("%s %.0f" % (nm, x) for nm, x in zip(names, per)))
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "ws":
+        ws(sys.argv[1])
+        sys.exit(0)
     main()
