@@ -93,8 +93,8 @@ __device__ double prefix_reduce(const double* tree, const double* top, int64_t n
 }
 
 // SPT samples per thread, PG of them in lock-step: the one-workgroup launch (1024 threads) takes
-// SPT = 8, PG = 4; the multi-workgroup launch one sample per thread (64-thread workgroups), so each
-// thread's serial work is one descent and one IS-weight pow
+// SPT = 8, PG = 4; the multi-workgroup launch one sample per thread (256-thread workgroups), so
+// each thread's serial work is one descent and one IS-weight pow
 template <int SPT, int PG>
 __global__ void __launch_bounds__(SPT == 1 ? 256 : PER_THREADS) k_per_sample(const double* __restrict__ sum_tree,
                                                            const double* __restrict__ min_tree, int64_t cap,
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(SPT == 1 ? 256 : PER_THREADS) k_per_sample(con
   __shared__ int32_t idx_s[SPT == 1 ? 1 : PER_MAX_B];
   __shared__ double top_s[TOPN];
   const int64_t ntop = cap < TOPN ? cap : TOPN;
-  // multi-workgroup launches: workgroup b takes samples [b * PER_MAX_B/PER_THREADS * blockDim.x, ...)
+  // multi-workgroup launches (SPT = 1): workgroup b takes samples [b * blockDim.x, (b + 1) * blockDim.x)
   // (each stages the top and forms the batch scalars itself; exp_counter then goes to k_per_count)
   const int base = blockIdx.x * SPT * blockDim.x;
   // thread 0 forms the batch scalars from global memory while the others stage the top (the same
@@ -580,8 +580,12 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
 int launch_per_set(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
                    const double* values_d, int n, const float* y_d, const float* V_d, const double* exp_counter_d,
                    double fresh, double eps, double alpha, double* max_priority_d, hipStream_t st) {
+  // k_per_top stages both trees' nroot subtree roots and their parents (4 nroot doubles) in
+  // dynamic LDS, which is 64 KiB per workgroup without an opt-in attribute
+  constexpr int64_t MW_MAX_ROOTS = 2048;
+  static_assert(4 * MW_MAX_ROOTS * sizeof(double) <= 65536, "k_per_top: dynamic LDS above 64 KiB");
   const int64_t sub = std::min<int64_t>(PER_SUB, capacity), nroot = capacity / sub;
-  const bool mw = n >= per_mw_min() && nroot <= 2048;
+  const bool mw = n >= per_mw_min() && nroot <= MW_MAX_ROOTS;
   if (!mw) {
     hipLaunchKernelGGL(k_per_set, dim3(1), dim3(PER_THREADS), 0, st, sum_tree_d, min_tree_d, capacity, idx_d, values_d,
                        n, y_d, V_d, exp_counter_d, fresh, eps, alpha, max_priority_d, 0);

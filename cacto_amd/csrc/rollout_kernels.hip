@@ -26,6 +26,8 @@
 
 #ifdef CACTO_STAMPS
 __device__ unsigned long long g_rstamps[16];
+__device__ unsigned long long g_ttacc[1024 * 2 * 2 * 10];  // [workgroup][team][wave 0/1][phase 0-8, steps]
+__device__ unsigned long long g_wsacc[1024 * 2 * 4 * 7];   // k_rollout_ws: [workgroup][team][wave][phase 0-5, steps]
 #define RSTAMP(k)                                                                     \
   do {                                                                                \
     if (blockIdx.x == 0 && threadIdx.x == 0 && it == 20) g_rstamps[k] = __builtin_amdgcn_s_memtime(); \
@@ -131,6 +133,81 @@ __device__ __forceinline__ float add_from_above(float v, int off) {
   return v + o;
 }
 
+// Layer 2 of the actor (K = 256) for the NG groups of 4 slots: x = h1 (LDS, broadcast layout) ->
+// h2 (LDS, [slot][feature]) for the 64 features of this wave. k = 64 kb + 16 v + q; lane 4q+i
+// reads {x[i][64kb + 16v + q], v = 0..3}.
+template <int NG, int NS, int REGK, int LDSK, bool PF, typename WT>
+__device__ __forceinline__ void ro_layer2(const RoActorRegs<NS, REGK>& R, WT& W, const float* __restrict__ W2g,
+                                          const Lane& L) {
+  using C = RoCfg<NG>;
+  floatx4 acc[NG][2];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) acc[g][0] = acc[g][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int rd = (L.lane >> 2) * 20 + 4 * (L.lane & 3);
+  // PF: LDS operands one step ahead (the next 64-k block's activations, the next 16-row block of
+  // LDS-resident weights), so their latency hides behind the current block's MFMAs. Measured per
+  // system (r03): DI +2.5 %, car_park +2 %, manipulator -3 %, UR5 -20 % (its streamed rows and
+  // chain dynamics need the registers), so only the systems without streamed rows take it.
+  auto lds_w = [&](int k0, float4* wl) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) wl[qq] = W.w2[(((k0 - REGK) / 4 + qq) * 4 + L.wave) * 64 + L.lane];
+  };
+  auto in_lds = [](int k0) { return k0 >= REGK && k0 < REGK + LDSK; };
+  float4 xn[NG], wn[4];
+  if constexpr (PF) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4) * C::H1B + rd]);
+    if (in_lds(0)) lds_w(0, wn);
+  }
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    float4 xv[NG];
+    if constexpr (PF) {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) xv[g] = xn[g];
+      if (kb + 1 < 4)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb + 1) * C::H1B + rd]);
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) xv[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb) * C::H1B + rd]);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int k0 = 64 * kb + 16 * v;  // a 16-row block lies in one residence region
+      float4 wl[4];
+      float wg[16];
+      if (in_lds(k0)) {
+        if constexpr (PF) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) wl[qq] = wn[qq];
+          if (in_lds(k0 + 16)) lds_w(k0 + 16, wn);
+        } else {
+          lds_w(k0, wl);
+        }
+      } else if (k0 >= REGK + LDSK) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) wg[q] = W2g[(k0 + q) * 256 + 64 * L.wave + L.lane];
+      }
+      if constexpr (PF)
+        if (!in_lds(k0) && in_lds(k0 + 16)) lds_w(k0 + 16, wn);
+      static_for<16>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        const int k = k0 + q;
+        const float w = k < REGK ? R.w2[k < REGK ? k : 0] : k < REGK + LDSK ? get4(wl[q >> 2], q & 3) : wg[q];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) acc[g][q & 1] = mfma_bc<q>(get4(xv[g], v), w, acc[g][q & 1]);
+      });
+    }
+  }
+  const int f = 64 * L.wave + L.lane;
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      W.h2[(4 * g + i) * C::H2S + f] = lrelu(fadd(fadd(acc[g][0][i], acc[g][1][i]), R.b2));
+}
+
 // Actor forward of the workgroup's SL slots: x0 -> h1 -> h2 -> a. Contains 3 barriers (the last
 // one publishes W.a).
 template <int NG, int NS, int NA, int REGK, int LDSK, bool PF, typename WT, typename Bar>
@@ -160,75 +237,8 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, WT& W, 
   }
   bar();
   RSTAMP(4);
-  // ---- layer 2 (K = 256): k = 64 kb + 16 v + q; lane 4q+i reads {x[i][64kb + 16v + q], v = 0..3}
-  {
-    floatx4 acc[NG][2];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) acc[g][0] = acc[g][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int rd = (L.lane >> 2) * 20 + 4 * (L.lane & 3);
-    // PF: LDS operands one step ahead (the next 64-k block's activations, the next 16-row block of
-    // LDS-resident weights), so their latency hides behind the current block's MFMAs. Measured per
-    // system (r03): DI +2.5 %, car_park +2 %, manipulator -3 %, UR5 -20 % (its streamed rows and
-    // chain dynamics need the registers), so only the systems without streamed rows take it.
-    auto lds_w = [&](int k0, float4* wl) {
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) wl[qq] = W.w2[(((k0 - REGK) / 4 + qq) * 4 + L.wave) * 64 + L.lane];
-    };
-    auto in_lds = [](int k0) { return k0 >= REGK && k0 < REGK + LDSK; };
-    float4 xn[NG], wn[4];
-    if constexpr (PF) {
-#pragma unroll
-      for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4) * C::H1B + rd]);
-      if (in_lds(0)) lds_w(0, wn);
-    }
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      float4 xv[NG];
-      if constexpr (PF) {
-#pragma unroll
-        for (int g = 0; g < NG; ++g) xv[g] = xn[g];
-        if (kb + 1 < 4)
-#pragma unroll
-          for (int g = 0; g < NG; ++g) xn[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb + 1) * C::H1B + rd]);
-      } else {
-#pragma unroll
-        for (int g = 0; g < NG; ++g) xv[g] = *reinterpret_cast<const float4*>(&W.h1[(g * 4 + kb) * C::H1B + rd]);
-      }
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int k0 = 64 * kb + 16 * v;  // a 16-row block lies in one residence region
-        float4 wl[4];
-        float wg[16];
-        if (in_lds(k0)) {
-          if constexpr (PF) {
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) wl[qq] = wn[qq];
-            if (in_lds(k0 + 16)) lds_w(k0 + 16, wn);
-          } else {
-            lds_w(k0, wl);
-          }
-        } else if (k0 >= REGK + LDSK) {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) wg[q] = W2g[(k0 + q) * 256 + 64 * L.wave + L.lane];
-        }
-        if constexpr (PF)
-          if (!in_lds(k0) && in_lds(k0 + 16)) lds_w(k0 + 16, wn);
-        static_for<16>([&](auto qc) {
-          constexpr int q = decltype(qc)::value;
-          const int k = k0 + q;
-          const float w = k < REGK ? R.w2[k < REGK ? k : 0] : k < REGK + LDSK ? get4(wl[q >> 2], q & 3) : wg[q];
-#pragma unroll
-          for (int g = 0; g < NG; ++g) acc[g][q & 1] = mfma_bc<q>(get4(xv[g], v), w, acc[g][q & 1]);
-        });
-      }
-    }
-    const int f = 64 * L.wave + L.lane;
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        W.h2[(4 * g + i) * C::H2S + f] = lrelu(fadd(fadd(acc[g][0][i], acc[g][1][i]), R.b2));
-  }
+  // ---- layer 2 (K = 256)
+  ro_layer2<NG, NS, REGK, LDSK, PF>(R, W, W2g, L);
   bar();
   RSTAMP(5);
   // ---- layer 3 (256 -> NA): one summation order for every NG (so the schedule never changes a
@@ -891,9 +901,43 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
   do {                                                                                                     \
     if (blockIdx.x == 0 && L.wave == 0 && L.lane == 0 && it == 20) g_rstamps[8 * team + k] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+  // accumulated phase cycles of every step of every team (waves 0 and 1 of the team, lane 0):
+  // [0] layer 1 + its barrier, [1] layer 2 + barrier, [2] layer 3 + barrier, [3] dynamics, stores,
+  // refill (wave 0; the other waves go straight to the barrier), [4] the end-of-step barrier
+  // (wave 0 also splits [3]: [5] action read + s' = f(s, a), [6] trajectory stores, [7] refill,
+  // [8] next input + ballot)
+  unsigned long long tacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, tprev = 0, tsub = 0;
+  int tbi = 0;
+  auto tmark = [&](int ph) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    if (ph == 1) tacc[0] += now - tprev;
+    if (ph == 2) tacc[1] += now - tprev;
+    if (ph == 3) tacc[2] += now - tprev;
+    if (ph == 4) tacc[3] += now - tprev;
+    if (ph == 5) tacc[4] += now - tprev;
+    tprev = now;
+    tsub = now;
+  };
+  auto tsubmark = [&](int k) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    if (k == 5) tacc[5] += now - tsub;
+    if (k == 6) tacc[6] += now - tsub;
+    if (k == 7) tacc[7] += now - tsub;
+    if (k == 8) tacc[8] += now - tsub;
+    tsub = now;
+  };
+#define TSUB(k) tsubmark(k)
+  auto sbar = [&] {
+    tbar();
+    tmark(++tbi);
+  };
+  int tsteps = 0;
 #else
 #define TSTAMP(k) \
   do {            \
+  } while (0)
+#define TSUB(k) \
+  do {          \
   } while (0)
 #endif
   for (int it = 0; S.anyact; ++it) {
@@ -903,7 +947,13 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
     // does: a counter barrier, unlike s_barrier, would wait forever for waves that left the loop on
     // an anyact they read too late.
     if (!use_actor) tbar();
+#ifdef CACTO_STAMPS
+    tbi = 0;
+    tmark(0);
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true>(R, V, W2g, L, it, sbar);
+#else
     if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true>(R, V, W2g, L, it, tbar);
+#endif
     TSTAMP(1);
     if (L.wave == 0) {
       const bool active = L.lane < SL && sr.act;
@@ -925,22 +975,312 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
           S.sS[c * ns + i] = sn[i];
           sr.s[i] = sn[i];
         }
+      }
+      TSUB(5);
+      if (active) {
         fin = ro_advance<NJ, NG>(c, sr.b, sr.t, sr.s, a, sd, T, Straj, Atraj, status, nrm, sr.n);
         sr.t += 1;
       }
+      TSUB(6);
       ro_refill<NJ, NG, RoTeamShared<NJ>, false>(fin, c, head, S, sd, S0, nsteps, order, T, B, G, Straj, status, nrm,
                                                   L, vb);
       if (fin) sr.load(S, c, false);
+      TSUB(7);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       x0l.write(S, nrm, L.lane);
       const uint64_t m = __ballot(L.lane < SL && S.sact[c]);
       if (L.lane == 0) S.anyact = m != 0;
+      TSUB(8);
       TSTAMP(2);
     }
+#ifdef CACTO_STAMPS
+    tmark(4);
+#endif
     tbar();
     TSTAMP(3);
+#ifdef CACTO_STAMPS
+    tmark(5);
+    ++tsteps;
+#endif
   }
+#ifdef CACTO_STAMPS
+  if (L.lane == 0 && L.wave < 2) {
+    unsigned long long* o = g_ttacc + ((size_t)(blockIdx.x * 2 + team) * 2 + L.wave) * 10;
+    for (int k = 0; k < 9; ++k) o[k] = tacc[k];
+    o[9] = tsteps;
+  }
+#endif
 #undef TSTAMP
+#undef TSUB
+}
+
+// ---------------------------------------------------------------- one episode slot per wave
+// k_rollout_ws: the two-team layout of k_rollout_tt (two 4-wave teams of 4 slots per workgroup,
+// team barriers, layer-2 rows shared in LDS), but each wave of a team OWNS one slot and runs that
+// slot's whole sequential chain itself: after layer 2 (all 4 waves, 64 features each, every slot)
+// wave w forms its slot's action (layer 3 — the same 64 lane chains and butterfly as ro_actor,
+// whose P = 64 threads per slot are exactly one wave), steps the dynamics, writes the trajectory,
+// refills its slot from the team's queue, normalises s_{t+1} and evaluates layer 1 of its slot
+// for all 256 features (VALU fmaf chains in q order: a K = 1 MFMA step rounds exactly like fmaf,
+// tools/mb/mfma_fma.hip) straight into the layer-2 operand layout. Per step: two team barriers
+// (h2 published, h1 published) instead of four, and the four slots' serial chains run on four
+// waves side by side instead of on four lanes of one wave. Every per-slot operation is the one
+// the other rollout kernels perform, so outputs are bit-identical to them; which slot runs an
+// episode (queue entries taken by an LDS counter) does not change its result.
+// x[lane] for lanes < N (x uniform across the wave) as a select chain kept in VGPRs: without the
+// empty asm the optimiser turns the chain into an indexed load from a scratch copy of x.
+template <int N, typename V>
+__device__ __forceinline__ V lane_pick(const V* x, int lane) {
+  V v = x[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
+    v = lane == i ? x[i] : v;
+    __asm__ volatile("" : "+v"(v));
+  }
+  return v;
+}
+
+template <int NJ>
+struct RoWsTeam {
+  float h1[4 * RoCfg<1>::H1B];  // layer-1 output of the 4 slots, layer-2 broadcast layout
+  float h2[4 * RoCfg<1>::H2S];  // layer-2 output [slot][feature]
+  int act[4];                   // slot active flags, published by the barrier that ends a step
+  int qhead;                    // the team's next queue entry
+  int bar;                      // team barrier arrivals
+};
+
+template <int NJ>
+struct RoWsShared {
+  float4 w2[RoSplitTT::LDSK / 4 * 4 * 64];
+  RoWsTeam<NJ> team[2];
+};
+
+template <int NJ>
+__global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
+    k_rollout_ws(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
+                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
+                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  constexpr int REGK = RoSplitTT::REGK, LDSK = RoSplitTT::LDSK;
+  using C = RoCfg<1>;
+  __shared__ RoWsShared<NJ> Sh;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const int team = threadIdx.x >> 8;
+  Lane L;
+  // team-local wave (team 1's wave 0 is the workgroup's wave 7: the two teams' wave w sit on
+  // different SIMDs) and thread index; wave w owns slot w
+  L.wave = (L.wave + team) & 3;
+  L.tid = L.wave * 64 + L.lane;
+  const int w = L.wave, lane = L.lane;
+  RoWsTeam<NJ>& S = Sh.team[team];
+  RoActorRegs<ns, REGK> R;
+  float w1[ns][4], b1[4], w3[na][4], b3[na];
+  if (use_actor) {
+    const float* W1 = N.flat + N.t.woff[0];
+    const float* W2 = N.flat + N.t.woff[1];
+    const float* W3 = N.flat + N.t.woff[2];
+    const int f = 64 * w + lane;
+#pragma unroll
+    for (int k = 0; k < REGK; ++k) R.w2[k] = W2[k * 256 + f];
+    R.b2 = N.bias(1, f);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int q = 0; q < ns; ++q) w1[q][m] = W1[q * 256 + lane + 64 * m];
+      b1[m] = N.bias(0, lane + 64 * m);
+#pragma unroll
+      for (int a = 0; a < na; ++a) w3[a][m] = W3[(lane + 64 * m) * na + a];
+    }
+#pragma unroll
+    for (int a = 0; a < na; ++a) b3[a] = N.bias(2, a);
+    for (int e = threadIdx.x; e < LDSK * 64; e += 2 * CACTO_THREADS) {
+      const int ln = e & 63, wv = (e >> 6) & 3, kq = e >> 8;
+      const int k = REGK + 4 * kq, col = 64 * wv + ln;
+      Sh.w2[e] = make_float4(W2[k * 256 + col], W2[(k + 1) * 256 + col], W2[(k + 2) * 256 + col],
+                             W2[(k + 3) * 256 + col]);
+    }
+  }
+  for (int e = L.tid; e < 4 * C::H1B; e += CACTO_THREADS) S.h1[e] = 0.f;
+  if (L.tid == 0) {
+    S.bar = 0;
+    S.qhead = 0;
+  }
+  __syncthreads();  // the only workgroup barrier: weights and team state in place
+  RoTeamBar tbar{&S.bar, 0, lane};
+  const int vb = 2 * (int)blockIdx.x + team, G = 2 * (int)gridDim.x;
+  // the normalisation of feature `lane` (lanes < ns), fixed for the launch: one division per lane
+  // per step instead of ns in sequence (RoNorm's arithmetic)
+  const RoNorm<ns> nrm(p);
+  float nl = 1.f;
+#pragma unroll
+  for (int q = 0; q < ns; ++q) nl = lane == q ? nrm.n[q] : nl;
+  const bool tl = lane == ns - 1;
+  ConstDyn<NJ> cd;
+  if constexpr (NJ > 0) {
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = sd.cd_L[k];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) cd.h[i] = sd.cd_h[i];
+  }
+  // the slot (wave-uniform): active, episode, length, step, s_t
+  bool act = false;
+  int b = 0, n = 0, t = 0;
+  double s[ns];
+#pragma unroll
+  for (int i = 0; i < ns; ++i) s[i] = 0.0;
+
+  // the next queue entries of the team until one has steps (ro_refill's dealing: snake order over
+  // the virtual workgroups vb; zero-length episodes completed on the spot)
+  auto refill = [&]() {
+    act = false;
+    while (true) {
+      int k = 0;
+      if (lane == 0) k = __hip_atomic_fetch_add(&S.qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      k = __builtin_amdgcn_readfirstlane(k);
+      const int r = k * G + ((k & 1) ? G - 1 - vb : vb);
+      if (r >= B) return;
+      const int bb = __builtin_amdgcn_readfirstlane(order ? order[r] : r);
+      const int nn = min(nsteps[bb], T);
+#pragma unroll
+      for (int i = 0; i < ns; ++i) s[i] = S0[(size_t)bb * ns + i];
+      if (Straj && lane < ns) Straj[(size_t)bb * (T + 1) * ns + lane] = lane_pick<ns>(s, lane);
+      if (nn == 0) {
+        if (status && lane == 0) status[bb] = 0;
+        continue;
+      }
+      b = bb;
+      n = nn;
+      t = 0;
+      act = true;
+      return;
+    }
+  };
+  // layer 1 of this wave's slot from s_t: x0[q] = normalise(s_t[q]) on lane q, broadcast through
+  // readlane; h1[k] = lrelu(b1[k] + sum_q x0[q] W1[q][k]) for k = lane + 64 m, written to the
+  // slot's column of the layer-2 operand layout (block m, q = lane & 15, v = lane >> 4)
+  auto layer1 = [&]() {
+    const double sv = lane_pick<ns>(s, lane);
+    const float qv = fdiv((float)sv, nl);
+    const float xv = nrm.on ? (tl ? fsub(fmul(qv, 2.0f), 1.0f) : qv) : (float)sv;
+    float x0[ns];
+#pragma unroll
+    for (int q = 0; q < ns; ++q) x0[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), q));
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], w1[q][m], acc);
+      S.h1[m * C::H1B + (lane & 15) * 20 + 4 * w + (lane >> 4)] = lrelu(fadd(acc, b1[m]));
+    }
+  };
+
+#ifdef CACTO_STAMPS
+  // accumulated phase cycles of every step (lane 0 of each wave): [0] loop test + layer 2 + its
+  // barrier, [1] layer 3, [2] s' = f(s, a) + trajectory stores, [3] refill, [4] layer 1, [5] the
+  // end-of-step barrier
+  unsigned long long wacc[6] = {0, 0, 0, 0, 0, 0}, wprev = __builtin_amdgcn_s_memtime();
+  int wsteps = 0;
+  auto wmark = [&](int ph) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (k == ph) wacc[k] += now - wprev;
+    wprev = now;
+  };
+#define WMARK(k) wmark(k)
+#else
+#define WMARK(k) \
+  do {           \
+  } while (0)
+#endif
+
+  refill();
+  if (act && use_actor) layer1();
+  if (lane == 0) S.act[w] = act;
+  tbar();
+  const float* W2g = N.flat + N.t.woff[1];
+  RoTeamView<na> V{Sh.w2, nullptr, nullptr, S.h1, S.h2, nullptr, nullptr};
+  for (int it = 0;; ++it) {
+    if ((S.act[0] | S.act[1] | S.act[2] | S.act[3]) == 0) break;
+    // every wave has read the flags (above) before any wave rewrites its own below: the layer-2
+    // barrier orders that; without the actor this barrier does
+    if (!use_actor) tbar();
+    float a[na];
+#pragma unroll
+    for (int i = 0; i < na; ++i) a[i] = 0.f;
+    if (use_actor) {
+      ro_layer2<1, ns, REGK, LDSK, true>(R, V, W2g, L);
+      tbar();
+      WMARK(0);
+      if (act) {
+        // layer 3 of slot w: lane j's chain over features j, j + 64, j + 128, j + 192, then the
+        // butterfly over the lanes (ro_actor's order with P = 64)
+        float pa[na];
+#pragma unroll
+        for (int i = 0; i < na; ++i) pa[i] = 0.f;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float h = S.h2[w * C::H2S + lane + 64 * m];
+#pragma unroll
+          for (int i = 0; i < na; ++i) pa[i] = fmaf(w3[i][m], h, pa[i]);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+          for (int i = 0; i < na; ++i) pa[i] = add_from_above(pa[i], off);
+#pragma unroll
+        for (int i = 0; i < na; ++i) a[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fadd(pa[i], b3[i]))));
+      }
+      WMARK(1);
+    }
+    bool fin = false;
+    if (act) {
+      double ad[na], sn[ns];
+#pragma unroll
+      for (int i = 0; i < na; ++i) ad[i] = (double)a[i];
+      if constexpr (NJ > 0)
+        env_simulate_const<NJ>(sd, cd, s, ad, sn);
+      else
+        env_simulate<NJ>(sd, s, ad, false, sn);
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
+      // the trajectory stores of (a_t, s_{t+1}): one component per lane
+      if (Atraj && lane < na) Atraj[((size_t)b * T + t) * na + lane] = lane_pick<na>(a, lane);
+      if (Straj && lane < ns) Straj[((size_t)b * (T + 1) + t + 1) * ns + lane] = lane_pick<ns>(sn, lane);
+      if (bad && Straj) {
+        // RL.py:229-231 drops the episode; the rest of its trajectory is NaN (the reward / EE pass
+        // skips NaN states)
+        for (int e = lane; e < (n - t - 1) * ns; e += 64)
+          Straj[((size_t)b * (T + 1) + t + 2) * ns + e] = __builtin_nan("");
+      }
+      fin = bad || t + 1 >= n;
+      if (fin && status && lane == 0) status[b] = bad ? 1 : 0;
+#pragma unroll
+      for (int i = 0; i < ns; ++i) s[i] = sn[i];
+      t += 1;
+    }
+    WMARK(2);
+    if (fin) refill();
+    WMARK(3);
+    if (act && use_actor) layer1();
+    if (lane == 0) S.act[w] = act;
+    WMARK(4);
+    tbar();
+    WMARK(5);
+#ifdef CACTO_STAMPS
+    ++wsteps;
+#endif
+  }
+#ifdef CACTO_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_wsacc + ((size_t)(blockIdx.x * 2 + team) * 4 + w) * 7;
+    for (int k = 0; k < 6; ++k) o[k] = wacc[k];
+    o[6] = wsteps;
+  }
+#endif
+#undef WMARK
 }
 
 // Rewards and end-effector positions of every recorded step (Env.step's reward and
@@ -1132,9 +1472,20 @@ struct LaunchRollout {
     // automatic only where it measured faster: the prismatic chain (DI 0.75 -> 0.72 ms at 4096
     // episodes); car_park's step was slower on two teams (0.42 -> 0.50 ms)
     const bool tt_auto = tt_sys && NJ > 0;
-    if (groups == -1 && !tt_sys) {
-      set_error("cacto_rollout_sched: groups -1 (two teams) needs a system without configuration-dependent M");
+    if ((groups == -1 || groups == -2) && !tt_sys) {
+      set_error("cacto_rollout_sched: groups -1 / -2 (two teams) need a system without configuration-dependent M");
       return CACTO_EINVAL;
+    }
+    if (groups == -2) {
+      // one slot per wave (k_rollout_ws)
+      if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
+      wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
+      if constexpr (tt_ok)
+        hipLaunchKernelGGL(k_rollout_ws<NJ>, dim3(wgs), dim3(2 * CACTO_THREADS), 0, st, sys->dev, v, S0, n, T,
+                           use_actor, S, A, status, order, B);
+      CACTO_CHECK_HIP(hipGetLastError());
+      if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
+      return CACTO_OK;
     }
     if (tt_sys && (groups == -1 || (tt_auto && groups == 0 && B / (2 * 4 * cus) == 2))) {
       if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
@@ -1190,6 +1541,18 @@ extern "C" int cacto_debug_rollout_stamps(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 16));
   return CACTO_OK;
 }
+// k_rollout_ws's accumulated phase cycles: 1024 x 2 x 4 x 7 values (see the kernel)
+extern "C" int cacto_debug_rollout_ws_acc(unsigned long long* out_h) {
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_wsacc), sizeof(unsigned long long) * 1024 * 2 * 4 * 7));
+  return CACTO_OK;
+}
+// k_rollout_tt's accumulated phase cycles: 1024 x 2 x 2 x 10 values (see the kernel)
+extern "C" int cacto_debug_rollout_tt_acc(unsigned long long* out_h) {
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_ttacc), sizeof(unsigned long long) * 1024 * 2 * 2 * 10));
+  return CACTO_OK;
+}
 #endif
 
 extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,
@@ -1198,8 +1561,8 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
                                    const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
-  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1,
-                "cacto_rollout_sched: groups must be 0, 1, 2, 4 or -1 (two teams)");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -2,
+                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams) or -2 (one slot per wave)");
   CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
   CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
                 "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");

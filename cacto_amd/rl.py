@@ -296,13 +296,21 @@ class RL_AC:
                 raise RuntimeError("capture_updates: a data-parallel loop is captured only over RCCL (backend "
                                    "'nccl'), not %r" % dist.get_backend(self.dp_group))
             self._dp_grad_buf(self.critic_model.P + self.actor_model.P)
+            keep = None
+            if per_buffer is not None:
+                # the uniforms on the device before the capture (a host tensor cannot be copied inside
+                # it), and the loop's y / V allocated here and kept alive with the graph
+                uniforms = uniforms.to(device=DEVICE, dtype=torch.float64).contiguous()
+                keep = (uniforms, torch.empty(B, dtype=torch.float32, device=DEVICE),
+                        torch.empty(B, dtype=torch.float32, device=DEVICE))
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 if per_buffer is None:
                     self._update_rows_n_dp(storage, idx_steps)
                 else:
-                    self.update_rows_n_per_dp(per_buffer, uniforms)
+                    self.update_rows_n_per_dp(per_buffer, keep[0], y=keep[1], V=keep[2])
+            g.keep = keep
             return g
         y = torch.empty(B, dtype=torch.float32, device=DEVICE)
         V = torch.empty_like(y)
@@ -373,13 +381,15 @@ class RL_AC:
                 after_critic(step)
         return apply
 
-    def update_rows_n_per_dp(self, buffer, uniforms):
+    def update_rows_n_per_dp(self, buffer, uniforms, y=None, V=None):
         """K data-parallel PER updates (RL.py:122-137 on every rank's replay shard, the sampling of
         replay_buffer.py:139-188 over the union of the shards) in the paired schedule of
         dp_pipeline: step t samples update t (one all-gather of the shards' (sum, min, rows), then
         the stratified sample and IS weights, all on the device), computes [critic gradient of
-        update t | actor gradient of update t - 1] into one buffer, all-reduces it ONCE, applies
-        both Adam steps, then updates the local priorities of update t. uniforms [K, B] (this
+        update t | actor gradient of update t - 1] into one buffer in two stages — the critic part's
+        async all-reduce is issued before the actor part is formed, the actor part's after it —
+        applies the critic's Adam step once its exchange is done (then the local priorities of
+        update t), and the actor's once its own is. uniforms [K, B] (this
         rank's random.random() draws, in order) go to the device in one copy. Every kernel sees the
         inputs of the sequential loop (sample -> update -> priorities), so the result equals K
         update_rows + update_priorities_device calls (bit for bit when the collective's sums are
@@ -391,8 +401,8 @@ class RL_AC:
         cfg = self._cfg_for(B)
         Pc, Pa = self.critic_model.P, self.actor_model.P
         g = self._dp_grad_buf(Pc + Pa)
-        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
-        V = torch.empty_like(y)
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE) if y is None else y
+        V = torch.empty_like(y) if V is None else V
         drawn = {}
 
         def stages(c, a):

@@ -426,3 +426,62 @@ def test_dp_loop_over_rccl_is_graph_capturable():
         assert np.array_equal(a, b) and np.array_equal(b, c)
     for a, b in zip(eager2, graphed2):
         assert np.array_equal(a, b)
+
+
+def _rccl_per_worker(rank, port, rows, U, q):
+    """One rank over RCCL: the data-parallel PER loop (update_rows_n_per_dp: shard-stats
+    all-gather, stratified sample, staged gradients, priority updates) eager and captured."""
+    import torch.distributed as dist
+    from cacto_amd.confs import load_conf
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    try:
+        conf = load_conf("double_integrator", fresh=True)
+        conf.prioritized_replay_alpha = 0.6
+        conf.BATCH_SIZE = U.shape[1]
+        out = []
+        for graphed in (False, True):
+            rl = _learner(1)
+            rl.set_data_parallel(1, dist.group.WORLD)
+            buf = PrioritizedReplayBuffer(conf, rl.sys)
+            buf.set_data_parallel(1, dist.group.WORLD)
+            buf.add_rows(rows)
+            Ud = torch.as_tensor(U, device="cuda")
+            if graphed:
+                g = rl.capture_updates(None, None, per_buffer=buf, uniforms=Ud)
+                g.replay()
+            else:
+                rl.update_rows_n_per_dp(buf, Ud)
+            torch.cuda.synchronize()
+            out.append((_state(rl), rl.steps.cpu().tolist(), buf.sum_tree.cpu().numpy(), buf.min_tree.cpu().numpy(),
+                        buf.exp_counter.cpu().numpy(), float(buf.max_priority.item())))
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_per_loop_over_rccl_is_graph_capturable():
+    """capture_updates(per_buffer=...) of the data-parallel PER loop over RCCL (one rank): the
+    replayed graph equals the eager update_rows_n_per_dp bit for bit — weights, moments, counters,
+    both trees, exp_counter, max_priority."""
+    import torch.multiprocessing as mp
+    rows = _rows(1500, 93)
+    U = np.random.default_rng(94).uniform(size=(5, 64))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_per_worker, args=(0, _free_port(), rows, U, q))
+    p.start()
+    try:
+        eager, graphed = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert p.exitcode == 0
+    assert eager[1] == graphed[1] == [5, 5]
+    for a, b in zip(eager[0], graphed[0]):
+        assert np.array_equal(a, b)
+    for a, b in zip(eager[2:5], graphed[2:5]):
+        assert np.array_equal(a, b)
+    assert eager[5] == graphed[5]
