@@ -670,6 +670,64 @@ extern "C" int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t 
                         alpha, max_priority_d, as_stream(stream));
 }
 
+// update_priorities 'ReLO' (replay_buffer.py:193-196, :200-218; dead in the shipped reference,
+// RB_type is never set): td_i = MSE(y, V)_i - MSE(y, V_tgt)_i with Keras MeanSquaredError
+// (reduction NONE, so per sample: f32 (V - y)^2 over the size-1 last axis), clipped as numpy clips
+// it, np.minimum(np.maximum(td, 0), max(td)); then p = fresh^count (f64) * td_norm (f32 -> f64, numpy
+// promotion) + eps in f64 — unlike the 'PER' branch, whose TF tensor keeps p in f32. One workgroup
+// (B <= PER_MAX_B): the per-sample leaves p^alpha go to leaves[], max_priority takes the batch max.
+__global__ void __launch_bounds__(PER_THREADS) k_per_relo(const int32_t* __restrict__ idx, const float* __restrict__ y,
+                                                         const float* __restrict__ V, const float* __restrict__ Vt,
+                                                         const double* __restrict__ exp_counter, double fresh,
+                                                         double eps, double alpha, int B, double* __restrict__ leaves,
+                                                         double* __restrict__ max_priority) {
+  __shared__ float red_f[PER_THREADS / 64];
+  __shared__ double red_d[PER_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  auto td_of = [&](int i) {
+    const float d1 = __fsub_rn(V[i], y[i]), d2 = __fsub_rn(Vt[i], y[i]);
+    return __fsub_rn(__fmul_rn(d1, d1), __fmul_rn(d2, d2));
+  };
+  float mx = -__builtin_inff();
+  for (int i = tid; i < B; i += blockDim.x) mx = fmaxf(mx, td_of(i));
+  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  if (lane == 0) red_f[wv] = mx;
+  __syncthreads();
+  mx = red_f[0];
+  for (int k = 1; k < (int)(blockDim.x / 64); ++k) mx = fmaxf(mx, red_f[k]);
+  double pm = -__builtin_inf();
+  for (int i = tid; i < B; i += blockDim.x) {
+    const float tn = fminf(fmaxf(td_of(i), 0.f), mx);
+    const double p = pow(fresh, exp_counter[idx[i]]) * (double)tn + eps;
+    leaves[i] = pow(p, alpha);
+    pm = fmax(pm, p);
+  }
+  for (int off = 32; off > 0; off >>= 1) pm = fmax(pm, __shfl_xor(pm, off));
+  if (lane == 0) red_d[wv] = pm;
+  __syncthreads();
+  if (tid == 0) {
+    double m = max_priority[0];
+    for (int k = 0; k < (int)(blockDim.x / 64); ++k) m = fmax(m, red_d[k]);
+    max_priority[0] = m;
+  }
+}
+
+extern "C" int cacto_per_update_relo(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                                     const float* y_d, const float* V_d, const float* Vt_d,
+                                     const double* exp_counter_d, double fresh_factor, double eps, double alpha,
+                                     double* max_priority_d, double* leaves_ws_d, int B, void* stream) {
+  CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && y_d && V_d && Vt_d && exp_counter_d && max_priority_d &&
+                    leaves_ws_d && pow2(capacity),
+                "cacto_per_update_relo: bad arguments");
+  CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_update_relo: 0 < B <= 8192");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(k_per_relo, dim3(1), dim3(PER_THREADS), 0, st, idx_d, y_d, V_d, Vt_d, exp_counter_d, fresh_factor,
+                     eps, alpha, B, leaves_ws_d, max_priority_d);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return launch_per_set(sum_tree_d, min_tree_d, capacity, idx_d, leaves_ws_d, B, nullptr, nullptr, nullptr, 0.0, 0.0,
+                        0.0, nullptr, st);
+}
+
 extern "C" int cacto_per_set_leaves(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
                                     const double* values_d, int n, void* stream) {
   CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && values_d && pow2(capacity), "cacto_per_set_leaves: bad arguments");

@@ -169,6 +169,10 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         self.eps = float(conf.prioritized_replay_eps)
         self.fresh = float(conf.fresh_factor)
         self.random = py_random or random  # replay_buffer.py:150 uses the global `random`
+        # replay_buffer.py:118 (commented out there, so 'PER'); 'ReLO' selects the other priority
+        # rule of update_priorities (replay_buffer.py:193-196)
+        self.RB_type = getattr(conf, "RB_type", "PER")
+        self._relo_ws = None
 
     def _rows_added(self, start, n):
         # leaves = max_priority ** alpha (replay_buffer.py:133-135) with the host's Python float
@@ -223,19 +227,31 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         s, r, sn, dv, d, term = self.gather(idx)
         return s, r, sn, dv, d, term, w.reshape(-1, 1), idx
 
-    def update_priorities_device(self, idx, y, V):
+    def update_priorities_device(self, idx, y, V, Vt=None):
         B = idx.shape[0]
+        if self.RB_type == "ReLO":
+            if Vt is None:
+                raise ValueError("update_priorities with RB_type 'ReLO' needs target_critic_value")
+            if self._relo_ws is None or self._relo_ws.numel() < B:
+                self._relo_ws = torch.empty(B, dtype=torch.float64, device=DEVICE)
+            L.lib().call("cacto_per_update_relo", dptr(self.sum_tree), dptr(self.min_tree), self.cap,
+                         dptr(idx, torch.int32), dptr(y.reshape(-1).contiguous(), torch.float32),
+                         dptr(V.reshape(-1).contiguous(), torch.float32),
+                         dptr(Vt.reshape(-1).contiguous(), torch.float32), dptr(self.exp_counter), self.fresh,
+                         self.eps, self.alpha, dptr(self.max_priority), dptr(self._relo_ws), B, stream())
+            return
         L.lib().call("cacto_per_update", dptr(self.sum_tree), dptr(self.min_tree), self.cap, dptr(idx, torch.int32),
                      dptr(y.reshape(-1).contiguous(), torch.float32), dptr(V.reshape(-1).contiguous(), torch.float32),
                      dptr(self.exp_counter), self.fresh, self.eps, self.alpha, dptr(self.max_priority), B, stream())
 
     def update_priorities(self, idxes, reward_to_go_batch, critic_value, target_critic_value=None):
-        """replay_buffer.py:190-218 ('PER')."""
+        """replay_buffer.py:190-218 (RB_type 'PER', or 'ReLO' with target_critic_value)."""
         idx = torch.as_tensor(np.asarray(idxes, dtype=np.int32) if not isinstance(idxes, torch.Tensor) else idxes,
                               dtype=torch.int32, device=DEVICE).contiguous()
         f32 = lambda x: torch.as_tensor(np.asarray(x) if not isinstance(x, torch.Tensor) else x, dtype=torch.float32,
                                         device=DEVICE).reshape(-1).contiguous()
-        self.update_priorities_device(idx, f32(reward_to_go_batch), f32(critic_value))
+        self.update_priorities_device(idx, f32(reward_to_go_batch), f32(critic_value),
+                                      None if target_critic_value is None else f32(target_critic_value))
 
     def set_leaves(self, idx, values):
         idx = torch.as_tensor(np.asarray(idx, dtype=np.int32), device=DEVICE)

@@ -451,6 +451,8 @@ class RL_AC:
         n = int(self.conf.UPDATE_LOOPS[ep])
         B = self.conf.BATCH_SIZE
         per = getattr(buffer, "prioritized", False)
+        if per and getattr(buffer, "RB_type", "PER") == "ReLO":
+            return self._learn_and_update_relo(update_step_counter, buffer, n, B)
         if per:
             if self._dp and (buffer.dp_world, buffer.dp_group) != (self.dp_world, self.dp_group):
                 buffer.set_data_parallel(self.dp_world, self.dp_group)
@@ -477,6 +479,22 @@ class RL_AC:
             for _ in range(k):
                 update_step_counter = self._after_step(update_step_counter)
             i += k
+        return update_step_counter
+
+    def _learn_and_update_relo(self, update_step_counter, buffer, n, B):
+        """RL.py:120-143 with RB_type 'ReLO' (replay_buffer.py:193-196): the priority rule needs
+        V_tgt(s) from the update (want_target_V), so the loop runs update by update — sample,
+        update (with y, V, V_tgt), priorities — instead of the pipelined PER call."""
+        if self._dp and (buffer.dp_world, buffer.dp_group) != (self.dp_world, self.dp_group):
+            buffer.set_data_parallel(self.dp_world, self.dp_group)
+        y = torch.empty(B, dtype=torch.float32, device=DEVICE)
+        V, Vt = torch.empty_like(y), torch.empty_like(y)
+        for _ in range(n):
+            U = torch.as_tensor(np.array([buffer.random.random() for _ in range(B)], dtype=np.float64), device=DEVICE)
+            idx, w = buffer.sample_device(U)
+            self.update_rows(buffer.storage, idx, w, y, V, Vt)
+            buffer.update_priorities_device(idx, y, V, Vt)
+            update_step_counter = self._after_step(update_step_counter)
         return update_step_counter
 
     def _after_step(self, counter):

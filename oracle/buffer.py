@@ -179,6 +179,24 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         pr = np.array([self.it_sum[int(i)] for i in idxes]) / self.it_sum.sum()
         return (pr * scale) ** (-self.beta) / max_weight
 
+    def update_priorities_relo(self, idxes, y, V, Vt):
+        """replay_buffer.py:193-196 + :200-218 ('ReLO' branch): Keras MeanSquaredError with reduction
+        NONE gives the per-sample f32 (V - y)^2; td = MSE(y, V) - MSE(y, V_tgt) (numpy f32);
+        td_norm = np.clip(td, 0, np.max(td)); p = fresh^count (f64) * td_norm (f32, promoted) + eps
+        — numpy arithmetic, so p is f64 here (the 'PER' branch multiplies a TF f32 tensor)."""
+        f32 = np.float32
+        y, V, Vt = (np.asarray(a, dtype=f32).reshape(-1) for a in (y, V, Vt))
+        td = (V - y) * (V - y) - (Vt - y) * (Vt - y)
+        td_norm = np.clip(td, 0, np.max(td))
+        new_p = self.fresh ** self.exp_counter[np.asarray(idxes)] * td_norm + self.eps
+        for idx, p in zip(idxes, new_p):
+            assert p > 0
+            leaf = p ** self.alpha
+            self.it_sum[int(idx)] = float(leaf)
+            self.it_min[int(idx)] = float(leaf)
+            self.max_priority = max(self.max_priority, float(p))
+        return new_p
+
     def update_priorities(self, idxes, y, V):
         """replay_buffer.py:190-218 ('PER' branch): p = fresh^count * |y - V| + eps.
         The reference multiplies a float64 numpy array by float32 TF tensors, so p is a float32

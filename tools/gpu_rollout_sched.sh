@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ws
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_nan_abort.py tests/test_gpu_dp.py -k "rollout or status or kept or ep0 or rccl" > gpurun_out/ws/tests.log 2>&1 &&
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_nan_abort.py tests/test_gpu_dp.py tests/test_gpu_relo.py -k "rollout or status or kept or ep0 or rccl or relo" > gpurun_out/ws/tests.log 2>&1 &&
 timeout -k 10 120 python -u tools/ro_sched.py double_integrator 4096 "0,0 -1,0 -2,0 2,0" > gpurun_out/ws/sched.log 2>&1 &&
 timeout -k 10 120 python -u tools/ro_sched.py car_park 4096 "0,0 -1,0 -2,0" >> gpurun_out/ws/sched.log 2>&1 &&
 timeout -k 10 120 python -u tools/ro_sched.py single_integrator 4096 "0,0 -1,0 -2,0" >> gpurun_out/ws/sched.log 2>&1 &&
