@@ -25,7 +25,7 @@
 #include "net_common.h"
 
 #ifdef CACTO_STAMPS
-__device__ unsigned long long g_rstamps[16];
+__device__ unsigned long long g_rstamps[20];
 __device__ unsigned long long g_ttacc[1024 * 2 * 2 * 10];  // [workgroup][team][wave 0/1][phase 0-8, steps]
 __device__ unsigned long long g_wsacc[1024 * 2 * 4 * 7];   // k_rollout_ws: [workgroup][team][wave][phase 0-5, steps]
 #define RSTAMP(k)                                                                     \
@@ -734,6 +734,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         x0l.write(Sh, nrm, L.lane);
       }
+      RSTAMP(16);
       if (active) {
         fin = ro_advance<NJ, NG>(c, sr.b, sr.t, sr.s, a, sd, T, Straj, Atraj, status, nrm, sr.n);
         sr.t += 1;
@@ -1040,6 +1041,9 @@ __device__ __forceinline__ V lane_pick(const V* x, int lane) {
   return v;
 }
 
+#ifndef RO_WS_SWAP
+#define RO_WS_SWAP 1  // k_rollout_ws layer 3: both actions in one permlane butterfly (0: per action)
+#endif
 template <int NJ>
 struct RoWsTeam {
   float h1[4 * RoCfg<1>::H1B];  // layer-1 output of the 4 slots, layer-2 broadcast layout
@@ -1225,12 +1229,29 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
 #pragma unroll
           for (int i = 0; i < na; ++i) pa[i] = fmaf(w3[i][m], h, pa[i]);
         }
+        if constexpr (na == 2 && RO_WS_SWAP) {
+          // both actions in one butterfly: v_permlane32_swap leaves lane j < 32 with
+          // pa0[j] + pa0[j + 32] and lane 32 + j with pa1[j] + pa1[j + 32], v_permlane16_swap then
+          // adds row r + 1 into row r of each half, and the row-local DPP levels finish: action 0's
+          // sum on lane 0, action 1's on lane 32. Every add is v[j] + v[j + off], in the order
+          // add_from_above forms it, so the sums are bit-identical (all VALU, no LDS round trip).
+          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[0]), __float_as_uint(pa[1]), false, false);
+          float v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+          v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1)
+          for (int off = 8; off >= 1; off >>= 1) v = add_from_above(v, off);
+          a[0] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)), b3[0]);
+          a[1] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)), b3[1 % na]);
+        } else {
 #pragma unroll
-          for (int i = 0; i < na; ++i) pa[i] = add_from_above(pa[i], off);
+          for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-        for (int i = 0; i < na; ++i) a[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fadd(pa[i], b3[i]))));
+            for (int i = 0; i < na; ++i) pa[i] = add_from_above(pa[i], off);
+#pragma unroll
+          for (int i = 0; i < na; ++i)
+            a[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fadd(pa[i], b3[i]))));
+        }
       }
       WMARK(1);
     }
@@ -1476,8 +1497,12 @@ struct LaunchRollout {
       set_error("cacto_rollout_sched: groups -1 / -2 (two teams) need a system without configuration-dependent M");
       return CACTO_EINVAL;
     }
-    if (groups == -2) {
-      // one slot per wave (k_rollout_ws)
+    // one slot per wave (k_rollout_ws) where it measured faster: the prismatic chain (DI 4096
+    // episodes: 0.725 -> 0.632 ms against k_rollout_tt) and the single integrator (0.366 -> 0.322
+    // ms); car / car_park keep the single-team kernel (their f64 trigonometry per step on one
+    // wave's chain measured slower: 1.84 -> 1.88 / 0.43 -> 0.51 ms). Up to two episodes per slot.
+    const bool ws_auto = tt_sys && NJ >= 0 && B <= 2 * 8 * cus;
+    if (groups == -2 || (groups == 0 && ws_auto)) {
       if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
       wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
       if constexpr (tt_ok)
@@ -1538,7 +1563,7 @@ struct LaunchRollout {
 #ifdef CACTO_STAMPS
 extern "C" int cacto_debug_rollout_stamps(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipDeviceSynchronize());
-  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 16));
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 20));
   return CACTO_OK;
 }
 // k_rollout_ws's accumulated phase cycles: 1024 x 2 x 4 x 7 values (see the kernel)

@@ -7,4 +7,6 @@ timeout -k 10 120 python -u tools/ro_sched.py double_integrator 4096 "0,0 -1,0 -
 timeout -k 10 120 python -u tools/ro_sched.py car_park 4096 "0,0 -1,0 -2,0" >> gpurun_out/ws/sched.log 2>&1 &&
 timeout -k 10 120 python -u tools/ro_sched.py single_integrator 4096 "0,0 -1,0 -2,0" >> gpurun_out/ws/sched.log 2>&1 &&
 timeout -k 10 120 python -u tools/ro_sched.py car 4096 "0,0 -1,0 -2,0" >> gpurun_out/ws/sched.log 2>&1 &&
-CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/tt_stamps.py double_integrator ws > gpurun_out/ws/stamps.log 2>&1
+CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/tt_stamps.py double_integrator ws > gpurun_out/ws/stamps.log 2>&1 &&
+CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/rollout_stamps.py ur5 2048 >> gpurun_out/ws/stamps.log 2>&1 &&
+CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so timeout -k 10 120 python -u tools/rollout_stamps.py manipulator 8192 >> gpurun_out/ws/stamps.log 2>&1

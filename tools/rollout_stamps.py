@@ -29,7 +29,7 @@ def main():
     for _ in range(3):
         out = rl.rollout_batch(None, None, T, inputs=inputs)
     torch.cuda.synchronize()
-    st = (ctypes.c_ulonglong * 16)()
+    st = (ctypes.c_ulonglong * 20)()
     L.lib().dll.cacto_debug_rollout_stamps(st)
     t = np.array(st[:4], dtype=np.float64)
     a1, a2 = float(st[4]) - t[0], float(st[5]) - float(st[4])
@@ -45,6 +45,9 @@ def main():
               % tuple("%.0f" % (float(st[k]) - t[2]) if st[k] > st[2] else "-" for k in (13, 14, 15)))
     print("   wave 0 after the dynamics phase: s' %.0f, advance/stores %.0f, refill+ballot %.0f, barrier %.0f"
           % (float(st[6]) - t[2], float(st[7]) - float(st[6]), float(st[8]) - float(st[7]), t[3] - float(st[8])))
+    if st[16] >= st[6]:
+        print("      (of advance/stores: next input (revolute chains: before the stores) %.0f, stores %.0f)"
+              % (float(st[16]) - float(st[6]), float(st[7]) - float(st[16])))
 
 
 if __name__ == "__main__":

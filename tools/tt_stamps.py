@@ -22,7 +22,7 @@ def main():
     for _ in range(3):
         rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(-1, 0))
     torch.cuda.synchronize()
-    st = (ctypes.c_ulonglong * 16)()
+    st = (ctypes.c_ulonglong * 20)()
     L.lib().dll.cacto_debug_rollout_stamps(st)
     v = np.array(st[:16], dtype=np.float64)
     for team in (0, 1):
