@@ -28,6 +28,7 @@
 __device__ unsigned long long g_rstamps[20];
 __device__ unsigned long long g_ttacc[1024 * 2 * 2 * 10];  // [workgroup][team][wave 0/1][phase 0-8, steps]
 __device__ unsigned long long g_wsacc[1024 * 2 * 4 * 7];   // k_rollout_ws: [workgroup][team][wave][phase 0-5, steps]
+                                                           // (k_rollout_ks: [workgroup][wave][...], the same size)
 #define RSTAMP(k)                                                                     \
   do {                                                                                \
     if (blockIdx.x == 0 && threadIdx.x == 0 && it == 20) g_rstamps[k] = __builtin_amdgcn_s_memtime(); \
@@ -136,11 +137,18 @@ __device__ __forceinline__ float add_from_above(float v, int off) {
 // Layer 2 of the actor (K = 256) for the NG groups of 4 slots: x = h1 (LDS, broadcast layout) ->
 // h2 (LDS, [slot][feature]) for the 64 features of this wave. k = 64 kb + 16 v + q; lane 4q+i
 // reads {x[i][64kb + 16v + q], v = 0..3}.
-template <int NG, int NS, int REGK, int LDSK, bool PF, typename WT>
+// Summation order (every kernel that can run a system forms the same one, so the schedule never
+// changes a result): SPLIT (the systems k_rollout_ks runs: NJ <= 2) — each half of K (k < 128,
+// k >= 128) as two MFMA chains over its even and odd k in increasing k, the half's sum = even +
+// odd, h2 = lrelu((lo + hi) + b2) (k_rollout_ks forms the two halves on two waves); otherwise (the
+// revolute chains, whose 16-slot kernels have no registers for the split) h2 = lrelu((even + odd)
+// + b2) over all of K.
+template <int NG, int NS, int REGK, int LDSK, bool PF, bool SPLIT, typename WT>
 __device__ __forceinline__ void ro_layer2(const RoActorRegs<NS, REGK>& R, WT& W, const float* __restrict__ W2g,
                                           const Lane& L) {
   using C = RoCfg<NG>;
   floatx4 acc[NG][2];
+  const int f = 64 * L.wave + L.lane;
 #pragma unroll
   for (int g = 0; g < NG; ++g) acc[g][0] = acc[g][1] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int rd = (L.lane >> 2) * 20 + 4 * (L.lane & 3);
@@ -199,18 +207,30 @@ __device__ __forceinline__ void ro_layer2(const RoActorRegs<NS, REGK>& R, WT& W,
         for (int g = 0; g < NG; ++g) acc[g][q & 1] = mfma_bc<q>(get4(xv[g], v), w, acc[g][q & 1]);
       });
     }
+    if (SPLIT && kb == 1) {
+      // the k < 128 half done: its sum parked in this lane's own h2 slots (no registers held across
+      // the second half), the chains restart for k >= 128
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) W.h2[(4 * g + i) * C::H2S + f] = fadd(acc[g][0][i], acc[g][1][i]);
+        acc[g][0] = acc[g][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
   }
-  const int f = 64 * L.wave + L.lane;
 #pragma unroll
   for (int g = 0; g < NG; ++g)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      W.h2[(4 * g + i) * C::H2S + f] = lrelu(fadd(fadd(acc[g][0][i], acc[g][1][i]), R.b2));
+    for (int i = 0; i < 4; ++i) {
+      float& h = W.h2[(4 * g + i) * C::H2S + f];
+      const float hi = fadd(acc[g][0][i], acc[g][1][i]);
+      h = lrelu(fadd(SPLIT ? fadd(h, hi) : hi, R.b2));
+    }
 }
 
 // Actor forward of the workgroup's SL slots: x0 -> h1 -> h2 -> a. Contains 3 barriers (the last
 // one publishes W.a).
-template <int NG, int NS, int NA, int REGK, int LDSK, bool PF, typename WT, typename Bar>
+template <int NG, int NS, int NA, int REGK, int LDSK, bool PF, bool SPLIT, typename WT, typename Bar>
 __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, WT& W, const float* __restrict__ W2g,
                                          const Lane& L, int it, Bar&& bar) {
   using C = RoCfg<NG>;
@@ -238,7 +258,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, WT& W, 
   bar();
   RSTAMP(4);
   // ---- layer 2 (K = 256)
-  ro_layer2<NG, NS, REGK, LDSK, PF>(R, W, W2g, L);
+  ro_layer2<NG, NS, REGK, LDSK, PF, SPLIT>(R, W, W2g, L);
   bar();
   RSTAMP(5);
   // ---- layer 3 (256 -> NA): one summation order for every NG (so the schedule never changes a
@@ -614,6 +634,53 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
   return fin;
 }
 
+// Env.simulate of the rollout (float64 state and action, f32in = false) with the system scalars it
+// reads held in registers for the whole launch: env_simulate / env_simulate_const read them from
+// the SysDevice parameter block at every call, and in k_rollout_ws that scalar load's latency sat on
+// every step's dynamics. The same operations in the same order as env_simulate(_const).
+struct RoSimScalars {
+  double dt, L_delta, tau_delta;
+};
+template <int NJ>
+__device__ __forceinline__ void ro_simulate(const RoSimScalars& k, const ConstDyn<NJ>& cd, const double* s,
+                                            const double* a, double* out) {
+  const double dt = k.dt;
+  if constexpr (NJ == 0) {
+    out[0] = s[0] + dt * a[0];
+    out[1] = s[1] + dt * a[1];
+    out[2] = s[2] + dt;
+  } else if constexpr (NJ == -1) {
+    const double dt2 = dt * dt;
+    const double c = cos(s[2]), sn = sin(s[2]);
+    out[0] = (s[0] + dt * s[3] * c) + dt2 * s[4] * c / 2.0;
+    out[1] = (s[1] + dt * s[3] * sn) + dt2 * s[4] * sn / 2.0;
+    out[2] = s[2] + dt * a[0];
+    out[3] = s[3] + dt * s[4];
+    out[4] = s[4] + dt * a[1];
+    out[5] = s[5] + dt;
+  } else if constexpr (NJ == -2) {
+    const double L = k.L_delta, tau = k.tau_delta;
+    out[0] = s[0] + dt * s[3] * cos(s[2]);
+    out[1] = s[1] + dt * s[3] * sin(s[2]);
+    out[2] = s[2] + dt * s[3] * tan(s[4]) / L;
+    out[3] = s[3] + dt * a[0];
+    out[4] = s[4] + dt * a[1] / tau;
+    out[5] = s[5] + dt;
+  } else {
+    double dv[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) dv[i] = a[i] - cd.h[i];
+    chol_solve<NJ>(cd.L, dv);
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      const double v = s[NJ + i];
+      out[i] = s[i] + v * dt;
+      out[NJ + i] = v + dv[i] * dt;
+    }
+    out[2 * NJ] = s[2 * NJ] + dt;
+  }
+}
+
 // One workgroup = SL episode slots (lane c < SL of wave 0 <-> slot c). Per step:
 //   actor (4 waves, MFMA, weights stationary)                                -> a (LDS)
 //   wave 0: s' = f(s, a) (chains with configuration-dependent M: RNEA on wave 0 and the CRBA
@@ -649,6 +716,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   __syncthreads();
   int head = 0;  // queue position (wave 0, uniform)
   const RoNorm<ns> nrm(p);
+  const RoSimScalars ks{p.dt, p.L_delta, p.tau_delta};
   if (L.wave == 0) {
     ro_refill<NJ, NG>(L.lane < SL, L.lane, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L,
                       (int)blockIdx.x);
@@ -673,7 +741,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (!use_actor) __syncthreads();
       }
     }
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2), (NJ <= 2)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
     RSTAMP(1);
     const bool active = L.lane < SL && (L.wave == 0 ? sr.act : Sh.sact[c] != 0);
     if (split_dyn) {
@@ -711,10 +779,10 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
             for (int i = 0; i < NJ; ++i) h[i] = Sh.hS[i * SL + c];
             chain_step<NJ>(sd, s, ad, M, h, sn);
           } else {
-            env_simulate_const<NJ>(sd, sr.cd, s, ad, sn);
+            ro_simulate<NJ>(ks, sr.cd, s, ad, sn);
           }
         } else {
-          env_simulate<NJ>(sd, s, ad, false, sn);
+          ro_simulate<NJ>(ks, sr.cd, s, ad, sn);
         }
         RSTAMP(6);
 #pragma unroll
@@ -874,6 +942,7 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
   const int vb = 2 * (int)blockIdx.x + team, G = 2 * (int)gridDim.x;
   int head = 0;
   const RoNorm<ns> nrm(p);
+  const RoSimScalars ks{p.dt, p.L_delta, p.tau_delta};
   const int c = L.lane % SL;
   // prismatic chains (the host runs this kernel for const_dyn chains only): M's Cholesky factor
   // and h do not depend on (q, v) — the values k_const_dyn_init tabled in SysDevice, computed by
@@ -951,9 +1020,9 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
 #ifdef CACTO_STAMPS
     tbi = 0;
     tmark(0);
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true>(R, V, W2g, L, it, sbar);
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true, true>(R, V, W2g, L, it, sbar);
 #else
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true>(R, V, W2g, L, it, tbar);
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, true, true>(R, V, W2g, L, it, tbar);
 #endif
     TSTAMP(1);
     if (L.wave == 0) {
@@ -967,10 +1036,7 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
           a[i] = use_actor ? S.W.a[c * na + i] : 0.f;
           ad[i] = (double)a[i];
         }
-        if constexpr (NJ > 0)
-          env_simulate_const<NJ>(sd, cd, sr.s, ad, sn);
-        else
-          env_simulate<NJ>(sd, sr.s, ad, false, sn);
+        ro_simulate<NJ>(ks, cd, sr.s, ad, sn);
 #pragma unroll
         for (int i = 0; i < ns; ++i) {
           S.sS[c * ns + i] = sn[i];
@@ -1127,6 +1193,7 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
 #pragma unroll
     for (int i = 0; i < NJ; ++i) cd.h[i] = sd.cd_h[i];
   }
+  const RoSimScalars ks{p.dt, p.L_delta, p.tau_delta};
   // the slot (wave-uniform): active, episode, length, step, s_t
   bool act = false;
   int b = 0, n = 0, t = 0;
@@ -1214,7 +1281,7 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
 #pragma unroll
     for (int i = 0; i < na; ++i) a[i] = 0.f;
     if (use_actor) {
-      ro_layer2<1, ns, REGK, LDSK, true>(R, V, W2g, L);
+      ro_layer2<1, ns, REGK, LDSK, true, true>(R, V, W2g, L);
       tbar();
       WMARK(0);
       if (act) {
@@ -1260,10 +1327,7 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
       double ad[na], sn[ns];
 #pragma unroll
       for (int i = 0; i < na; ++i) ad[i] = (double)a[i];
-      if constexpr (NJ > 0)
-        env_simulate_const<NJ>(sd, cd, s, ad, sn);
-      else
-        env_simulate<NJ>(sd, s, ad, false, sn);
+      ro_simulate<NJ>(ks, cd, s, ad, sn);
       bool bad = false;
 #pragma unroll
       for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
@@ -1302,6 +1366,258 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
   }
 #endif
 #undef WMARK
+}
+
+// ---------------------------------------------------------------- one slot per wave, K split
+// k_rollout_ks: one 8-wave workgroup per CU runs 8 episode slots, wave w owning slot w as in
+// k_rollout_ws (layer 3, dynamics, stores, refill and layer 1 of its slot). Layer 2 is split over
+// the waves by feature quarter AND by half of K: wave (fq, h) = (w & 3, w >> 2) multiplies the
+// 128 rows [128 h, 128 h + 128) of W2 for features 64 fq + lane — held in its registers for the
+// whole launch, so the 256 KB of layer-2 weights live in the 8 waves' registers and no weight row
+// is read from LDS per step — for all 8 slots (two groups of 4 samples, 256 MFMAs), and parks its
+// half sum; layer 3 adds the two halves (the SPLIT order of ro_layer2, so results are identical to
+// the other rollout kernels). Two hardware barriers per step (one workgroup = one team).
+template <int NJ>
+struct RoKsShared {
+  float h1[2 * 4 * RoCfg<1>::H1B];  // layer-1 output of the 8 slots (groups 0, 1), layer-2 operand layout
+  float P[2][8 * 256];              // layer-2 half sums [k half][slot][feature]
+  int act[8];                       // slot active flags, published by the barrier that ends a step
+  int qhead;                        // the workgroup's next queue entry
+};
+
+template <int NJ>
+__global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
+    k_rollout_ks(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
+                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
+                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  constexpr int H1B = RoCfg<1>::H1B;
+  __shared__ RoKsShared<NJ> Sh;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fq = w & 3, hk = w >> 2;  // layer 2: features 64 fq + lane, rows [128 hk, 128 hk + 128)
+  const int sg = w >> 2, si = w & 3;  // this wave's slot w = 4 sg + si (group, sample)
+  float w2[128], b2[4], w1[ns][4], b1[4], w3[na][4], b3[na];
+  if (use_actor) {
+    const float* W1 = N.flat + N.t.woff[0];
+    const float* W2 = N.flat + N.t.woff[1];
+    const float* W3 = N.flat + N.t.woff[2];
+#pragma unroll
+    for (int k = 0; k < 128; ++k) w2[k] = W2[(128 * hk + k) * 256 + 64 * fq + lane];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int q = 0; q < ns; ++q) w1[q][m] = W1[q * 256 + lane + 64 * m];
+      b1[m] = N.bias(0, lane + 64 * m);
+      b2[m] = N.bias(1, lane + 64 * m);
+#pragma unroll
+      for (int a = 0; a < na; ++a) w3[a][m] = W3[(lane + 64 * m) * na + a];
+    }
+#pragma unroll
+    for (int a = 0; a < na; ++a) b3[a] = N.bias(2, a);
+  }
+  for (int e = threadIdx.x; e < 2 * 4 * H1B; e += 8 * CACTO_WAVE) Sh.h1[e] = 0.f;
+  if (threadIdx.x == 0) Sh.qhead = 0;
+  __syncthreads();
+  const int vb = (int)blockIdx.x, G = (int)gridDim.x;
+  const RoNorm<ns> nrm(p);
+  float nl = 1.f;
+#pragma unroll
+  for (int q = 0; q < ns; ++q) nl = lane == q ? nrm.n[q] : nl;
+  const bool tl = lane == ns - 1;
+  ConstDyn<NJ> cd;
+  if constexpr (NJ > 0) {
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = sd.cd_L[k];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) cd.h[i] = sd.cd_h[i];
+  }
+  const RoSimScalars ks{p.dt, p.L_delta, p.tau_delta};
+  bool act = false;
+  int b = 0, n = 0, t = 0;
+  double s[ns];
+#pragma unroll
+  for (int i = 0; i < ns; ++i) s[i] = 0.0;
+
+  auto refill = [&]() {  // k_rollout_ws's refill, over the workgroup's queue
+    act = false;
+    while (true) {
+      int k = 0;
+      if (lane == 0) k = __hip_atomic_fetch_add(&Sh.qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      k = __builtin_amdgcn_readfirstlane(k);
+      const int r = k * G + ((k & 1) ? G - 1 - vb : vb);
+      if (r >= B) return;
+      const int bb = __builtin_amdgcn_readfirstlane(order ? order[r] : r);
+      const int nn = min(nsteps[bb], T);
+#pragma unroll
+      for (int i = 0; i < ns; ++i) s[i] = S0[(size_t)bb * ns + i];
+      if (Straj && lane < ns) Straj[(size_t)bb * (T + 1) * ns + lane] = lane_pick<ns>(s, lane);
+      if (nn == 0) {
+        if (status && lane == 0) status[bb] = 0;
+        continue;
+      }
+      b = bb;
+      n = nn;
+      t = 0;
+      act = true;
+      return;
+    }
+  };
+  auto layer1 = [&]() {  // k_rollout_ws's layer 1, into this slot's column of the two-group layout
+    const double sv = lane_pick<ns>(s, lane);
+    const float qv = fdiv((float)sv, nl);
+    const float xv = nrm.on ? (tl ? fsub(fmul(qv, 2.0f), 1.0f) : qv) : (float)sv;
+    float x0[ns];
+#pragma unroll
+    for (int q = 0; q < ns; ++q) x0[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), q));
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], w1[q][m], acc);
+      Sh.h1[(sg * 4 + m) * H1B + (lane & 15) * 20 + 4 * si + (lane >> 4)] = lrelu(fadd(acc, b1[m]));
+    }
+  };
+
+#ifdef CACTO_STAMPS
+  // accumulated phase cycles of every step (lane 0 of each wave): [0] loop test + layer 2 + its
+  // barrier, [1] layer 3, [2] s' = f(s, a) + trajectory stores, [3] refill, [4] layer 1, [5] the
+  // end-of-step barrier
+  unsigned long long wacc[6] = {0, 0, 0, 0, 0, 0}, wprev = __builtin_amdgcn_s_memtime();
+  int wsteps = 0;
+  auto wmark = [&](int ph) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (k == ph) wacc[k] += now - wprev;
+    wprev = now;
+  };
+#define KMARK(k) wmark(k)
+#else
+#define KMARK(k) \
+  do {           \
+  } while (0)
+#endif
+
+  refill();
+  if (act && use_actor) layer1();
+  if (lane == 0) Sh.act[w] = act;
+  __syncthreads();
+  const int rd = (lane >> 2) * 20 + 4 * (lane & 3);
+  for (int it = 0;; ++it) {
+    int any = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) any |= Sh.act[k];
+    if (any == 0) break;
+    // every wave has read the flags (above) before any wave rewrites its own below: the layer-2
+    // barrier orders that; without the actor this barrier does
+    if (!use_actor) __syncthreads();
+    float a[na];
+#pragma unroll
+    for (int i = 0; i < na; ++i) a[i] = 0.f;
+    if (use_actor) {
+      // layer 2, this wave's half of K for features 64 fq + lane, both slot groups
+      float4 xa[2][2];
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+        for (int kl = 0; kl < 2; ++kl)
+          xa[gg][kl] = *reinterpret_cast<const float4*>(&Sh.h1[(gg * 4 + 2 * hk + kl) * H1B + rd]);
+      floatx4 acc[2][2];
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) acc[gg][0] = acc[gg][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kl = 0; kl < 2; ++kl)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          static_for<16>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+#pragma unroll
+            for (int gg = 0; gg < 2; ++gg)
+              acc[gg][q & 1] = mfma_bc<q>(get4(xa[gg][kl], v), w2[64 * kl + 16 * v + q], acc[gg][q & 1]);
+          });
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Sh.P[hk][(4 * gg + i) * 256 + 64 * fq + lane] = fadd(acc[gg][0][i], acc[gg][1][i]);
+      __syncthreads();
+      KMARK(0);
+      if (act) {
+        // layer 3 of slot w on the two halves' sums: h2 = lrelu((lo + hi) + b2), then ro_actor's
+        // chains and butterfly (both actions in one permlane butterfly for na == 2)
+        float pa[na];
+#pragma unroll
+        for (int i = 0; i < na; ++i) pa[i] = 0.f;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int f = lane + 64 * m;
+          const float h = lrelu(fadd(fadd(Sh.P[0][w * 256 + f], Sh.P[1][w * 256 + f]), b2[m]));
+#pragma unroll
+          for (int i = 0; i < na; ++i) pa[i] = fmaf(w3[i][m], h, pa[i]);
+        }
+        if constexpr (na == 2) {
+          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[0]), __float_as_uint(pa[1]), false, false);
+          float v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+          v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+#pragma unroll
+          for (int off = 8; off >= 1; off >>= 1) v = add_from_above(v, off);
+          a[0] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)), b3[0]);
+          a[1] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)), b3[1 % na]);
+        } else {
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+            for (int i = 0; i < na; ++i) pa[i] = add_from_above(pa[i], off);
+#pragma unroll
+          for (int i = 0; i < na; ++i)
+            a[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fadd(pa[i], b3[i]))));
+        }
+      }
+      KMARK(1);
+    }
+    bool fin = false;
+    if (act) {
+      double ad[na], sn[ns];
+#pragma unroll
+      for (int i = 0; i < na; ++i) ad[i] = (double)a[i];
+      ro_simulate<NJ>(ks, cd, s, ad, sn);
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
+      if (Atraj && lane < na) Atraj[((size_t)b * T + t) * na + lane] = lane_pick<na>(a, lane);
+      if (Straj && lane < ns) Straj[((size_t)b * (T + 1) + t + 1) * ns + lane] = lane_pick<ns>(sn, lane);
+      if (bad && Straj) {
+        for (int e = lane; e < (n - t - 1) * ns; e += 64)
+          Straj[((size_t)b * (T + 1) + t + 2) * ns + e] = __builtin_nan("");
+      }
+      fin = bad || t + 1 >= n;
+      if (fin && status && lane == 0) status[b] = bad ? 1 : 0;
+#pragma unroll
+      for (int i = 0; i < ns; ++i) s[i] = sn[i];
+      t += 1;
+    }
+    KMARK(2);
+    if (fin) refill();
+    KMARK(3);
+    if (act && use_actor) layer1();
+    if (lane == 0) Sh.act[w] = act;
+    KMARK(4);
+    __syncthreads();
+    KMARK(5);
+#ifdef CACTO_STAMPS
+    ++wsteps;
+#endif
+  }
+#ifdef CACTO_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_wsacc + ((size_t)blockIdx.x * 8 + w) * 7;
+    for (int k = 0; k < 6; ++k) o[k] = wacc[k];
+    o[6] = wsteps;
+  }
+#endif
+#undef KMARK
 }
 
 // Rewards and end-effector positions of every recorded step (Env.step's reward and
@@ -1493,16 +1809,27 @@ struct LaunchRollout {
     // automatic only where it measured faster: the prismatic chain (DI 0.75 -> 0.72 ms at 4096
     // episodes); car_park's step was slower on two teams (0.42 -> 0.50 ms)
     const bool tt_auto = tt_sys && NJ > 0;
-    if ((groups == -1 || groups == -2) && !tt_sys) {
+    if ((groups == -1 || groups == -2 || groups == -3) && !tt_sys) {
       set_error("cacto_rollout_sched: groups -1 / -2 (two teams) need a system without configuration-dependent M");
       return CACTO_EINVAL;
     }
-    // one slot per wave (k_rollout_ws) where it measured faster: the prismatic chain (DI 4096
-    // episodes: 0.725 -> 0.632 ms against k_rollout_tt) and the single integrator (0.366 -> 0.322
-    // ms); car / car_park keep the single-team kernel (their f64 trigonometry per step on one
-    // wave's chain measured slower: 1.84 -> 1.88 / 0.43 -> 0.51 ms). Up to two episodes per slot.
-    const bool ws_auto = tt_sys && NJ >= 0 && B <= 2 * 8 * cus;
-    if (groups == -2 || (groups == 0 && ws_auto)) {
+    // one slot per wave with layer 2 split over K (k_rollout_ks) for every system it can run, up
+    // to two episodes per slot. Measured at 4096 episodes (ms per rollout, one MI355X): DI
+    // k_rollout_tt 0.750 / k_rollout_ws 0.630 / k_rollout_ks 0.578; SI single-team 0.519 / ws 0.326
+    // / ks 0.292; car_park single-team 0.432 / ks 0.405; car 1.865 / 1.768.
+    const bool ks_auto = tt_sys && B <= 2 * 8 * cus;
+    if (groups == -3 || (groups == 0 && ks_auto)) {
+      // one slot per wave, layer 2 split over K (k_rollout_ks), one 8-wave workgroup per CU
+      if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
+      wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
+      if constexpr (tt_ok)
+        hipLaunchKernelGGL(k_rollout_ks<NJ>, dim3(wgs), dim3(8 * CACTO_WAVE), 0, st, sys->dev, v, S0, n, T,
+                           use_actor, S, A, status, order, B);
+      CACTO_CHECK_HIP(hipGetLastError());
+      if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
+      return CACTO_OK;
+    }
+    if (groups == -2) {
       if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
       wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
       if constexpr (tt_ok)
@@ -1586,8 +1913,9 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
                                    const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
-  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -2,
-                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams) or -2 (one slot per wave)");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -2 || groups == -3,
+                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams), -2 (one slot per wave) or -3 "
+                "(one slot per wave, layer 2 split over K)");
   CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
   CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
                 "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");

@@ -44,14 +44,14 @@ def main():
               ", ".join("%s %.0f" % (n, x) for n, x in zip(names, per)))
 
 
-def ws(system):
-    """k_rollout_ws (groups -2): per-phase cycles per step, every wave of every team."""
+def ws(system, groups=-2):
+    """k_rollout_ws (groups -2) / k_rollout_ks (groups -3): per-phase cycles per step, every wave."""
     conf, env, rl = bench.make_learner(system)
     S0, n = bench.initial_states(env, conf, 4096, seed=0)
     T = int(n.max())
     inputs = rl.rollout_inputs(S0, n)
     for _ in range(3):
-        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(-2, 0))
+        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(groups, 0))
     torch.cuda.synchronize()
     acc = (ctypes.c_ulonglong * (1024 * 2 * 4 * 7))()
     L.lib().dll.cacto_debug_rollout_ws_acc(acc)
@@ -59,12 +59,12 @@ def ws(system):
     names = ["loop test + layer 2 + bar", "layer 3", "s'=f(s,a) + stores", "refill", "layer 1", "end barrier"]
     steps = a[..., 6].sum()
     per = a[..., :6].sum(axis=(0, 1, 2)) / max(steps, 1)
-    print(system, "k_rollout_ws, %d wave-steps: cycles per step %.0f = " % (steps, per.sum()) +
+    print(system, "k_rollout_%s, %d wave-steps: cycles per step %.0f = " % ("ws" if groups == -2 else "ks", steps, per.sum()) +
           ", ".join("%s %.0f" % (nm, x) for nm, x in zip(names, per)))
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 2 and sys.argv[2] == "ws":
-        ws(sys.argv[1])
+    if len(sys.argv) > 2 and sys.argv[2] in ("ws", "ks"):
+        ws(sys.argv[1], -2 if sys.argv[2] == "ws" else -3)
         sys.exit(0)
     main()
