@@ -150,7 +150,7 @@ def dry_run(args):
                           "backend": os.environ.get("CACTO_DIST_BACKEND", "nccl")}))
 
 
-def pmc_traffic(kernel=("k_rollout_tt<2", "k_rollout<2,")):
+def pmc_traffic(kernel=("k_rollout_ks<2", "k_rollout_tt<2", "k_rollout<2,")):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summaries
     (profiles/rNN_pmc_{fetch,write}.csv, made by tools/prof_summary.py from separate --pmc
     FETCH_SIZE / WRITE_SIZE passes). gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE
@@ -167,7 +167,8 @@ def pmc_traffic(kernel=("k_rollout_tt<2", "k_rollout<2,")):
 
     def mean(path, counter):
         # the first of `kernels` the summary holds: the double integrator's sequential pass at its
-        # bench schedule (k_rollout_tt<2> since round 3, k_rollout<2, 2> before)
+        # bench schedule (k_rollout_ks<2> since round 4, k_rollout_tt<2> in round 3, k_rollout<2, 2>
+        # before)
         with open(path) as f:
             rows = list(csv.DictReader(f))
         for k in kernels:
@@ -883,7 +884,8 @@ def main():
                        "parallelism": "dp%d" % world},
             "segments": roll["segments"],
             "long_region": roll["long_region"],
-            "roofline": {"kernel": "k_rollout (k_rollout_tt<2>: two 4-slot teams per workgroup at this schedule)",
+            "roofline": {"kernel": "k_rollout (k_rollout_ks<2>: one slot per wave, layer 2 split over K, at this "
+                                   "schedule)",
                          "bound": "mfma", "achieved": achieved / 1e12,
                          "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

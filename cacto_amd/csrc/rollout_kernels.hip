@@ -1620,6 +1620,261 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
 #undef KMARK
 }
 
+// ---------------------------------------------------------------- K split, two slot groups in antiphase
+// k_rollout_kp: k_rollout_ks's layout (8 waves, wave w owns slot w and multiplies W2 rows
+// [128 h, 128 h + 128) for features 64 fq + lane from its registers) with the two groups of 4
+// slots half a step apart. A step is two half-steps; in half-step ph every wave runs layer 2 of
+// group ph ^ 1 (128 MFMAs) while the 4 waves of group ph run their slots' serial part — layer 3
+// from the half sums the previous half-step parked, the dynamics, the stores, the refill, layer 1.
+// Waves w and w + 4 share a SIMD and belong to different groups, so on every SIMD one wave feeds
+// the matrix core while the other runs its slot's VALU / LDS chain (and then its own 128 MFMAs).
+// Same per-slot operations as k_rollout_ks (the same half sums, bit-identical results).
+template <int NJ>
+struct RoKpShared {
+  float h1[2 * 4 * RoCfg<1>::H1B];  // layer-1 output of the 8 slots (groups 0, 1), layer-2 operand layout
+  float P[2][8 * 256];              // layer-2 half sums [k half][slot][feature]
+  int act[2][8];                    // slot active flags by step parity
+  int qhead;
+};
+
+template <int NJ>
+__global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
+    k_rollout_kp(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
+                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
+                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  constexpr int H1B = RoCfg<1>::H1B;
+  __shared__ RoKpShared<NJ> Sh;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fq = w & 3, hk = w >> 2;  // layer 2: features 64 fq + lane, rows [128 hk, 128 hk + 128)
+  const int sg = w >> 2, si = w & 3;  // this wave's slot w = 4 sg + si (group, sample)
+  float w2[128], b2[4], w1[ns][4], b1[4], w3[na][4], b3[na];
+  if (use_actor) {
+    const float* W1 = N.flat + N.t.woff[0];
+    const float* W2 = N.flat + N.t.woff[1];
+    const float* W3 = N.flat + N.t.woff[2];
+#pragma unroll
+    for (int k = 0; k < 128; ++k) w2[k] = W2[(128 * hk + k) * 256 + 64 * fq + lane];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int q = 0; q < ns; ++q) w1[q][m] = W1[q * 256 + lane + 64 * m];
+      b1[m] = N.bias(0, lane + 64 * m);
+      b2[m] = N.bias(1, lane + 64 * m);
+#pragma unroll
+      for (int a = 0; a < na; ++a) w3[a][m] = W3[(lane + 64 * m) * na + a];
+    }
+#pragma unroll
+    for (int a = 0; a < na; ++a) b3[a] = N.bias(2, a);
+  }
+  for (int e = threadIdx.x; e < 2 * 4 * H1B; e += 8 * CACTO_WAVE) Sh.h1[e] = 0.f;
+  if (threadIdx.x == 0) Sh.qhead = 0;
+  __syncthreads();
+  const int vb = (int)blockIdx.x, G = (int)gridDim.x;
+  const RoNorm<ns> nrm(p);
+  float nl = 1.f;
+#pragma unroll
+  for (int q = 0; q < ns; ++q) nl = lane == q ? nrm.n[q] : nl;
+  const bool tl = lane == ns - 1;
+  ConstDyn<NJ> cd;
+  if constexpr (NJ > 0) {
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = sd.cd_L[k];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) cd.h[i] = sd.cd_h[i];
+  }
+  const RoSimScalars ks{p.dt, p.L_delta, p.tau_delta};
+  bool act = false;
+  int b = 0, n = 0, t = 0;
+  double s[ns];
+#pragma unroll
+  for (int i = 0; i < ns; ++i) s[i] = 0.0;
+
+  auto refill = [&]() {  // k_rollout_ks's refill
+    act = false;
+    while (true) {
+      int k = 0;
+      if (lane == 0) k = __hip_atomic_fetch_add(&Sh.qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      k = __builtin_amdgcn_readfirstlane(k);
+      const int r = k * G + ((k & 1) ? G - 1 - vb : vb);
+      if (r >= B) return;
+      const int bb = __builtin_amdgcn_readfirstlane(order ? order[r] : r);
+      const int nn = min(nsteps[bb], T);
+#pragma unroll
+      for (int i = 0; i < ns; ++i) s[i] = S0[(size_t)bb * ns + i];
+      if (Straj && lane < ns) Straj[(size_t)bb * (T + 1) * ns + lane] = lane_pick<ns>(s, lane);
+      if (nn == 0) {
+        if (status && lane == 0) status[bb] = 0;
+        continue;
+      }
+      b = bb;
+      n = nn;
+      t = 0;
+      act = true;
+      return;
+    }
+  };
+  auto layer1 = [&]() {  // k_rollout_ks's layer 1
+    const double sv = lane_pick<ns>(s, lane);
+    const float qv = fdiv((float)sv, nl);
+    const float xv = nrm.on ? (tl ? fsub(fmul(qv, 2.0f), 1.0f) : qv) : (float)sv;
+    float x0[ns];
+#pragma unroll
+    for (int q = 0; q < ns; ++q) x0[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), q));
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], w1[q][m], acc);
+      Sh.h1[(sg * 4 + m) * H1B + (lane & 15) * 20 + 4 * si + (lane >> 4)] = lrelu(fadd(acc, b1[m]));
+    }
+  };
+  // the slot's serial part of one step: action (layer 3 on the parked half sums), dynamics,
+  // trajectory stores, end of episode, refill, next layer-1 column
+  auto slot_step = [&]() {
+    if (!act) return;
+    float a[na];
+#pragma unroll
+    for (int i = 0; i < na; ++i) a[i] = 0.f;
+    if (use_actor) {
+      float pa[na];
+#pragma unroll
+      for (int i = 0; i < na; ++i) pa[i] = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int f = lane + 64 * m;
+        const float h = lrelu(fadd(fadd(Sh.P[0][w * 256 + f], Sh.P[1][w * 256 + f]), b2[m]));
+#pragma unroll
+        for (int i = 0; i < na; ++i) pa[i] = fmaf(w3[i][m], h, pa[i]);
+      }
+      if constexpr (na == 2) {
+        const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[0]), __float_as_uint(pa[1]), false, false);
+        float v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+        const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) v = add_from_above(v, off);
+        a[0] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)), b3[0]);
+        a[1] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)), b3[1 % na]);
+      } else {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+          for (int i = 0; i < na; ++i) pa[i] = add_from_above(pa[i], off);
+#pragma unroll
+        for (int i = 0; i < na; ++i)
+          a[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fadd(pa[i], b3[i]))));
+      }
+    }
+    double ad[na], sn[ns];
+#pragma unroll
+    for (int i = 0; i < na; ++i) ad[i] = (double)a[i];
+    ro_simulate<NJ>(ks, cd, s, ad, sn);
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
+    if (Atraj && lane < na) Atraj[((size_t)b * T + t) * na + lane] = lane_pick<na>(a, lane);
+    if (Straj && lane < ns) Straj[((size_t)b * (T + 1) + t + 1) * ns + lane] = lane_pick<ns>(sn, lane);
+    if (bad && Straj) {
+      for (int e = lane; e < (n - t - 1) * ns; e += 64) Straj[((size_t)b * (T + 1) + t + 2) * ns + e] = __builtin_nan("");
+    }
+    const bool fin = bad || t + 1 >= n;
+    if (fin && status && lane == 0) status[b] = bad ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < ns; ++i) s[i] = sn[i];
+    t += 1;
+    if (fin) refill();
+    if (act && use_actor) layer1();
+  };
+  const int rd = (lane >> 2) * 20 + 4 * (lane & 3);
+  // layer 2 of slot group gg: this wave's half of K, features 64 fq + lane -> its half sums
+  auto layer2 = [&](int gg) {
+    float4 xa[2];
+#pragma unroll
+    for (int kl = 0; kl < 2; ++kl) xa[kl] = *reinterpret_cast<const float4*>(&Sh.h1[(gg * 4 + 2 * hk + kl) * H1B + rd]);
+    floatx4 acc[2];
+    acc[0] = acc[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kl = 0; kl < 2; ++kl)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        static_for<16>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          acc[q & 1] = mfma_bc<q>(get4(xa[kl], v), w2[64 * kl + 16 * v + q], acc[q & 1]);
+        });
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Sh.P[hk][(4 * gg + i) * 256 + 64 * fq + lane] = fadd(acc[0][i], acc[1][i]);
+  };
+
+  if (!use_actor) {
+    // zero controls (ep == 0): the slots share nothing but the queue, so every wave steps its own
+    // slot until the queue is empty, without barriers
+    refill();
+    while (act) slot_step();
+    return;
+  }
+
+#ifdef CACTO_STAMPS
+  // accumulated cycles per half-step (lane 0 of each wave): [0] slot part (waves of the active
+  // group), [1] layer 2, [2] barrier; [3] half-steps with a slot part
+  unsigned long long wacc[6] = {0, 0, 0, 0, 0, 0}, wprev = 0;
+  auto wmark = [&](int ph) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if (k == ph) wacc[k] += now - wprev;
+    wprev = now;
+  };
+#define PMARK(k) wmark(k)
+#else
+#define PMARK(k) \
+  do {           \
+  } while (0)
+#endif
+
+  refill();
+  if (act) layer1();
+  if (lane == 0) Sh.act[1][w] = act;  // the flags "of step -1"
+  __syncthreads();
+  layer2(0);  // prologue: group 0's layer 2, so its slots can take the first half-step
+  __syncthreads();
+  for (int st = 0;; ++st) {
+    int any = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) any |= Sh.act[(st + 1) & 1][k];
+    if (any == 0) break;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+#ifdef CACTO_STAMPS
+      wprev = __builtin_amdgcn_s_memtime();
+#endif
+      // the serial part first: the matrix core is fed by the other group's wave on this SIMD
+      if (sg == ph) {
+        slot_step();
+        if (lane == 0) Sh.act[st & 1][w] = act;
+      }
+      PMARK(0);
+      layer2(ph ^ 1);
+      PMARK(1);
+      __syncthreads();
+      PMARK(2);
+#ifdef CACTO_STAMPS
+      if (sg == ph) wacc[3] += 1;
+#endif
+    }
+  }
+#ifdef CACTO_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = g_wsacc + ((size_t)blockIdx.x * 8 + w) * 7;
+    for (int k = 0; k < 6; ++k) o[k] = wacc[k];
+    o[6] = 0;
+  }
+#endif
+#undef PMARK
+}
+
 // Rewards and end-effector positions of every recorded step (Env.step's reward and
 // get_end_effector_position, environment.py:70-78, :146-156): one thread per (episode, t),
 // r_t = reward(w, s_t, a_t) for t < n, EE_t = EE(s_t) for t <= n; NaN states (a dropped episode)
@@ -1809,7 +2064,7 @@ struct LaunchRollout {
     // automatic only where it measured faster: the prismatic chain (DI 0.75 -> 0.72 ms at 4096
     // episodes); car_park's step was slower on two teams (0.42 -> 0.50 ms)
     const bool tt_auto = tt_sys && NJ > 0;
-    if ((groups == -1 || groups == -2 || groups == -3) && !tt_sys) {
+    if (groups < 0 && !tt_sys) {
       set_error("cacto_rollout_sched: groups -1 / -2 (two teams) need a system without configuration-dependent M");
       return CACTO_EINVAL;
     }
@@ -1818,6 +2073,17 @@ struct LaunchRollout {
     // k_rollout_tt 0.750 / k_rollout_ws 0.630 / k_rollout_ks 0.578; SI single-team 0.519 / ws 0.326
     // / ks 0.292; car_park single-team 0.432 / ks 0.405; car 1.865 / 1.768.
     const bool ks_auto = tt_sys && B <= 2 * 8 * cus;
+    if (groups == -4) {
+      // k_rollout_ks with the two slot groups half a step apart (k_rollout_kp)
+      if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
+      wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
+      if constexpr (tt_ok)
+        hipLaunchKernelGGL(k_rollout_kp<NJ>, dim3(wgs), dim3(8 * CACTO_WAVE), 0, st, sys->dev, v, S0, n, T,
+                           use_actor, S, A, status, order, B);
+      CACTO_CHECK_HIP(hipGetLastError());
+      if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
+      return CACTO_OK;
+    }
     if (groups == -3 || (groups == 0 && ks_auto)) {
       // one slot per wave, layer 2 split over K (k_rollout_ks), one 8-wave workgroup per CU
       if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
@@ -1913,9 +2179,9 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
                                    const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
-  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -2 || groups == -3,
-                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams), -2 (one slot per wave) or -3 "
-                "(one slot per wave, layer 2 split over K)");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || (groups <= -1 && groups >= -4),
+                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams), -2 (one slot per wave), -3 "
+                "(one slot per wave, layer 2 split over K) or -4 (-3 with the slot groups in antiphase)");
   CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
   CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
                 "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");

@@ -63,7 +63,27 @@ def ws(system, groups=-2):
           ", ".join("%s %.0f" % (nm, x) for nm, x in zip(names, per)))
 
 
+def kp(system):
+    """k_rollout_kp (groups -4): slot part per step, layer 2 and barrier per half-step."""
+    conf, env, rl = bench.make_learner(system)
+    S0, n = bench.initial_states(env, conf, 4096, seed=0)
+    T = int(n.max())
+    inputs = rl.rollout_inputs(S0, n)
+    for _ in range(3):
+        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(-4, 0))
+    torch.cuda.synchronize()
+    acc = (ctypes.c_ulonglong * (1024 * 2 * 4 * 7))()
+    L.lib().dll.cacto_debug_rollout_ws_acc(acc)
+    a = np.array(acc[:], dtype=np.float64).reshape(1024 * 8, 7)
+    steps = a[:, 3].sum()
+    print(system, "k_rollout_kp, %d slot-steps: slot part %.0f per step; per half-step layer 2 %.0f, barrier %.0f"
+          % (steps, a[:, 0].sum() / max(steps, 1), a[:, 1].sum() / max(2 * steps, 1), a[:, 2].sum() / max(2 * steps, 1)))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "kp":
+        kp(sys.argv[1])
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[2] in ("ws", "ks"):
         ws(sys.argv[1], -2 if sys.argv[2] == "ws" else -3)
         sys.exit(0)
