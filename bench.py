@@ -136,6 +136,11 @@ def dry_run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # launcher tests: a rank that fails or hangs before the rendezvous
+    if os.environ.get("CACTO_DRYRUN_FAIL_RANK") == str(rank):
+        sys.exit(3)
+    if os.environ.get("CACTO_DRYRUN_HANG_RANK") == str(rank):
+        time.sleep(3600)
     me = dict(rank=rank, local_rank=local, world_size=world, device="cuda:%d" % local,
               master="%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")))
     ranks = [me]

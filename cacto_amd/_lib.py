@@ -120,7 +120,12 @@ class _Lib:
                                "(there is no CPU fallback)" % path)
         self.path = path
         self.dll = C.CDLL(path)
+        # CACTO_LIB_PARTIAL=1 (diagnostics only: A/B runs against libraries of older revisions)
+        # binds the symbols the library has and skips the rest
+        partial = os.environ.get("CACTO_LIB_PARTIAL") == "1"
         for name, (res, args) in _SIGS.items():
+            if partial and not hasattr(self.dll, name):
+                continue
             fn = getattr(self.dll, name)
             fn.restype = res
             fn.argtypes = args

@@ -55,3 +55,19 @@ def test_world_mismatch_is_refused():
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_failing_rank_fails_the_launch():
+    """A rank that exits non-zero ends the launch with its code; the ranks left waiting in the
+    rendezvous are killed, not waited for."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--dry-run"], capture_output=True, text=True,
+                       timeout=180, env=_env(CACTO_DRYRUN_FAIL_RANK="1"))
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "rank 1 exited with 3" in r.stderr
+
+
+def test_hanging_rank_is_killed_at_the_timeout():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--launch-timeout", "8"],
+                       capture_output=True, text=True, timeout=180, env=_env(CACTO_DRYRUN_HANG_RANK="0"))
+    assert r.returncode == 124
+    assert "killing them" in r.stderr
