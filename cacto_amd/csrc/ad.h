@@ -228,6 +228,101 @@ __device__ inline void rnea_t(const SysDevice& sd, const T* q, const T* v, const
   }
 }
 
+// Two-tangent numbers (value, d/dq_k, d/dv_k): the a and b parts of HD without the mixed part,
+// for the RNEA derivative passes, which read only tau.a and tau.b. Every a / b component is formed
+// by HD's formula, so the results are those of the HD pass bit for bit, at 3/4 of the registers.
+struct TD {
+  double v, a, b;
+  __device__ TD() = default;
+  __device__ constexpr TD(double x) : v(x), a(0.0), b(0.0) {}
+  __device__ constexpr TD(double x, double da, double db) : v(x), a(da), b(db) {}
+};
+__device__ __forceinline__ TD operator+(TD x, TD y) { return TD(x.v + y.v, x.a + y.a, x.b + y.b); }
+__device__ __forceinline__ TD operator-(TD x, TD y) { return TD(x.v - y.v, x.a - y.a, x.b - y.b); }
+__device__ __forceinline__ TD operator-(TD x) { return TD(-x.v, -x.a, -x.b); }
+__device__ __forceinline__ TD operator*(TD x, TD y) {
+  return TD(x.v * y.v, x.v * y.a + x.a * y.v, x.v * y.b + x.b * y.v);
+}
+__device__ __forceinline__ TD operator*(double s, TD x) { return TD(s * x.v, s * x.a, s * x.b); }
+__device__ __forceinline__ TD operator*(TD x, double s) { return s * x; }
+__device__ __forceinline__ TD operator+(TD x, double s) { return TD(x.v + s, x.a, x.b); }
+__device__ __forceinline__ TD operator+(double s, TD x) { return x + s; }
+__device__ __forceinline__ TD operator-(TD x, double s) { return TD(x.v - s, x.a, x.b); }
+__device__ __forceinline__ TD operator-(double s, TD x) { return TD(s - x.v, -x.a, -x.b); }
+__device__ __forceinline__ void sincos(TD x, TD* s, TD* c) {
+  double sv, cv;
+  ::sincos(x.v, &sv, &cv);
+  *s = TD(sv, cv * x.a, cv * x.b);
+  *c = TD(cv, -sv * x.a, -sv * x.b);
+}
+
+// Dual numbers (value, one tangent): one direction of the RNEA derivative passes on its own
+// thread. The tangent is formed by TD's (and HD's) formula for that component, so it is the same
+// value bit for bit.
+struct DN {
+  double v, a;
+  __device__ DN() = default;
+  __device__ constexpr DN(double x) : v(x), a(0.0) {}
+  __device__ constexpr DN(double x, double da) : v(x), a(da) {}
+};
+__device__ __forceinline__ DN operator+(DN x, DN y) { return DN(x.v + y.v, x.a + y.a); }
+__device__ __forceinline__ DN operator-(DN x, DN y) { return DN(x.v - y.v, x.a - y.a); }
+__device__ __forceinline__ DN operator-(DN x) { return DN(-x.v, -x.a); }
+__device__ __forceinline__ DN operator*(DN x, DN y) { return DN(x.v * y.v, x.v * y.a + x.a * y.v); }
+__device__ __forceinline__ DN operator*(double s, DN x) { return DN(s * x.v, s * x.a); }
+__device__ __forceinline__ DN operator*(DN x, double s) { return s * x; }
+__device__ __forceinline__ DN operator+(DN x, double s) { return DN(x.v + s, x.a); }
+__device__ __forceinline__ DN operator+(double s, DN x) { return x + s; }
+__device__ __forceinline__ DN operator-(DN x, double s) { return DN(x.v - s, x.a); }
+__device__ __forceinline__ DN operator-(double s, DN x) { return DN(s - x.v, -x.a); }
+__device__ __forceinline__ void sincos(DN x, DN* s, DN* c) {
+  double sv, cv;
+  ::sincos(x.v, &sv, &cv);
+  *s = DN(sv, cv * x.a);
+  *c = DN(cv, -sv * x.a);
+}
+
+// rnea_t for the derivative passes (T = TD, DN) with the joint placements recomputed in the
+// backward sweep instead of held from the forward one (NJ SE3 of tangent numbers was most of the
+// pass's registers); joint_placement_t is deterministic, so the values are the same.
+template <int NJ, typename T>
+__device__ inline void rnea_tan(const SysDevice& sd, const T* q, const T* v, const double* qdd, T* tau) {
+  SVT<T> f[NJ];
+  SVT<T> vp{{T(0.0), T(0.0), T(0.0)}, {T(0.0), T(0.0), T(0.0)}};
+  SVT<T> ap{{T(-sd.p.gravity[0]), T(-sd.p.gravity[1]), T(-sd.p.gravity[2])}, {T(0.0), T(0.0), T(0.0)}};
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    const JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    const SE3T<T> X = joint_placement_t<T>(j, q[i]);
+    const SV S = joint_S(j);
+    const SVT<T> Sv{scale3(v[i], lift<T>(S.l)), scale3(v[i], lift<T>(S.a))};
+    SVT<T> vi = act_motion_inv_t(X, vp);
+    vi.l = vi.l + Sv.l;
+    vi.a = vi.a + Sv.a;
+    SVT<T> ai = act_motion_inv_t(X, ap);
+    const SVT<T> c = cross_motion_t(vi, Sv);
+    ai.l = ai.l + c.l + lift<T>(qdd[i] * S.l);
+    ai.a = ai.a + c.a + lift<T>(qdd[i] * S.a);
+    const Inertia I = j.inertia();
+    const SVT<T> Iv = inertia_mul_t(I, vi), Ia = inertia_mul_t(I, ai);
+    const SVT<T> vf = cross_force_t(vi, Iv);
+    f[i] = {Ia.l + vf.l, Ia.a + vf.a};
+    vp = vi;
+    ap = ai;
+  }
+#pragma unroll
+  for (int i = NJ - 1; i >= 0; --i) {
+    const JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    const SV S = joint_S(j);
+    tau[i] = dot3(lift<T>(S.l), f[i].l) + dot3(lift<T>(S.a), f[i].a);
+    if (i > 0) {
+      const SVT<T> fp = act_force_t(joint_placement_t<T>(j, q[i]), f[i]);
+      f[i - 1].l = f[i - 1].l + fp.l;
+      f[i - 1].a = f[i - 1].a + fp.a;
+    }
+  }
+}
+
 // World translation of the EE frame (framesForwardKinematics + oMf['EE'].translation).
 template <int NJ, typename T>
 __device__ inline V3T<T> chain_ee_t(const SysDevice& sd, const T* q) {

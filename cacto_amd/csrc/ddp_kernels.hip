@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Sobolev labels without CasADi: the DDP backward pass of TO.backward_pass
 // (TO.py:119-202) along recorded trajectories, on the GPU.
 //
@@ -366,13 +367,13 @@ __device__ inline void ddp_chain_jacobians(const SysDevice& sd, const double* x,
     for (int i = 0; i < NJ; ++i) A[i * N + NJ + i] = dt;
 #pragma unroll 1
     for (int k = 0; k < NJ; ++k) {
-      HD q[NJ], v[NJ], tau[NJ];
+      TD q[NJ], v[NJ], tau[NJ];
 #pragma unroll
       for (int i = 0; i < NJ; ++i) {
-        q[i] = HD(x[i], i == k ? 1.0 : 0.0, 0.0, 0.0);
-        v[i] = HD(x[NJ + i], 0.0, i == k ? 1.0 : 0.0, 0.0);
+        q[i] = TD(x[i], i == k ? 1.0 : 0.0, 0.0);
+        v[i] = TD(x[NJ + i], 0.0, i == k ? 1.0 : 0.0);
       }
-      rnea_t<NJ, HD>(sd, q, v, qdd, tau);
+      rnea_tan<NJ, TD>(sd, q, v, qdd, tau);
 #pragma unroll
       for (int r = 0; r < NJ; ++r) {
         double sq = 0.0, sv = 0.0;
@@ -444,6 +445,187 @@ __global__ void __launch_bounds__(64) k_ddp_derivs(const SysDevice* __restrict__
   for (int k = 0; k < N * N; ++k) rec[(size_t)(RC::A + k) * n_ep] = A[k];
 #pragma unroll
   for (int k = 0; k < N * M; ++k) rec[(size_t)(RC::B + k) * n_ep] = B[k];
+}
+
+// k_ddp_derivs for the revolute chains as three kernels, each with the registers of its own part
+// (one thread per (episode, step) carried all of it: A, B, l_xx and NJ hyper-dual RNEA passes
+// held at once, 9 KB of scratch per lane for UR5):
+//   k_ddp_prim  one thread per step: M^-1 (CRBA, inverse), bias forces, qdd = M^-1 (u - h) ->
+//               a [t][k][e] workspace; B = M^-1 dt and A's q rows straight to the record;
+//   k_ddp_tan   one thread per (step, direction): direction d < NJ is d/dq_d, d >= NJ d/dv_{d-NJ},
+//               one RNEA on dual numbers -> column d of A's v rows;
+//   k_ddp_lx    one thread per step (the terminal one included): l_x, l_xx.
+// Every value is formed by the same operations in the same order as k_ddp_derivs (the dual
+// number's tangent is the hyper-dual's a or b part), so the records are bit-identical.
+template <int NJ>
+struct DdpPrim {
+  static constexpr int MINV = 0, QDD = NJ * NJ, R = NJ * NJ + NJ;
+};
+
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ddp_prim(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
+                                                 int64_t ldS, const double* __restrict__ U, int64_t ldU,
+                                                 const int32_t* __restrict__ nsteps, int n_ep, double* __restrict__ ws,
+                                                 double* __restrict__ pw) {
+  using RC = DdpRec<NJ>;
+  using PC = DdpPrim<NJ>;
+  constexpr int N = RC::N, ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.y;
+  if (e >= n_ep) return;
+  const int Te = nsteps[e];
+  if (t >= Te) return;  // the terminal step has no A, B; Te < 0: a dropped episode
+  const SysDevice& sd = *sdp;
+  const double dt = sd.p.dt;
+  double x[N], u[NJ], Mm[NJ * NJ], Minv[NJ * NJ], h[NJ];
+#pragma unroll
+  for (int k = 0; k < N; ++k) x[k] = S[((size_t)e * ldS + t) * ns + k];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) u[k] = U[((size_t)e * ldU + t) * na + k];
+  chain_mass<NJ>(sd, x, Mm);
+  small_inverse<NJ>(Mm, Minv);
+  chain_nle<NJ>(sd, x, x + NJ, h);
+  double* pr = pw + (size_t)t * PC::R * n_ep + e;
+#pragma unroll
+  for (int r = 0; r < NJ; ++r) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) s += Minv[r * NJ + k] * (u[k] - h[k]);
+    pr[(size_t)(PC::QDD + r) * n_ep] = s;
+  }
+#pragma unroll
+  for (int k = 0; k < NJ * NJ; ++k) pr[(size_t)(PC::MINV + k) * n_ep] = Minv[k];
+  double* rec = ws + (size_t)t * RC::R * n_ep + e;
+#pragma unroll
+  for (int i = 0; i < NJ; ++i)
+#pragma unroll
+    for (int c = 0; c < N; ++c) rec[(size_t)(RC::A + i * N + c) * n_ep] = c == i ? 1.0 : (c == NJ + i ? dt : 0.0);
+#pragma unroll
+  for (int k = 0; k < NJ * NJ; ++k) rec[(size_t)(RC::B + k) * n_ep] = 0.0;
+#pragma unroll
+  for (int r = 0; r < NJ; ++r)
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) rec[(size_t)(RC::B + (NJ + r) * NJ + c) * n_ep] = Minv[r * NJ + c] * dt;
+}
+
+// A DN spatial vector in LDS, structure of arrays over the 64 lanes of the block
+struct SvLds {
+  double* b;  // 12 x 64 doubles: (l.x, l.y, l.z, a.x, a.y, a.z) values then tangents
+  __device__ __forceinline__ void st(int lane, const SVT<DN>& f) const {
+    const DN c[6] = {f.l.x, f.l.y, f.l.z, f.a.x, f.a.y, f.a.z};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      b[k * 64 + lane] = c[k].v;
+      b[(6 + k) * 64 + lane] = c[k].a;
+    }
+  }
+  __device__ __forceinline__ SVT<DN> ld(int lane) const {
+    DN c[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c[k] = DN(b[k * 64 + lane], b[(6 + k) * 64 + lane]);
+    return {{c[0], c[1], c[2]}, {c[3], c[4], c[5]}};
+  }
+};
+
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ddp_tan(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
+                                                int64_t ldS, const int32_t* __restrict__ nsteps, int n_ep,
+                                                double* __restrict__ ws, const double* __restrict__ pw) {
+  using RC = DdpRec<NJ>;
+  using PC = DdpPrim<NJ>;
+  constexpr int N = RC::N, ns = Dims<NJ>::NS;
+  // rnea_tan<NJ, DN> with the joint loops rolled and the per-joint forces parked in LDS (the fully
+  // unrolled pass held every joint's parameters and forces in registers and spilled 4.5 KB per
+  // lane); the same operations in the same order
+  __shared__ double fl[NJ * 12 * 64];
+  __shared__ double taul[NJ * 64];
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x * blockDim.x + lane;
+  const int t = blockIdx.y, d = blockIdx.z;
+  if (e >= n_ep) return;
+  const int Te = nsteps[e];
+  if (t >= Te) return;
+  const SysDevice& sd = *sdp;
+  const double dt = sd.p.dt;
+  const double* pr = pw + (size_t)t * PC::R * n_ep + e;
+  const double* xs = S + ((size_t)e * ldS + t) * ns;
+  const bool dq = d < NJ;
+  const int k = dq ? d : d - NJ;
+  SVT<DN> vp{{DN(0.0), DN(0.0), DN(0.0)}, {DN(0.0), DN(0.0), DN(0.0)}};
+  SVT<DN> ap{{DN(-sd.p.gravity[0]), DN(-sd.p.gravity[1]), DN(-sd.p.gravity[2])}, {DN(0.0), DN(0.0), DN(0.0)}};
+#pragma unroll 1
+  for (int i = 0; i < NJ; ++i) {
+    const JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    const DN qi(xs[i], dq && i == k ? 1.0 : 0.0), vi_(xs[NJ + i], !dq && i == k ? 1.0 : 0.0);
+    const double qddi = pr[(size_t)(PC::QDD + i) * n_ep];
+    const SE3T<DN> X = joint_placement_t<DN>(j, qi);
+    const SV Sj = joint_S(j);
+    const SVT<DN> Sv{scale3(vi_, lift<DN>(Sj.l)), scale3(vi_, lift<DN>(Sj.a))};
+    SVT<DN> vi = act_motion_inv_t(X, vp);
+    vi.l = vi.l + Sv.l;
+    vi.a = vi.a + Sv.a;
+    SVT<DN> ai = act_motion_inv_t(X, ap);
+    const SVT<DN> c = cross_motion_t(vi, Sv);
+    ai.l = ai.l + c.l + lift<DN>(qddi * Sj.l);
+    ai.a = ai.a + c.a + lift<DN>(qddi * Sj.a);
+    const Inertia I = j.inertia();
+    const SVT<DN> Iv = inertia_mul_t(I, vi), Ia = inertia_mul_t(I, ai);
+    const SVT<DN> vf = cross_force_t(vi, Iv);
+    SvLds{fl + i * 12 * 64}.st(lane, {Ia.l + vf.l, Ia.a + vf.a});
+    vp = vi;
+    ap = ai;
+  }
+  SVT<DN> f = SvLds{fl + (NJ - 1) * 12 * 64}.ld(lane);
+#pragma unroll 1
+  for (int i = NJ - 1; i >= 0; --i) {
+    const JointView j{sd.joints + i * CACTO_JOINT_COLS};
+    const SV Sj = joint_S(j);
+    const DN ti = dot3(lift<DN>(Sj.l), f.l) + dot3(lift<DN>(Sj.a), f.a);
+    taul[i * 64 + lane] = ti.a;
+    if (i > 0) {
+      const DN qi(xs[i], dq && i == k ? 1.0 : 0.0);
+      const SVT<DN> fp = act_force_t(joint_placement_t<DN>(j, qi), f);
+      const SVT<DN> fo = SvLds{fl + (i - 1) * 12 * 64}.ld(lane);
+      f.l = fo.l + fp.l;
+      f.a = fo.a + fp.a;
+    }
+  }
+  double* rec = ws + (size_t)t * RC::R * n_ep + e;
+#pragma unroll
+  for (int r = 0; r < NJ; ++r) {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) s += pr[(size_t)(PC::MINV + r * NJ + c) * n_ep] * taul[c * 64 + lane];
+    if (dq)
+      rec[(size_t)(RC::A + (NJ + r) * N + k) * n_ep] = -dt * s;
+    else
+      rec[(size_t)(RC::A + (NJ + r) * N + NJ + k) * n_ep] = (r == k ? 1.0 : 0.0) + -dt * s;
+  }
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ddp_lx(const SysDevice* __restrict__ sdp, const double* __restrict__ S,
+                                               int64_t ldS, const int32_t* __restrict__ nsteps, int n_ep,
+                                               double* __restrict__ ws) {
+  using RC = DdpRec<NJ>;
+  constexpr int N = RC::N, ns = Dims<NJ>::NS;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.y;
+  if (e >= n_ep) return;
+  const int Te = nsteps[e];
+  if (t > Te) return;
+  const SysDevice& sd = *sdp;
+  double x[N], w[7], lx[N], lxx[N * N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) x[k] = S[((size_t)e * ldS + t) * ns + k];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) w[k] = t == Te ? sd.p.w_terminal[k] : sd.p.w_running[k];
+  ddp_lx<NJ>(sd, w, x, lx, lxx);
+  double* rec = ws + (size_t)t * RC::R * n_ep + e;
+#pragma unroll
+  for (int k = 0; k < N; ++k) rec[(size_t)(RC::LX + k) * n_ep] = lx[k];
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) rec[(size_t)(RC::LXX + k) * n_ep] = lxx[k];
 }
 
 // Env.augmented_derivative (environment.py:111-132; SI :221-233, Car :420-435, CarPark :567-582) for
@@ -844,8 +1026,30 @@ struct LaunchDdp {
         double* ws = nullptr;
         const int rc = ddp_workspace(const_cast<cacto_sys*>(sys), (size_t)ldS * RC::R * n_ep * sizeof(double), &ws);
         if (rc != CACTO_OK) return rc;
-        hipLaunchKernelGGL(k_ddp_derivs<NJ>, dim3(ceil_div(n_ep, 64), (unsigned)ldS), dim3(64), 0, st, sys->dev, S,
-                           ldS, U, ldU, n, n_ep, ws);
+        // revolute chains: primal / per-direction tangent / cost-derivative kernels (CACTO_DDP_SPLIT=0:
+        // the one-thread-per-step k_ddp_derivs)
+        static const char* split_env = std::getenv("CACTO_DDP_SPLIT");
+        const bool split = NJ > 2 && !(split_env && split_env[0] == '0');
+        if constexpr (NJ > 2) {
+          if (split) {
+            using PC = DdpPrim<NJ>;
+            double* pw = nullptr;
+            const size_t rec_bytes = (size_t)ldS * RC::R * n_ep * sizeof(double);
+            const int rc2 = ddp_workspace(const_cast<cacto_sys*>(sys), rec_bytes + (size_t)ldS * PC::R * n_ep * sizeof(double),
+                                          &ws);
+            if (rc2 != CACTO_OK) return rc2;
+            pw = ws + (size_t)ldS * RC::R * n_ep;
+            const dim3 g(ceil_div(n_ep, 64), (unsigned)ldS);
+            hipLaunchKernelGGL(k_ddp_prim<NJ>, g, dim3(64), 0, st, sys->dev, S, ldS, U, ldU, n, n_ep, ws, pw);
+            CACTO_CHECK_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_ddp_lx<NJ>, g, dim3(64), 0, st, sys->dev, S, ldS, n, n_ep, ws);
+            CACTO_CHECK_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_ddp_tan<NJ>, dim3(g.x, g.y, 2 * NJ), dim3(64), 0, st, sys->dev, S, ldS, n, n_ep, ws, pw);
+          }
+        }
+        if (!split)
+          hipLaunchKernelGGL(k_ddp_derivs<NJ>, dim3(ceil_div(n_ep, 64), (unsigned)ldS), dim3(64), 0, st, sys->dev, S,
+                             ldS, U, ldU, n, n_ep, ws);
         CACTO_CHECK_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_ddp_riccati_wave<NJ>, dim3(n_ep), dim3(64), 0, st, sys->dev, U, ldU, n, n_ep, mu, ws,
                            ldS, out);

@@ -87,3 +87,37 @@ def test_ddp_backward_bad_arguments_fail_loudly():
         L.lib().call("cacto_ddp_backward", to.sys.handle, dptr(S, torch.float64), 0, dptr(U, torch.float64), 3,
                      dptr(torch.tensor([2], dtype=torch.int32, device="cuda"), torch.int32), 1, 1e-9,
                      dptr(S, torch.float64), stream())
+
+
+def _labels_in_subprocess(system, split, S, U, T):
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as d:
+        np.savez(os.path.join(d, "in.npz"), S=S, U=U, T=T)
+        code = ("import sys, numpy as np, torch; sys.path.insert(0, %r)\n"
+                "from cacto_amd.confs import load_conf\nfrom cacto_amd.environment import make_env\n"
+                "from cacto_amd.to import TO\nz = np.load(%r)\nconf = load_conf(%r)\n"
+                "to = TO(make_env(conf), conf, w_S=1e-2)\n"
+                "out = to.backward_pass_batch(*(torch.as_tensor(z[k], device='cuda') for k in ('S', 'U', 'T')))\n"
+                "np.save(%r, out.cpu().numpy())\n") % (root, os.path.join(d, "in.npz"), system,
+                                                       os.path.join(d, "out.npy"))
+        env = dict(os.environ, CACTO_DDP_SPLIT="1" if split else "0")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return np.load(os.path.join(d, "out.npy"))
+
+
+@pytest.mark.parametrize("system", ["manipulator", "ur5"])
+def test_ddp_split_derivative_kernels_equal_the_fused_one(system):
+    """The revolute chains' derivative records from the three split kernels (primal, one dual-number
+    RNEA per direction with the forces in LDS, cost derivatives) are the fused k_ddp_derivs' bit
+    for bit, and so are the labels."""
+    conf, oe, _ = _setup(system)
+    S, U, T = _episodes(conf, oe, 70, random.Random(33), zero_len=(5,))
+    T[7] = -1                                  # a dropped episode: skipped by both
+    a = _labels_in_subprocess(system, True, S, U, T)
+    b = _labels_in_subprocess(system, False, S, U, T)
+    assert np.array_equal(a, b)
