@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(64) k_env_jacobians(const SysDevice* __restric
   }
 }
 
-// Rows -> one-step episodes for k_ddp_derivs: S2 [B, 2, ns] (the state twice), nsteps = 1.
+// Rows -> one-step episodes for the derivative kernels: S2 [B, 2, ns] (the state twice), nsteps = 1.
 template <int NJ>
 __global__ void k_jac_prep(const double* __restrict__ S, int B, double* __restrict__ S2, int32_t* __restrict__ n1) {
   constexpr int ns = Dims<NJ>::NS;
@@ -1076,17 +1076,23 @@ struct LaunchJac {
       }
       if constexpr (NJ > 2) {
         using RC = DdpRec<NJ>;
+        using PC = DdpPrim<NJ>;
         constexpr int ns = Dims<NJ>::NS;
-        const size_t rec = (size_t)2 * RC::R * B, s2 = (size_t)2 * B * ns;
+        // step 0 of B one-step episodes: only A, B are read, so no l_x kernel
+        const size_t rec = (size_t)2 * RC::R * B, pwn = (size_t)PC::R * B, s2 = (size_t)2 * B * ns;
         double* ws = nullptr;
-        const int rc = ddp_workspace(const_cast<cacto_sys*>(sys), (rec + s2 + B) * sizeof(double), &ws);
+        const int rc = ddp_workspace(const_cast<cacto_sys*>(sys), (rec + pwn + s2 + B) * sizeof(double), &ws);
         if (rc != CACTO_OK) return rc;
-        double* S2 = ws + rec;
+        double* pw = ws + rec;
+        double* S2 = pw + pwn;
         int32_t* n1 = reinterpret_cast<int32_t*>(S2 + s2);
         hipLaunchKernelGGL(k_jac_prep<NJ>, dim3(ceil_div(B * 2 * ns, 256)), dim3(256), 0, st, S, B, S2, n1);
         CACTO_CHECK_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_ddp_derivs<NJ>, dim3(ceil_div(B, 64), 2), dim3(64), 0, st, sys->dev, S2, (int64_t)2, U,
-                           (int64_t)1, n1, B, ws);
+        const dim3 g(ceil_div(B, 64), 1);
+        hipLaunchKernelGGL(k_ddp_prim<NJ>, g, dim3(64), 0, st, sys->dev, S2, (int64_t)2, U, (int64_t)1, n1, B, ws, pw);
+        CACTO_CHECK_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_ddp_tan<NJ>, dim3(g.x, 1, 2 * NJ), dim3(64), 0, st, sys->dev, S2, (int64_t)2, n1, B, ws,
+                           pw);
         CACTO_CHECK_HIP(hipGetLastError());
         constexpr int per = RC::N * RC::N + RC::N * RC::M;
         hipLaunchKernelGGL(k_jac_extract<NJ>, dim3(ceil_div(B * per, 256)), dim3(256), 0, st, ws, B, Fx, Fu);

@@ -27,8 +27,7 @@
 #ifdef CACTO_STAMPS
 __device__ unsigned long long g_rstamps[20];
 __device__ unsigned long long g_ttacc[1024 * 2 * 2 * 10];  // [workgroup][team][wave 0/1][phase 0-8, steps]
-__device__ unsigned long long g_wsacc[1024 * 2 * 4 * 7];   // k_rollout_ws: [workgroup][team][wave][phase 0-5, steps]
-                                                           // (k_rollout_ks: [workgroup][wave][...], the same size)
+__device__ unsigned long long g_wsacc[1024 * 8 * 7];  // k_rollout_ks: [workgroup][wave][phase 0-5, steps]
 #define RSTAMP(k)                                                                     \
   do {                                                                                \
     if (blockIdx.x == 0 && threadIdx.x == 0 && it == 20) g_rstamps[k] = __builtin_amdgcn_s_memtime(); \
@@ -636,8 +635,8 @@ __device__ __forceinline__ bool ro_advance(int c, int b, int tc, const double* s
 
 // Env.simulate of the rollout (float64 state and action, f32in = false) with the system scalars it
 // reads held in registers for the whole launch: env_simulate / env_simulate_const read them from
-// the SysDevice parameter block at every call, and in k_rollout_ws that scalar load's latency sat on
-// every step's dynamics. The same operations in the same order as env_simulate(_const).
+// the SysDevice parameter block at every call, and in the one-slot-per-wave kernel that scalar
+// load's latency sat on every step's dynamics. The same operations in the same order as env_simulate(_const).
 struct RoSimScalars {
   double dt, L_delta, tau_delta;
 };
@@ -1081,19 +1080,6 @@ __global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
 #undef TSUB
 }
 
-// ---------------------------------------------------------------- one episode slot per wave
-// k_rollout_ws: the two-team layout of k_rollout_tt (two 4-wave teams of 4 slots per workgroup,
-// team barriers, layer-2 rows shared in LDS), but each wave of a team OWNS one slot and runs that
-// slot's whole sequential chain itself: after layer 2 (all 4 waves, 64 features each, every slot)
-// wave w forms its slot's action (layer 3 — the same 64 lane chains and butterfly as ro_actor,
-// whose P = 64 threads per slot are exactly one wave), steps the dynamics, writes the trajectory,
-// refills its slot from the team's queue, normalises s_{t+1} and evaluates layer 1 of its slot
-// for all 256 features (VALU fmaf chains in q order: a K = 1 MFMA step rounds exactly like fmaf,
-// tools/mb/mfma_fma.hip) straight into the layer-2 operand layout. Per step: two team barriers
-// (h2 published, h1 published) instead of four, and the four slots' serial chains run on four
-// waves side by side instead of on four lanes of one wave. Every per-slot operation is the one
-// the other rollout kernels perform, so outputs are bit-identical to them; which slot runs an
-// episode (queue entries taken by an LDS counter) does not change its result.
 // x[lane] for lanes < N (x uniform across the wave) as a select chain kept in VGPRs: without the
 // empty asm the optimiser turns the chain into an indexed load from a scratch copy of x.
 template <int N, typename V>
@@ -1107,270 +1093,14 @@ __device__ __forceinline__ V lane_pick(const V* x, int lane) {
   return v;
 }
 
-#ifndef RO_WS_SWAP
-#define RO_WS_SWAP 1  // k_rollout_ws layer 3: both actions in one permlane butterfly (0: per action)
-#endif
-template <int NJ>
-struct RoWsTeam {
-  float h1[4 * RoCfg<1>::H1B];  // layer-1 output of the 4 slots, layer-2 broadcast layout
-  float h2[4 * RoCfg<1>::H2S];  // layer-2 output [slot][feature]
-  int act[4];                   // slot active flags, published by the barrier that ends a step
-  int qhead;                    // the team's next queue entry
-  int bar;                      // team barrier arrivals
-};
-
-template <int NJ>
-struct RoWsShared {
-  float4 w2[RoSplitTT::LDSK / 4 * 4 * 64];
-  RoWsTeam<NJ> team[2];
-};
-
-template <int NJ>
-__global__ void __launch_bounds__(2 * CACTO_THREADS, 1)
-    k_rollout_ws(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
-                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
-                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
-  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
-  constexpr int REGK = RoSplitTT::REGK, LDSK = RoSplitTT::LDSK;
-  using C = RoCfg<1>;
-  __shared__ RoWsShared<NJ> Sh;
-  const SysDevice& sd = *sdp;
-  const cacto_sys_params& p = sd.p;
-  const int team = threadIdx.x >> 8;
-  Lane L;
-  // team-local wave (team 1's wave 0 is the workgroup's wave 7: the two teams' wave w sit on
-  // different SIMDs) and thread index; wave w owns slot w
-  L.wave = (L.wave + team) & 3;
-  L.tid = L.wave * 64 + L.lane;
-  const int w = L.wave, lane = L.lane;
-  RoWsTeam<NJ>& S = Sh.team[team];
-  RoActorRegs<ns, REGK> R;
-  float w1[ns][4], b1[4], w3[na][4], b3[na];
-  if (use_actor) {
-    const float* W1 = N.flat + N.t.woff[0];
-    const float* W2 = N.flat + N.t.woff[1];
-    const float* W3 = N.flat + N.t.woff[2];
-    const int f = 64 * w + lane;
-#pragma unroll
-    for (int k = 0; k < REGK; ++k) R.w2[k] = W2[k * 256 + f];
-    R.b2 = N.bias(1, f);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-#pragma unroll
-      for (int q = 0; q < ns; ++q) w1[q][m] = W1[q * 256 + lane + 64 * m];
-      b1[m] = N.bias(0, lane + 64 * m);
-#pragma unroll
-      for (int a = 0; a < na; ++a) w3[a][m] = W3[(lane + 64 * m) * na + a];
-    }
-#pragma unroll
-    for (int a = 0; a < na; ++a) b3[a] = N.bias(2, a);
-    for (int e = threadIdx.x; e < LDSK * 64; e += 2 * CACTO_THREADS) {
-      const int ln = e & 63, wv = (e >> 6) & 3, kq = e >> 8;
-      const int k = REGK + 4 * kq, col = 64 * wv + ln;
-      Sh.w2[e] = make_float4(W2[k * 256 + col], W2[(k + 1) * 256 + col], W2[(k + 2) * 256 + col],
-                             W2[(k + 3) * 256 + col]);
-    }
-  }
-  for (int e = L.tid; e < 4 * C::H1B; e += CACTO_THREADS) S.h1[e] = 0.f;
-  if (L.tid == 0) {
-    S.bar = 0;
-    S.qhead = 0;
-  }
-  __syncthreads();  // the only workgroup barrier: weights and team state in place
-  RoTeamBar tbar{&S.bar, 0, lane};
-  const int vb = 2 * (int)blockIdx.x + team, G = 2 * (int)gridDim.x;
-  // the normalisation of feature `lane` (lanes < ns), fixed for the launch: one division per lane
-  // per step instead of ns in sequence (RoNorm's arithmetic)
-  const RoNorm<ns> nrm(p);
-  float nl = 1.f;
-#pragma unroll
-  for (int q = 0; q < ns; ++q) nl = lane == q ? nrm.n[q] : nl;
-  const bool tl = lane == ns - 1;
-  ConstDyn<NJ> cd;
-  if constexpr (NJ > 0) {
-#pragma unroll
-    for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = sd.cd_L[k];
-#pragma unroll
-    for (int i = 0; i < NJ; ++i) cd.h[i] = sd.cd_h[i];
-  }
-  const RoSimScalars ks{p.dt, p.L_delta, p.tau_delta};
-  // the slot (wave-uniform): active, episode, length, step, s_t
-  bool act = false;
-  int b = 0, n = 0, t = 0;
-  double s[ns];
-#pragma unroll
-  for (int i = 0; i < ns; ++i) s[i] = 0.0;
-
-  // the next queue entries of the team until one has steps (ro_refill's dealing: snake order over
-  // the virtual workgroups vb; zero-length episodes completed on the spot)
-  auto refill = [&]() {
-    act = false;
-    while (true) {
-      int k = 0;
-      if (lane == 0) k = __hip_atomic_fetch_add(&S.qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      k = __builtin_amdgcn_readfirstlane(k);
-      const int r = k * G + ((k & 1) ? G - 1 - vb : vb);
-      if (r >= B) return;
-      const int bb = __builtin_amdgcn_readfirstlane(order ? order[r] : r);
-      const int nn = min(nsteps[bb], T);
-#pragma unroll
-      for (int i = 0; i < ns; ++i) s[i] = S0[(size_t)bb * ns + i];
-      if (Straj && lane < ns) Straj[(size_t)bb * (T + 1) * ns + lane] = lane_pick<ns>(s, lane);
-      if (nn == 0) {
-        if (status && lane == 0) status[bb] = 0;
-        continue;
-      }
-      b = bb;
-      n = nn;
-      t = 0;
-      act = true;
-      return;
-    }
-  };
-  // layer 1 of this wave's slot from s_t: x0[q] = normalise(s_t[q]) on lane q, broadcast through
-  // readlane; h1[k] = lrelu(b1[k] + sum_q x0[q] W1[q][k]) for k = lane + 64 m, written to the
-  // slot's column of the layer-2 operand layout (block m, q = lane & 15, v = lane >> 4)
-  auto layer1 = [&]() {
-    const double sv = lane_pick<ns>(s, lane);
-    const float qv = fdiv((float)sv, nl);
-    const float xv = nrm.on ? (tl ? fsub(fmul(qv, 2.0f), 1.0f) : qv) : (float)sv;
-    float x0[ns];
-#pragma unroll
-    for (int q = 0; q < ns; ++q) x0[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), q));
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float acc = 0.f;
-#pragma unroll
-      for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], w1[q][m], acc);
-      S.h1[m * C::H1B + (lane & 15) * 20 + 4 * w + (lane >> 4)] = lrelu(fadd(acc, b1[m]));
-    }
-  };
-
-#ifdef CACTO_STAMPS
-  // accumulated phase cycles of every step (lane 0 of each wave): [0] loop test + layer 2 + its
-  // barrier, [1] layer 3, [2] s' = f(s, a) + trajectory stores, [3] refill, [4] layer 1, [5] the
-  // end-of-step barrier
-  unsigned long long wacc[6] = {0, 0, 0, 0, 0, 0}, wprev = __builtin_amdgcn_s_memtime();
-  int wsteps = 0;
-  auto wmark = [&](int ph) {
-    const unsigned long long now = __builtin_amdgcn_s_memtime();
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-      if (k == ph) wacc[k] += now - wprev;
-    wprev = now;
-  };
-#define WMARK(k) wmark(k)
-#else
-#define WMARK(k) \
-  do {           \
-  } while (0)
-#endif
-
-  refill();
-  if (act && use_actor) layer1();
-  if (lane == 0) S.act[w] = act;
-  tbar();
-  const float* W2g = N.flat + N.t.woff[1];
-  RoTeamView<na> V{Sh.w2, nullptr, nullptr, S.h1, S.h2, nullptr, nullptr};
-  for (int it = 0;; ++it) {
-    if ((S.act[0] | S.act[1] | S.act[2] | S.act[3]) == 0) break;
-    // every wave has read the flags (above) before any wave rewrites its own below: the layer-2
-    // barrier orders that; without the actor this barrier does
-    if (!use_actor) tbar();
-    float a[na];
-#pragma unroll
-    for (int i = 0; i < na; ++i) a[i] = 0.f;
-    if (use_actor) {
-      ro_layer2<1, ns, REGK, LDSK, true, true>(R, V, W2g, L);
-      tbar();
-      WMARK(0);
-      if (act) {
-        // layer 3 of slot w: lane j's chain over features j, j + 64, j + 128, j + 192, then the
-        // butterfly over the lanes (ro_actor's order with P = 64)
-        float pa[na];
-#pragma unroll
-        for (int i = 0; i < na; ++i) pa[i] = 0.f;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const float h = S.h2[w * C::H2S + lane + 64 * m];
-#pragma unroll
-          for (int i = 0; i < na; ++i) pa[i] = fmaf(w3[i][m], h, pa[i]);
-        }
-        if constexpr (na == 2 && RO_WS_SWAP) {
-          // both actions in one butterfly: v_permlane32_swap leaves lane j < 32 with
-          // pa0[j] + pa0[j + 32] and lane 32 + j with pa1[j] + pa1[j + 32], v_permlane16_swap then
-          // adds row r + 1 into row r of each half, and the row-local DPP levels finish: action 0's
-          // sum on lane 0, action 1's on lane 32. Every add is v[j] + v[j + off], in the order
-          // add_from_above forms it, so the sums are bit-identical (all VALU, no LDS round trip).
-          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[0]), __float_as_uint(pa[1]), false, false);
-          float v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
-          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-          v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
-#pragma unroll
-          for (int off = 8; off >= 1; off >>= 1) v = add_from_above(v, off);
-          a[0] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)), b3[0]);
-          a[1] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)), b3[1 % na]);
-        } else {
-#pragma unroll
-          for (int off = 32; off >= 1; off >>= 1)
-#pragma unroll
-            for (int i = 0; i < na; ++i) pa[i] = add_from_above(pa[i], off);
-#pragma unroll
-          for (int i = 0; i < na; ++i)
-            a[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fadd(pa[i], b3[i]))));
-        }
-      }
-      WMARK(1);
-    }
-    bool fin = false;
-    if (act) {
-      double ad[na], sn[ns];
-#pragma unroll
-      for (int i = 0; i < na; ++i) ad[i] = (double)a[i];
-      ro_simulate<NJ>(ks, cd, s, ad, sn);
-      bool bad = false;
-#pragma unroll
-      for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
-      // the trajectory stores of (a_t, s_{t+1}): one component per lane
-      if (Atraj && lane < na) Atraj[((size_t)b * T + t) * na + lane] = lane_pick<na>(a, lane);
-      if (Straj && lane < ns) Straj[((size_t)b * (T + 1) + t + 1) * ns + lane] = lane_pick<ns>(sn, lane);
-      if (bad && Straj) {
-        // RL.py:229-231 drops the episode; the rest of its trajectory is NaN (the reward / EE pass
-        // skips NaN states)
-        for (int e = lane; e < (n - t - 1) * ns; e += 64)
-          Straj[((size_t)b * (T + 1) + t + 2) * ns + e] = __builtin_nan("");
-      }
-      fin = bad || t + 1 >= n;
-      if (fin && status && lane == 0) status[b] = bad ? 1 : 0;
-#pragma unroll
-      for (int i = 0; i < ns; ++i) s[i] = sn[i];
-      t += 1;
-    }
-    WMARK(2);
-    if (fin) refill();
-    WMARK(3);
-    if (act && use_actor) layer1();
-    if (lane == 0) S.act[w] = act;
-    WMARK(4);
-    tbar();
-    WMARK(5);
-#ifdef CACTO_STAMPS
-    ++wsteps;
-#endif
-  }
-#ifdef CACTO_STAMPS
-  if (lane == 0) {
-    unsigned long long* o = g_wsacc + ((size_t)(blockIdx.x * 2 + team) * 4 + w) * 7;
-    for (int k = 0; k < 6; ++k) o[k] = wacc[k];
-    o[6] = wsteps;
-  }
-#endif
-#undef WMARK
-}
-
 // ---------------------------------------------------------------- one slot per wave, K split
-// k_rollout_ks: one 8-wave workgroup per CU runs 8 episode slots, wave w owning slot w as in
-// k_rollout_ws (layer 3, dynamics, stores, refill and layer 1 of its slot). Layer 2 is split over
+// k_rollout_ks: one 8-wave workgroup per CU runs 8 episode slots, wave w owning slot w: after
+// layer 2 the wave forms its slot's action (layer 3 — ro_actor's P = 64 lane chains per slot are
+// exactly one wave, and the two actions share one permlane butterfly), steps the f64 dynamics,
+// writes the trajectory (one component per lane), refills its slot from the workgroup's queue (an
+// LDS counter: which slot runs an episode does not change its result) and evaluates layer 1 of its
+// slot for all 256 features as fmaf chains straight into the layer-2 operand layout (a K = 1 MFMA
+// step rounds exactly like fmaf, tools/mb/mfma_fma.hip). Layer 2 is split over
 // the waves by feature quarter AND by half of K: wave (fq, h) = (w & 3, w >> 2) multiplies the
 // 128 rows [128 h, 128 h + 128) of W2 for features 64 fq + lane — held in its registers for the
 // whole launch, so the 256 KB of layer-2 weights live in the 8 waves' registers and no weight row
@@ -1440,7 +1170,9 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
 #pragma unroll
   for (int i = 0; i < ns; ++i) s[i] = 0.0;
 
-  auto refill = [&]() {  // k_rollout_ws's refill, over the workgroup's queue
+  // the next queue entries until one has steps (ro_refill's dealing: snake order over the
+  // workgroups; zero-length episodes completed on the spot)
+  auto refill = [&]() {
     act = false;
     while (true) {
       int k = 0;
@@ -1464,7 +1196,10 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
       return;
     }
   };
-  auto layer1 = [&]() {  // k_rollout_ws's layer 1, into this slot's column of the two-group layout
+  // layer 1 of this wave's slot from s_t: x0[q] = normalise(s_t[q]) on lane q, broadcast through
+  // readlane; h1[k] = lrelu(b1[k] + sum_q x0[q] W1[q][k]) for k = lane + 64 m, into the slot's
+  // column of the two-group layer-2 operand layout
+  auto layer1 = [&]() {
     const double sv = lane_pick<ns>(s, lane);
     const float qv = fdiv((float)sv, nl);
     const float xv = nrm.on ? (tl ? fsub(fmul(qv, 2.0f), 1.0f) : qv) : (float)sv;
@@ -1618,261 +1353,6 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
   }
 #endif
 #undef KMARK
-}
-
-// ---------------------------------------------------------------- K split, two slot groups in antiphase
-// k_rollout_kp: k_rollout_ks's layout (8 waves, wave w owns slot w and multiplies W2 rows
-// [128 h, 128 h + 128) for features 64 fq + lane from its registers) with the two groups of 4
-// slots half a step apart. A step is two half-steps; in half-step ph every wave runs layer 2 of
-// group ph ^ 1 (128 MFMAs) while the 4 waves of group ph run their slots' serial part — layer 3
-// from the half sums the previous half-step parked, the dynamics, the stores, the refill, layer 1.
-// Waves w and w + 4 share a SIMD and belong to different groups, so on every SIMD one wave feeds
-// the matrix core while the other runs its slot's VALU / LDS chain (and then its own 128 MFMAs).
-// Same per-slot operations as k_rollout_ks (the same half sums, bit-identical results).
-template <int NJ>
-struct RoKpShared {
-  float h1[2 * 4 * RoCfg<1>::H1B];  // layer-1 output of the 8 slots (groups 0, 1), layer-2 operand layout
-  float P[2][8 * 256];              // layer-2 half sums [k half][slot][feature]
-  int act[2][8];                    // slot active flags by step parity
-  int qhead;
-};
-
-template <int NJ>
-__global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
-    k_rollout_kp(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
-                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
-                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
-  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA;
-  constexpr int H1B = RoCfg<1>::H1B;
-  __shared__ RoKpShared<NJ> Sh;
-  const SysDevice& sd = *sdp;
-  const cacto_sys_params& p = sd.p;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int fq = w & 3, hk = w >> 2;  // layer 2: features 64 fq + lane, rows [128 hk, 128 hk + 128)
-  const int sg = w >> 2, si = w & 3;  // this wave's slot w = 4 sg + si (group, sample)
-  float w2[128], b2[4], w1[ns][4], b1[4], w3[na][4], b3[na];
-  if (use_actor) {
-    const float* W1 = N.flat + N.t.woff[0];
-    const float* W2 = N.flat + N.t.woff[1];
-    const float* W3 = N.flat + N.t.woff[2];
-#pragma unroll
-    for (int k = 0; k < 128; ++k) w2[k] = W2[(128 * hk + k) * 256 + 64 * fq + lane];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-#pragma unroll
-      for (int q = 0; q < ns; ++q) w1[q][m] = W1[q * 256 + lane + 64 * m];
-      b1[m] = N.bias(0, lane + 64 * m);
-      b2[m] = N.bias(1, lane + 64 * m);
-#pragma unroll
-      for (int a = 0; a < na; ++a) w3[a][m] = W3[(lane + 64 * m) * na + a];
-    }
-#pragma unroll
-    for (int a = 0; a < na; ++a) b3[a] = N.bias(2, a);
-  }
-  for (int e = threadIdx.x; e < 2 * 4 * H1B; e += 8 * CACTO_WAVE) Sh.h1[e] = 0.f;
-  if (threadIdx.x == 0) Sh.qhead = 0;
-  __syncthreads();
-  const int vb = (int)blockIdx.x, G = (int)gridDim.x;
-  const RoNorm<ns> nrm(p);
-  float nl = 1.f;
-#pragma unroll
-  for (int q = 0; q < ns; ++q) nl = lane == q ? nrm.n[q] : nl;
-  const bool tl = lane == ns - 1;
-  ConstDyn<NJ> cd;
-  if constexpr (NJ > 0) {
-#pragma unroll
-    for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = sd.cd_L[k];
-#pragma unroll
-    for (int i = 0; i < NJ; ++i) cd.h[i] = sd.cd_h[i];
-  }
-  const RoSimScalars ks{p.dt, p.L_delta, p.tau_delta};
-  bool act = false;
-  int b = 0, n = 0, t = 0;
-  double s[ns];
-#pragma unroll
-  for (int i = 0; i < ns; ++i) s[i] = 0.0;
-
-  auto refill = [&]() {  // k_rollout_ks's refill
-    act = false;
-    while (true) {
-      int k = 0;
-      if (lane == 0) k = __hip_atomic_fetch_add(&Sh.qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      k = __builtin_amdgcn_readfirstlane(k);
-      const int r = k * G + ((k & 1) ? G - 1 - vb : vb);
-      if (r >= B) return;
-      const int bb = __builtin_amdgcn_readfirstlane(order ? order[r] : r);
-      const int nn = min(nsteps[bb], T);
-#pragma unroll
-      for (int i = 0; i < ns; ++i) s[i] = S0[(size_t)bb * ns + i];
-      if (Straj && lane < ns) Straj[(size_t)bb * (T + 1) * ns + lane] = lane_pick<ns>(s, lane);
-      if (nn == 0) {
-        if (status && lane == 0) status[bb] = 0;
-        continue;
-      }
-      b = bb;
-      n = nn;
-      t = 0;
-      act = true;
-      return;
-    }
-  };
-  auto layer1 = [&]() {  // k_rollout_ks's layer 1
-    const double sv = lane_pick<ns>(s, lane);
-    const float qv = fdiv((float)sv, nl);
-    const float xv = nrm.on ? (tl ? fsub(fmul(qv, 2.0f), 1.0f) : qv) : (float)sv;
-    float x0[ns];
-#pragma unroll
-    for (int q = 0; q < ns; ++q) x0[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), q));
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float acc = 0.f;
-#pragma unroll
-      for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], w1[q][m], acc);
-      Sh.h1[(sg * 4 + m) * H1B + (lane & 15) * 20 + 4 * si + (lane >> 4)] = lrelu(fadd(acc, b1[m]));
-    }
-  };
-  // the slot's serial part of one step: action (layer 3 on the parked half sums), dynamics,
-  // trajectory stores, end of episode, refill, next layer-1 column
-  auto slot_step = [&]() {
-    if (!act) return;
-    float a[na];
-#pragma unroll
-    for (int i = 0; i < na; ++i) a[i] = 0.f;
-    if (use_actor) {
-      float pa[na];
-#pragma unroll
-      for (int i = 0; i < na; ++i) pa[i] = 0.f;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int f = lane + 64 * m;
-        const float h = lrelu(fadd(fadd(Sh.P[0][w * 256 + f], Sh.P[1][w * 256 + f]), b2[m]));
-#pragma unroll
-        for (int i = 0; i < na; ++i) pa[i] = fmaf(w3[i][m], h, pa[i]);
-      }
-      if constexpr (na == 2) {
-        const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[0]), __float_as_uint(pa[1]), false, false);
-        float v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
-        const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-        v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) v = add_from_above(v, off);
-        a[0] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)), b3[0]);
-        a[1] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)), b3[1 % na]);
-      } else {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1)
-#pragma unroll
-          for (int i = 0; i < na; ++i) pa[i] = add_from_above(pa[i], off);
-#pragma unroll
-        for (int i = 0; i < na; ++i)
-          a[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(fadd(pa[i], b3[i]))));
-      }
-    }
-    double ad[na], sn[ns];
-#pragma unroll
-    for (int i = 0; i < na; ++i) ad[i] = (double)a[i];
-    ro_simulate<NJ>(ks, cd, s, ad, sn);
-    bool bad = false;
-#pragma unroll
-    for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
-    if (Atraj && lane < na) Atraj[((size_t)b * T + t) * na + lane] = lane_pick<na>(a, lane);
-    if (Straj && lane < ns) Straj[((size_t)b * (T + 1) + t + 1) * ns + lane] = lane_pick<ns>(sn, lane);
-    if (bad && Straj) {
-      for (int e = lane; e < (n - t - 1) * ns; e += 64) Straj[((size_t)b * (T + 1) + t + 2) * ns + e] = __builtin_nan("");
-    }
-    const bool fin = bad || t + 1 >= n;
-    if (fin && status && lane == 0) status[b] = bad ? 1 : 0;
-#pragma unroll
-    for (int i = 0; i < ns; ++i) s[i] = sn[i];
-    t += 1;
-    if (fin) refill();
-    if (act && use_actor) layer1();
-  };
-  const int rd = (lane >> 2) * 20 + 4 * (lane & 3);
-  // layer 2 of slot group gg: this wave's half of K, features 64 fq + lane -> its half sums
-  auto layer2 = [&](int gg) {
-    float4 xa[2];
-#pragma unroll
-    for (int kl = 0; kl < 2; ++kl) xa[kl] = *reinterpret_cast<const float4*>(&Sh.h1[(gg * 4 + 2 * hk + kl) * H1B + rd]);
-    floatx4 acc[2];
-    acc[0] = acc[1] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kl = 0; kl < 2; ++kl)
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-        static_for<16>([&](auto qc) {
-          constexpr int q = decltype(qc)::value;
-          acc[q & 1] = mfma_bc<q>(get4(xa[kl], v), w2[64 * kl + 16 * v + q], acc[q & 1]);
-        });
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Sh.P[hk][(4 * gg + i) * 256 + 64 * fq + lane] = fadd(acc[0][i], acc[1][i]);
-  };
-
-  if (!use_actor) {
-    // zero controls (ep == 0): the slots share nothing but the queue, so every wave steps its own
-    // slot until the queue is empty, without barriers
-    refill();
-    while (act) slot_step();
-    return;
-  }
-
-#ifdef CACTO_STAMPS
-  // accumulated cycles per half-step (lane 0 of each wave): [0] slot part (waves of the active
-  // group), [1] layer 2, [2] barrier; [3] half-steps with a slot part
-  unsigned long long wacc[6] = {0, 0, 0, 0, 0, 0}, wprev = 0;
-  auto wmark = [&](int ph) {
-    const unsigned long long now = __builtin_amdgcn_s_memtime();
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-      if (k == ph) wacc[k] += now - wprev;
-    wprev = now;
-  };
-#define PMARK(k) wmark(k)
-#else
-#define PMARK(k) \
-  do {           \
-  } while (0)
-#endif
-
-  refill();
-  if (act) layer1();
-  if (lane == 0) Sh.act[1][w] = act;  // the flags "of step -1"
-  __syncthreads();
-  layer2(0);  // prologue: group 0's layer 2, so its slots can take the first half-step
-  __syncthreads();
-  for (int st = 0;; ++st) {
-    int any = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) any |= Sh.act[(st + 1) & 1][k];
-    if (any == 0) break;
-#pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-#ifdef CACTO_STAMPS
-      wprev = __builtin_amdgcn_s_memtime();
-#endif
-      // the serial part first: the matrix core is fed by the other group's wave on this SIMD
-      if (sg == ph) {
-        slot_step();
-        if (lane == 0) Sh.act[st & 1][w] = act;
-      }
-      PMARK(0);
-      layer2(ph ^ 1);
-      PMARK(1);
-      __syncthreads();
-      PMARK(2);
-#ifdef CACTO_STAMPS
-      if (sg == ph) wacc[3] += 1;
-#endif
-    }
-  }
-#ifdef CACTO_STAMPS
-  if (lane == 0) {
-    unsigned long long* o = g_wsacc + ((size_t)blockIdx.x * 8 + w) * 7;
-    for (int k = 0; k < 6; ++k) o[k] = wacc[k];
-    o[6] = 0;
-  }
-#endif
-#undef PMARK
 }
 
 // Rewards and end-effector positions of every recorded step (Env.step's reward and
@@ -2065,41 +1545,20 @@ struct LaunchRollout {
     // episodes); car_park's step was slower on two teams (0.42 -> 0.50 ms)
     const bool tt_auto = tt_sys && NJ > 0;
     if (groups < 0 && !tt_sys) {
-      set_error("cacto_rollout_sched: groups -1 / -2 (two teams) need a system without configuration-dependent M");
+      set_error("cacto_rollout_sched: groups -1 / -3 need a system without configuration-dependent M");
       return CACTO_EINVAL;
     }
     // one slot per wave with layer 2 split over K (k_rollout_ks) for every system it can run, up
     // to two episodes per slot. Measured at 4096 episodes (ms per rollout, one MI355X): DI
-    // k_rollout_tt 0.750 / k_rollout_ws 0.630 / k_rollout_ks 0.578; SI single-team 0.519 / ws 0.326
-    // / ks 0.292; car_park single-team 0.432 / ks 0.405; car 1.865 / 1.768.
+    // k_rollout_tt 0.750 / one slot per wave in two teams (round 4, removed) 0.630 / k_rollout_ks
+    // 0.578; SI single-team 0.519 / ks 0.292; car_park single-team 0.432 / ks 0.405; car 1.865 / 1.768.
     const bool ks_auto = tt_sys && B <= 2 * 8 * cus;
-    if (groups == -4) {
-      // k_rollout_ks with the two slot groups half a step apart (k_rollout_kp)
-      if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
-      wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
-      if constexpr (tt_ok)
-        hipLaunchKernelGGL(k_rollout_kp<NJ>, dim3(wgs), dim3(8 * CACTO_WAVE), 0, st, sys->dev, v, S0, n, T,
-                           use_actor, S, A, status, order, B);
-      CACTO_CHECK_HIP(hipGetLastError());
-      if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
-      return CACTO_OK;
-    }
     if (groups == -3 || (groups == 0 && ks_auto)) {
       // one slot per wave, layer 2 split over K (k_rollout_ks), one 8-wave workgroup per CU
       if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
       wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
       if constexpr (tt_ok)
         hipLaunchKernelGGL(k_rollout_ks<NJ>, dim3(wgs), dim3(8 * CACTO_WAVE), 0, st, sys->dev, v, S0, n, T,
-                           use_actor, S, A, status, order, B);
-      CACTO_CHECK_HIP(hipGetLastError());
-      if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
-      return CACTO_OK;
-    }
-    if (groups == -2) {
-      if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
-      wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
-      if constexpr (tt_ok)
-        hipLaunchKernelGGL(k_rollout_ws<NJ>, dim3(wgs), dim3(2 * CACTO_THREADS), 0, st, sys->dev, v, S0, n, T,
                            use_actor, S, A, status, order, B);
       CACTO_CHECK_HIP(hipGetLastError());
       if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
@@ -2159,10 +1618,10 @@ extern "C" int cacto_debug_rollout_stamps(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_rstamps), sizeof(unsigned long long) * 20));
   return CACTO_OK;
 }
-// k_rollout_ws's accumulated phase cycles: 1024 x 2 x 4 x 7 values (see the kernel)
+// k_rollout_ks's accumulated phase cycles: 1024 x 8 x 7 values (see the kernel)
 extern "C" int cacto_debug_rollout_ws_acc(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipDeviceSynchronize());
-  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_wsacc), sizeof(unsigned long long) * 1024 * 2 * 4 * 7));
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_wsacc), sizeof(unsigned long long) * 1024 * 8 * 7));
   return CACTO_OK;
 }
 // k_rollout_tt's accumulated phase cycles: 1024 x 2 x 2 x 10 values (see the kernel)
@@ -2179,9 +1638,9 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
                                    const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
-  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || (groups <= -1 && groups >= -4),
-                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams), -2 (one slot per wave), -3 "
-                "(one slot per wave, layer 2 split over K) or -4 (-3 with the slot groups in antiphase)");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -3,
+                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams) or -3 (one slot per wave, layer 2 "
+                "split over K)");
   CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
   CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
                 "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");

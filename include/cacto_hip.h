@@ -301,10 +301,9 @@ int cacto_rollout(const cacto_sys* sys, const float* actor_netbuf_d, const doubl
 /* cacto_rollout with an explicit schedule: `groups` 4-episode groups per workgroup (1, 2 or 4;
  * 0 = automatic: about two episodes per slot) or, for systems whose step needs no workgroup-wide
  * dynamics (SI, car, car_park and the prismatic DI), an 8-slot workgroup kind: -1 = two
- * independent 4-slot teams (k_rollout_tt), -2 = one slot per wave in two teams (k_rollout_ws),
- * -3 = one slot per wave with layer 2 split over K, the layer-2 weights in registers
- * (k_rollout_ks; automatic for those systems up to two episodes per slot), -4 = -3 with the two
- * slot groups half a step apart (k_rollout_kp); and `workgroups` (0 = one per CU, capped by B).
+ * independent 4-slot teams (k_rollout_tt), -3 = one slot per wave with layer 2 split over K, the
+ * layer-2 weights in registers (k_rollout_ks; automatic for those systems up to two episodes per
+ * slot); and `workgroups` (0 = one per CU, capped by B).
  * Same outputs as cacto_rollout for any schedule (tests use it to force slot refills and to
  * compare the kernels). */
 int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netbuf_d, const double* S0_d,

@@ -86,7 +86,7 @@ def setup():
     return conf, genv, oe, rl, S0, fail, stable
 
 
-@pytest.mark.parametrize("sched", [(1, 3), (-1, 2), (-2, 2), (-2, 1), (-3, 3), (-3, 1), (-4, 3), (-4, 1)])
+@pytest.mark.parametrize("sched", [(1, 3), (-1, 2), (-3, 3), (-3, 1)])
 def test_status_matches_oracle_under_refill(setup, sched):
     conf, genv, oe, rl, S0, fail, stable = setup
     ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]
@@ -106,7 +106,7 @@ def test_status_matches_oracle_under_refill(setup, sched):
             assert np.isnan(S[k, ns_[k]]).any()
 
 
-@pytest.mark.parametrize("sched", [(1, 3), (-1, 2), (-2, 2), (-2, 1), (-3, 3), (-3, 1), (-4, 3), (-4, 1)])
+@pytest.mark.parametrize("sched", [(1, 3), (-1, 2), (-3, 3), (-3, 1)])
 def test_kept_episodes_equal_a_clean_run(setup, sched):
     conf, genv, oe, rl, S0, fail, stable = setup
     ns_ = [conf.NSTEPS - int(s[-1] / conf.dt) for s in S0]

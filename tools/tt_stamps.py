@@ -1,6 +1,7 @@
-"""Diagnostic: per-phase cycles of one step (step 20, workgroup 0) of each team of k_rollout_tt
-(CACTO_STAMPS build). Not part of the product path.
-    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/tt_stamps.py [system]"""
+"""Diagnostic: per-phase cycles of one step (step 20, workgroup 0) of each team of k_rollout_tt,
+or ('ks') per-phase cycles of every step of k_rollout_ks (CACTO_STAMPS build). Not part of the
+product path.
+    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/tt_stamps.py [system] [ks]"""
 import ctypes
 import os
 import sys
@@ -44,47 +45,27 @@ def main():
               ", ".join("%s %.0f" % (n, x) for n, x in zip(names, per)))
 
 
-def ws(system, groups=-2):
-    """k_rollout_ws (groups -2) / k_rollout_ks (groups -3): per-phase cycles per step, every wave."""
+def ks(system):
+    """k_rollout_ks (groups -3): per-phase cycles per step, every wave."""
     conf, env, rl = bench.make_learner(system)
     S0, n = bench.initial_states(env, conf, 4096, seed=0)
     T = int(n.max())
     inputs = rl.rollout_inputs(S0, n)
     for _ in range(3):
-        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(groups, 0))
+        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(-3, 0))
     torch.cuda.synchronize()
-    acc = (ctypes.c_ulonglong * (1024 * 2 * 4 * 7))()
+    acc = (ctypes.c_ulonglong * (1024 * 8 * 7))()
     L.lib().dll.cacto_debug_rollout_ws_acc(acc)
-    a = np.array(acc[:], dtype=np.float64).reshape(1024, 2, 4, 7)
+    a = np.array(acc[:], dtype=np.float64).reshape(1024, 8, 7)
     names = ["loop test + layer 2 + bar", "layer 3", "s'=f(s,a) + stores", "refill", "layer 1", "end barrier"]
     steps = a[..., 6].sum()
-    per = a[..., :6].sum(axis=(0, 1, 2)) / max(steps, 1)
-    print(system, "k_rollout_%s, %d wave-steps: cycles per step %.0f = " % ("ws" if groups == -2 else "ks", steps, per.sum()) +
+    per = a[..., :6].sum(axis=(0, 1)) / max(steps, 1)
+    print(system, "k_rollout_ks, %d wave-steps: cycles per step %.0f = " % (steps, per.sum()) +
           ", ".join("%s %.0f" % (nm, x) for nm, x in zip(names, per)))
 
 
-def kp(system):
-    """k_rollout_kp (groups -4): slot part per step, layer 2 and barrier per half-step."""
-    conf, env, rl = bench.make_learner(system)
-    S0, n = bench.initial_states(env, conf, 4096, seed=0)
-    T = int(n.max())
-    inputs = rl.rollout_inputs(S0, n)
-    for _ in range(3):
-        rl.rollout_batch(None, None, T, inputs=inputs, want=("S", "A"), sched=(-4, 0))
-    torch.cuda.synchronize()
-    acc = (ctypes.c_ulonglong * (1024 * 2 * 4 * 7))()
-    L.lib().dll.cacto_debug_rollout_ws_acc(acc)
-    a = np.array(acc[:], dtype=np.float64).reshape(1024 * 8, 7)
-    steps = a[:, 3].sum()
-    print(system, "k_rollout_kp, %d slot-steps: slot part %.0f per step; per half-step layer 2 %.0f, barrier %.0f"
-          % (steps, a[:, 0].sum() / max(steps, 1), a[:, 1].sum() / max(2 * steps, 1), a[:, 2].sum() / max(2 * steps, 1)))
-
-
 if __name__ == "__main__":
-    if len(sys.argv) > 2 and sys.argv[2] == "kp":
-        kp(sys.argv[1])
-        sys.exit(0)
-    if len(sys.argv) > 2 and sys.argv[2] in ("ws", "ks"):
-        ws(sys.argv[1], -2 if sys.argv[2] == "ws" else -3)
+    if len(sys.argv) > 2 and sys.argv[2] == "ks":
+        ks(sys.argv[1])
         sys.exit(0)
     main()
