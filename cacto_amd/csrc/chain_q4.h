@@ -733,15 +733,21 @@ __global__ void __launch_bounds__(Q4_THREADS)
     k_chain_pair_q4(const SysDevice* __restrict__ sdp, NetView C, NetView Tg, NetView Ac, ChainScalars cs,
                     const double* __restrict__ storage, const int32_t* __restrict__ idx_c,
                     const float* __restrict__ isw, const int32_t* __restrict__ idx_a, int B, int nct, GradBufs gbc,
-                    GradBufs gba, float* __restrict__ y_out, float* __restrict__ V_out, int32_t* __restrict__ step) {
+                    GradBufs gba, float* __restrict__ y_out, float* __restrict__ V_out, int32_t* __restrict__ step,
+                    int nx) {
   constexpr size_t bytes = sizeof(Q4CriticLds) > sizeof(Q4ActorLds) ? sizeof(Q4CriticLds) : sizeof(Q4ActorLds);
   __shared__ __attribute__((aligned(16))) unsigned char smem[bytes];
-  if ((int)blockIdx.x < nct) {
-    q4_critic_chain(*reinterpret_cast<Q4CriticLds*>(smem), blockIdx.x, sdp, C, Tg, cs, storage, idx_c, isw, B, gbc,
-                    y_out, V_out, nullptr, step);
+  // workgroup -> (role, tile): the 2 nct tiles (critic tiles first) on nx of the 8 XCDs. Blocks b
+  // and b + 8 are dealt to one XCD (observed dealing: only which XCD's L2 serves a tile depends on
+  // it, never a result), so blocks with b % 8 >= nx exit at once and tile sl * nx + b % 8 runs on
+  // block b, sl = b / 8: with nx < 8 each weight image is fetched into nx L2s instead of eight.
+  const int x = blockIdx.x & 7, j = (blockIdx.x >> 3) * nx + x;
+  if (x >= nx || j >= 2 * nct) return;
+  if (j < nct) {
+    q4_critic_chain(*reinterpret_cast<Q4CriticLds*>(smem), j, sdp, C, Tg, cs, storage, idx_c, isw, B, gbc, y_out,
+                    V_out, nullptr, step);
   } else {
-    q4_actor_chain<NJ>(*reinterpret_cast<Q4ActorLds*>(smem), blockIdx.x - nct, sdp, Ac, C, cs, storage, idx_a, B, gba,
-                       step);
+    q4_actor_chain<NJ>(*reinterpret_cast<Q4ActorLds*>(smem), j - nct, sdp, Ac, C, cs, storage, idx_a, B, gba, step);
   }
 }
 

@@ -73,12 +73,13 @@ __device__ __forceinline__ float clog_backward(float x, float g) {
 }
 
 // ---------------------------------------------------------------- critic chain (a11)
+// 92.7 KB: with the actor chain's 65 KB one critic and one actor workgroup share a CU (the
+// pipelined large-batch update runs critic(t+1) and actor(t) side by side)
 struct CriticLds {
   float4 X0[64], XT[64], G0[64];
   float4 Cs[24 * 64];  // cos z_l
-  float4 Hs[24 * 64];  // h_l = sin z_l
+  float4 Hs[24 * 64];  // h_l = sin z_l; zbar_l from the Sobolev backward on (the same slot: read, then written)
   float4 G[16 * 64];
-  float4 ZB[24 * 64];
   float4 GB[16 * 64];
   float4 red[4 * 64];
   float st[256], stn[256], dvdx[256];
@@ -92,7 +93,7 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
                                              const float* __restrict__ isw, int B, const GradBufs& gb,
                                              float* __restrict__ y_out, float* __restrict__ V_out,
                                              float* __restrict__ Vt_out, int32_t* __restrict__ step) {
-  float4 *X0 = S.X0, *XT = S.XT, *G0 = S.G0, *Cs = S.Cs, *Hs = S.Hs, *G = S.G, *ZB = S.ZB, *GB = S.GB, *red = S.red;
+  float4 *X0 = S.X0, *XT = S.XT, *G0 = S.G0, *Cs = S.Cs, *Hs = S.Hs, *G = S.G, *ZB = S.Hs, *GB = S.GB, *red = S.red;
   float *st = S.st, *stn = S.stn, *dvdx = S.dvdx, *Rs = S.Rs, *ds = S.ds, *ws = S.ws, *Vn = S.Vn, *V = S.V, *y = S.y,
         *Vb = S.Vb, *Vt2 = S.Vt2;
   CSTAMP_DECL;
@@ -195,6 +196,8 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
     CSTAMP(5);
     // backward of the first backward, l = 0..3 (see oracle/nn.py compute_critic_grad), on the
     // forward fragments (no bias, loaded before the Sobolev loss above)
+    // ZB aliases Hs: each lane reads sin z_l of its element, then writes zbar_l over it (no other
+    // reader of that element is left: later passes read other layers' slots)
     auto sp_epi = [&](int l, float4* nxt) {
       return [&, l, nxt](int ot, floatx4 acc) {
         const float4 sz = Hs[(zoff[l] + ot) * 64 + L.lane], cz = Cs[(zoff[l] + ot) * 64 + L.lane];
@@ -310,11 +313,24 @@ __global__ void __launch_bounds__(CACTO_THREADS)
 }
 
 // ---------------------------------------------------------------- actor chain (a12)
+// Waves per SIMD the large-batch actor chain is compiled for. 2 (<= 256 registers, some spilled)
+// lets one actor and one critic workgroup share a CU: manipulator B = 8192 5.86 k -> 7.14 k
+// updates/s, car_park 8.78 k -> 8.99 k; the DI (10.84 k -> 10.53 k) and UR5 (10.6 k -> 9.1 k:
+// 1.9 KB of spills) keep 1. AG_WPE overrides it for every system (A/B builds).
+template <int NJ>
+constexpr int actor_grad_wpe() {
+#ifdef AG_WPE
+  return AG_WPE;
+#else
+  return (NJ == 3 || NJ == -2) ? 2 : 1;
+#endif
+}
+// 65 KB (see CriticLds). The 40-tile region W holds, in turn: the actor's h1, h2 (tiles 0-31); the
+// critic pass at s' — its h ping-pong (0-15) and cos z (16-39); the actor's zbar2 (16-31).
 struct ActorLds {
   float4 X0[64], XS[64], G0[64], ZB3[64];
-  float4 ZA[32 * 64];  // actor z1, z2
-  float4 H[32 * 64];   // actor h ping-pong; later critic H (16) + actor zbar2 (16)
-  float4 ZC[24 * 64];  // critic cos z at s'
+  float4 W[40 * 64];
+  unsigned char ZS[32 * 64];  // sign bits (z > 0) of the actor's z1, z2: bit r of [(l * 16 + ot) * 64 + lane]
   float4 red[4 * 64];
   float st[256], stn[256], gn[256];
   float A[16 * CACTO_MAX_ACTION];
@@ -330,7 +346,8 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
                                             const NetView& Ac, const NetView& C, const ChainScalars& cs,
                                             const double* __restrict__ storage, const int32_t* __restrict__ idx, int B,
                                             const GradBufs& gb, int32_t* __restrict__ step) {
-  float4 *X0 = S.X0, *XS = S.XS, *G0 = S.G0, *ZB3 = S.ZB3, *ZA = S.ZA, *H = S.H, *ZC = S.ZC, *red = S.red;
+  float4 *X0 = S.X0, *XS = S.XS, *G0 = S.G0, *ZB3 = S.ZB3, *H = S.W, *ZC = S.W + 16 * 64, *red = S.red;
+  unsigned char* ZS = S.ZS;
   float *st = S.st, *stn = S.stn, *gn = S.gn, *A = S.A, *Fu = S.Fu, *dra = S.dra, *Vn = S.Vn;
   double* term_s = S.term_s;
   CSTAMP(0);
@@ -357,7 +374,8 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   __syncthreads();
   // actor forward; h1 -> LT_1, h2 -> LT_2
   CSTAMP(1);
-  actor_forward_tile(Ac, na, X0, ZA, H, red, A, L, [&](int l, int ot, float4, float4 h4) {
+  actor_forward_tile(Ac, na, X0, nullptr, H, red, A, L, [&](int l, int ot, float4 z4, float4 h4) {
+    ZS[(l * 16 + ot) * 64 + L.lane] = (z4.x > 0.f) | (z4.y > 0.f) << 1 | (z4.z > 0.f) << 2 | (z4.w > 0.f) << 3;
     store_panel(gb.LT[l + 1], ld, s0 + L.c, ot, L.g, h4);
   }, &F1);
   __syncthreads();
@@ -453,19 +471,17 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   CSTAMP(7);
   // zbar2 = (abar W3^T) * lrelu'(z2) ; zbar1 = (zbar2 W2^T) * lrelu'(z1)
   auto epi2 = [&](int it, floatx4 acc) {
-    const float4 z = ZA[(16 + it) * 64 + L.lane];
-    const float zz[4] = {z.x, z.y, z.z, z.w};
+    const unsigned zs = ZS[(16 + it) * 64 + L.lane];
     float o[4];
-    for (int r = 0; r < 4; ++r) o[r] = zz[r] > 0.f ? acc[r] : fmul(acc[r], 0.3f);
+    for (int r = 0; r < 4; ++r) o[r] = (zs >> r & 1) ? acc[r] : fmul(acc[r], 0.3f);
     const float4 v = make_float4(o[0], o[1], o[2], o[3]);
     ZB2[it * 64 + L.lane] = v;
     store_panel(gb.RT[1], ld, s0 + L.c, it, L.g, v);
   };
   auto epi1 = [&](int it, floatx4 acc) {
-    const float4 z = ZA[it * 64 + L.lane];
-    const float zz[4] = {z.x, z.y, z.z, z.w};
+    const unsigned zs = ZS[it * 64 + L.lane];
     float o[4];
-    for (int r = 0; r < 4; ++r) o[r] = zz[r] > 0.f ? acc[r] : fmul(acc[r], 0.3f);
+    for (int r = 0; r < 4; ++r) o[r] = (zs >> r & 1) ? acc[r] : fmul(acc[r], 0.3f);
     store_panel(gb.RT[0], ld, s0 + L.c, it, L.g, make_float4(o[0], o[1], o[2], o[3]));
   };
   if (wide) {
@@ -489,7 +505,7 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
 }
 
 template <int NJ>
-__global__ void __launch_bounds__(CACTO_THREADS)
+__global__ void __launch_bounds__(CACTO_THREADS) __attribute__((amdgpu_waves_per_eu(actor_grad_wpe<NJ>(), 8)))
     k_actor_grad(const SysDevice* __restrict__ sdp, NetView Ac, NetView C, ChainScalars cs,
                  const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
                  int32_t* __restrict__ step) {
@@ -1145,6 +1161,22 @@ struct LaunchActorChain {
 };
 
 // nct: critic tiles (= actor tiles) of the batch's chain tile size
+// XCDs the paired q4 grid of 2 nct tiles runs on (k_chain_pair_q4): about 8 tiles per XCD, at
+// most all 8 XCDs. Measured (updates/s, 1 MI355X): manipulator B = 64 (32 tiles) on 8 XCDs 33.4 k,
+// on 4 36.2 k; UR5 B = 64 24.3 k / 29.1 k; DI B = 128 (64 tiles) on 8 39.4 k, on 4 38.3 k.
+// CACTO_PAIR_XCDS (1, 2, 4 or 8) overrides it (read once; benchmarks).
+inline int pair_xcds(int nct) {
+  static const int forced = [] {
+    const char* e = std::getenv("CACTO_PAIR_XCDS");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4 || v == 8) ? v : 0;
+  }();
+  if (forced) return forced;
+  int nx = 1;
+  while (nx < 8 && 2 * nct > 8 * nx) nx *= 2;
+  return nx;
+}
+
 template <int NJ>
 struct LaunchChainPair {
   static int run(const cacto_sys* sys, NetView C, NetView Tg, NetView Ac, ChainScalars cs, const double* storage,
@@ -1153,8 +1185,9 @@ struct LaunchChainPair {
     const int Bp = gbc.Bp;
     if (chain_tile(Bp) == Q4_TILE) {
       const int nct = Bp / Q4_TILE;
-      hipLaunchKernelGGL(k_chain_pair_q4<NJ>, dim3(2 * nct), dim3(Q4_THREADS), 0, st, sys->dev, C, Tg, Ac, cs,
-                         storage, idx_c, isw, idx_a, B, nct, gbc, gba, y, V, step);
+      const int nx = pair_xcds(nct);
+      hipLaunchKernelGGL(k_chain_pair_q4<NJ>, dim3(8 * ceil_div(2 * nct, nx)), dim3(Q4_THREADS), 0, st, sys->dev, C,
+                         Tg, Ac, cs, storage, idx_c, isw, idx_a, B, nct, gbc, gba, y, V, step, nx);
     } else {
       const int nct = Bp / CACTO_TILE;
       hipLaunchKernelGGL(k_chain_pair<NJ>, dim3(2 * nct), dim3(CACTO_THREADS), 0, st, sys->dev, C, Tg, Ac, cs,

@@ -73,6 +73,18 @@ struct NetView {
   __device__ __forceinline__ float w(int l, int i, int o) const { return flat[t.woff[l] + i * t.out[l] + o]; }
 };
 
+// Fragment block blk (64 lanes x float4, wave-uniform index) of a packed weight image A (a
+// kernel-argument pointer, so wave-uniform too) by a buffer load: the block's byte offset goes in
+// an SGPR and the lane's in one VGPR shared by every load, so a pass that issues all its fragment
+// loads up front holds no 64-bit address per load in VGPRs. Same data as A[blk * 64 + lane].
+__device__ __forceinline__ float4 ldfrag(const float4* __restrict__ A, int blk, int lane) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(A), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, blk * 1024, 0));
+}
+// the wave index as a value the compiler knows is wave-uniform (SGPR), for fragment indices
+__device__ __forceinline__ int uniform_wave(int wave) { return __builtin_amdgcn_readfirstlane(wave); }
+
 // The 4 bias values of out tile ot for this lane (features 16 ot + 4 g + r), or zeros.
 __device__ __forceinline__ float4 tile_bias(const float* __restrict__ bias, int ot, int lane) {
   if (!bias) return make_float4(0.f, 0.f, 0.f, 0.f);
@@ -98,18 +110,18 @@ __device__ __forceinline__ floatx4 add_bias(floatx4 acc, const float* bias, floa
 template <int KT, typename Epi>
 __device__ __forceinline__ void mm_layer_t(const float4* __restrict__ A, int OT, const float4* X, int wave, int lane,
                                            Epi&& epi, const float* __restrict__ bias) {
-  int ot = wave;
+  int ot = uniform_wave(wave);
   if (ot >= OT) return;
   float4 a[KT];
 #pragma unroll
-  for (int k = 0; k < KT; ++k) a[k] = A[((size_t)ot * KT + k) * 64 + lane];
+  for (int k = 0; k < KT; ++k) a[k] = ldfrag(A, ot * KT + k, lane);
   float4 bv = tile_bias(bias, ot, lane);
   while (true) {
     const int nxt = ot + CACTO_NWAVES;
     float4 an[KT], bn = bv;
     if (nxt < OT) {
 #pragma unroll
-      for (int k = 0; k < KT; ++k) an[k] = A[((size_t)nxt * KT + k) * 64 + lane];
+      for (int k = 0; k < KT; ++k) an[k] = ldfrag(A, nxt * KT + k, lane);
       bn = tile_bias(bias, nxt, lane);
     }
     // the 4 k-steps of a fragment block go to 4 independent accumulators (issue-bound chain)
@@ -146,11 +158,12 @@ struct Frags {
   template <bool BIAS>
   __device__ __forceinline__ void load(const float4* __restrict__ A, const float* __restrict__ bias, int OT, int wave,
                                        int lane) {
+    wave = uniform_wave(wave);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int ot = min(wave + CACTO_NWAVES * t, OT - 1);
 #pragma unroll
-      for (int k = 0; k < KT; ++k) a[t][k] = A[((size_t)ot * KT + k) * 64 + lane];
+      for (int k = 0; k < KT; ++k) a[t][k] = ldfrag(A, ot * KT + k, lane);
       if (BIAS) {
         const float* bp = bias + 16 * ot + 4 * (lane >> 4);
         b[t] = make_float4(bp[0], bp[1], bp[2], bp[3]);
@@ -198,9 +211,10 @@ struct Frag1 {
   float4 a[NT], b[NT];
   __device__ __forceinline__ void load(const float4* __restrict__ A, const float* __restrict__ bias, int wave,
                                        int lane) {
+    wave = uniform_wave(wave);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      a[t] = A[(size_t)(wave + CACTO_NWAVES * t) * 64 + lane];
+      a[t] = ldfrag(A, wave + CACTO_NWAVES * t, lane);
       b[t] = tile_bias(bias, wave + CACTO_NWAVES * t, lane);
     }
   }
@@ -224,15 +238,16 @@ template <int KT>
 struct FragTile {
   float4 a[KT];
   __device__ __forceinline__ void load(const float4* __restrict__ A, int wave, int lane) {
+    wave = uniform_wave(wave);
 #pragma unroll
-    for (int k = 0; k < KT; ++k) a[k] = A[((size_t)wave * KT + k) * 64 + lane];
+    for (int k = 0; k < KT; ++k) a[k] = ldfrag(A, wave * KT + k, lane);
   }
 };
 // mm_layer_t (no bias) with the first tile's fragments preloaded
 template <int KT, typename Epi>
 __device__ __forceinline__ void mm_layer_t_pre(const FragTile<KT>& F0, const float4* __restrict__ A, int OT,
                                                const float4* X, int wave, int lane, Epi&& epi) {
-  int ot = wave;
+  int ot = uniform_wave(wave);
   if (ot >= OT) return;
   float4 a[KT];
 #pragma unroll
@@ -242,7 +257,7 @@ __device__ __forceinline__ void mm_layer_t_pre(const FragTile<KT>& F0, const flo
     float4 an[KT];
     if (nxt < OT) {
 #pragma unroll
-      for (int k = 0; k < KT; ++k) an[k] = A[((size_t)nxt * KT + k) * 64 + lane];
+      for (int k = 0; k < KT; ++k) an[k] = ldfrag(A, nxt * KT + k, lane);
     }
     floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
 #pragma unroll

@@ -33,10 +33,11 @@ __device__ __forceinline__ void mm_single_tile(const float4* __restrict__ A, int
       if (4 * L.g + r < nout) bq[r] = bias[4 * L.g + r];
   }
   float4 a[4], b[4];
+  const int wave = uniform_wave(L.wave);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int kt = min(L.wave + 4 * i, KT - 1);
-    a[i] = A[kt * 64 + L.lane];
+    const int kt = min(wave + 4 * i, KT - 1);
+    a[i] = ldfrag(A, kt, L.lane);
     b[i] = X[kt * 64 + L.lane];
   }
   floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
@@ -76,8 +77,9 @@ struct SplitFrag {
   template <bool BIAS>
   __device__ __forceinline__ void load(const float4* __restrict__ A, int KT, const float* __restrict__ bias, int nout,
                                        const Lane& L) {
+    const int wave = uniform_wave(L.wave);
 #pragma unroll
-    for (int i = 0; i < NK; ++i) a[i] = A[min(L.wave + 4 * i, KT - 1) * 64 + L.lane];  // branch-free (clamped)
+    for (int i = 0; i < NK; ++i) a[i] = ldfrag(A, min(wave + 4 * i, KT - 1), L.lane);  // branch-free (clamped)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 4 * L.g + r;
