@@ -12,8 +12,8 @@ struct cacto_sys {
   cacto::NetTopo actor, critic;
   void* ddp_ws = nullptr;  // cacto_ddp_backward's per-step derivative records (grow-only)
   size_t ddp_ws_bytes = 0;
-  hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its two events
-  hipEvent_t ev_critic = nullptr, ev_actor[2] = {nullptr, nullptr};
+  hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its events
+  hipEvent_t ev_critic = nullptr, ev_actor[3] = {nullptr, nullptr, nullptr};
   std::mutex pipe_mu;  // one two-stream pipeline at a time per handle (they share side / events)
   // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (layer << 16 | net << 15 | item, -1 = none), for
   // the critic alone, the actor alone and both (built at creation, cacto_build_wgrad_adam_items)

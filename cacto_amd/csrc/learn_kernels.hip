@@ -317,12 +317,15 @@ __global__ void __launch_bounds__(CACTO_THREADS)
 // lets one actor and one critic workgroup share a CU: manipulator B = 8192 5.86 k -> 7.14 k
 // updates/s, car_park 8.78 k -> 8.99 k; the DI (10.84 k -> 10.53 k) and UR5 (10.6 k -> 9.1 k:
 // 1.9 KB of spills) keep 1. AG_WPE overrides it for every system (A/B builds).
+#ifndef AG_RING
+#define AG_RING 24  // fragments in flight in the actor's W2^T pass (mm_layer_ring)
+#endif
 template <int NJ>
 constexpr int actor_grad_wpe() {
 #ifdef AG_WPE
   return AG_WPE;
 #else
-  return (NJ == 3 || NJ == -2) ? 2 : 1;
+  return NJ == 6 ? 1 : 2;
 #endif
 }
 // 65 KB (see CriticLds). The 40-tile region W holds, in turn: the actor's h1, h2 (tiles 0-31); the
@@ -441,11 +444,8 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   // KT = 1, every tile; W2^T: the first tile's 16 blocks); issued after the loads above waited on
   Frag1<4> B2;
   FragTile<16> B1;
-  const bool wide = Ac.t.OT[2] == 1 && Ac.t.KT[2] == 4 * CACTO_NWAVES && Ac.t.KT[1] == 16 && Ac.t.OT[1] == 16;
-  if (wide) {
-    B2.load(Ac.bwd(2), nullptr, L.wave, L.lane);
-    B1.load(Ac.bwd(1), L.wave, L.lane);
-  }
+  B2.load(Ac.bwd(2), nullptr, L.wave, L.lane);
+  B1.load(Ac.bwd(1), L.wave, L.lane);
   __syncthreads();
   if (L.wave == 0) {
     const int c = L.c;
@@ -484,17 +484,12 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
     for (int r = 0; r < 4; ++r) o[r] = (zs >> r & 1) ? acc[r] : fmul(acc[r], 0.3f);
     store_panel(gb.RT[0], ld, s0 + L.c, it, L.g, make_float4(o[0], o[1], o[2], o[3]));
   };
-  if (wide) {
-    mm_layer1_pre<4>(B2, ZB3, L.wave, L.lane, epi2, nullptr);
-    __syncthreads();
-    CSTAMP(8);
-    mm_layer_t_pre<16>(B1, Ac.bwd(1), 16, ZB2, L.wave, L.lane, epi1);
-    __syncthreads();
-  } else {
-    layer(Ac.bwd(2), Ac.t.KT[2], Ac.t.OT[2], ZB3, red, L, epi2);
-    CSTAMP(8);
-    layer(Ac.bwd(1), Ac.t.KT[1], Ac.t.OT[1], ZB2, red, L, epi1);
-  }
+  // the actor's fixed shape (see actor_forward_tile): W3^T KT = 1, W2^T KT = 16, 16 out tiles each
+  mm_layer1_pre<4>(B2, ZB3, L.wave, L.lane, epi2, nullptr);
+  __syncthreads();
+  CSTAMP(8);
+  mm_layer_ring<16, 4, AG_RING>(B1, Ac.bwd(1), ZB2, L.wave, L.lane, epi1);
+  __syncthreads();
   CSTAMP(9);
   __syncthreads();
   CSTAMP_FLUSH;
@@ -559,12 +554,25 @@ struct WgArgs {
 // block loads each LT/RT panel slice once for 4 tiles instead of once per tile.
 constexpr int WG_BLK = 4;
 
-__global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab) {
+//
+// xcd = 1: the items of one chunk run on blocks that share an XCD (blocks b and b + 8 are dealt to
+// one; observed dealing, so it decides only which L2 serves a re-read): chunk (b / 8 / tpc) * 8 +
+// b % 8, item (b / 8) % tpc. The 4 (resp. nbi) blocks that read one LT (RT) slice then read it from
+// one L2 instead of up to four; the grid is padded to whole groups of 8 chunks.
+__global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab, int xcd) {
   // 32 KiB: the 16 tiles are reduced in two rounds of 8, so a GEMM workgroup fits on a CU beside
-  // a chain workgroup (~110 KiB) — the pipelined update runs the two concurrently
+  // a chain workgroup — the pipelined update runs the two concurrently
   __shared__ float4 part[4 * (WG_BLK * WG_BLK / 2) * 64];
-  const int chunk = blockIdx.x / a.tpc;
-  int rem = blockIdx.x - chunk * a.tpc;
+  int chunk, rem;
+  if (xcd) {
+    const int sl = blockIdx.x >> 3;
+    chunk = (sl / a.tpc) * 8 + (blockIdx.x & 7);
+    rem = sl % a.tpc;
+    if (chunk >= a.nch) return;
+  } else {
+    chunk = blockIdx.x / a.tpc;
+    rem = blockIdx.x - chunk * a.tpc;
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   int li = 0;
   while (rem >= a.toff[li + 1]) ++li;
@@ -1218,7 +1226,7 @@ struct Workspace {
   GradBufs crit, act;
   float* slab;    // critic weight-gradient slabs
   float* slab_a;  // actor's (a separate region: cacto_update_n overlaps the two steps)
-  float* cshadow; // second critic net buffer (cacto_update_n alternates the critic between the two)
+  float* cshadow; // two more critic net buffers (cacto_update_n rotates the critic over three)
   int32_t* pidx;  // cacto_update_n_per: sampled indices, two buffers of Bp
   float* pisw;    // and the IS weights of the current update
   float* scal;  // y, V, Vt scratch (3 * Bp)
@@ -1263,9 +1271,9 @@ Workspace plan(const cacto_sys* sys, int B, char* base) {
   w.slab_a = f ? f + off : nullptr;
   off += align64((size_t)nch_a * ta.params);
   w.cshadow = f ? f + off : nullptr;
-  off += align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
+  off += 2 * align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
   w.pidx = f ? reinterpret_cast<int32_t*>(f + off) : nullptr;
-  off += align64((size_t)2 * Bp);
+  off += align64((size_t)3 * Bp);
   w.pisw = f ? f + off : nullptr;
   off += align64((size_t)Bp);
   w.scal = f ? f + off : nullptr;
@@ -1299,7 +1307,14 @@ WgArgs wg_args(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int
 int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int bias_r0, float* slab,
                  hipStream_t st, int* nch) {
   const WgArgs a = wg_args(t, gb, r_begin, r_end, bias_r0);
-  hipLaunchKernelGGL(k_wgrad, dim3(a.nch * a.tpc), dim3(256), 0, st, a, slab);
+  // chunks grouped by XCD from 8 chunks on (CACTO_WG_XCD=0 / 1 forces it off / on; benchmarks)
+  static const int forced = [] {
+    const char* e = std::getenv("CACTO_WG_XCD");
+    return e ? std::atoi(e) : -1;
+  }();
+  const int xcd = forced >= 0 ? forced : a.nch >= 8;
+  const int grid = xcd ? 8 * ceil_div(a.nch, 8) * a.tpc : a.nch * a.tpc;
+  hipLaunchKernelGGL(k_wgrad, dim3(grid), dim3(256), 0, st, a, slab, xcd);
   CACTO_CHECK_HIP(hipGetLastError());
   *nch = a.nch;
   return CACTO_OK;
@@ -1702,12 +1717,16 @@ extern "C" int cacto_update_pair_apply(const cacto_sys* sys, const cacto_nets* n
 // as a two-stream pipeline. The critic step of update t+1 reads only the critic, the target and the
 // rows — never the actor — so it runs while the actor step of update t is still going:
 //   stream : critic chain(t) on C_t, wgrad, Adam(t): C_t -> C_{t+1} (+ soft target update)
-//   side   : [wait Adam(t)], actor chain(t) against C_{t+1}, wgrad, Adam(actor)
-// The critic alternates between the caller's net buffer and a workspace copy (C_t in buffer t % 2),
-// so Adam(t) overwrites the buffer actor chain(t-2) read — the only ordering the stream needs from
-// the side stream (an event two updates old). Every kernel sees the same inputs as in K sequential
-// cacto_update calls, so the results are bit-identical; the final critic is copied back if it ended
-// in the workspace buffer, and the side stream joins the caller's stream before returning.
+//   side   : [wait Adam(t)], actor chain(t) against C_{t+1}, wgrad, Adam(actor), [event]
+// The critic rotates over the caller's net buffer and two workspace copies (C_t in buffer t % 3),
+// so Adam(t) overwrites the buffer actor chain(t-3) read (and, with PER, the sampler of update t
+// the index buffer it read) — the only ordering the stream needs from the side stream: the event
+// of side iteration t-3, recorded after that iteration's Adam, normally long signalled. (With two
+// buffers the event had to follow the actor chain itself, and its record packet cost the side
+// stream — the critical one — a queue gap between the chain and its GEMM.) Every kernel sees the
+// same inputs as in K sequential cacto_update calls, so the results are bit-identical; the final
+// critic is copied back if it ended in a workspace buffer, and the side stream joins the caller's
+// stream before returning.
 namespace {
 // PER state of cacto_update_n_per (replay_buffer.py:139-218)
 struct PerArgs {
@@ -1782,7 +1801,7 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
 int ensure_side_stream(cacto_sys* ms) {
   if (ms->side) return CACTO_OK;
   hipStream_t side = nullptr;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // CACTO_SIDE_PRIO=hi|lo: the side (actor) stream at the device's greatest / least priority
   // (read once; benchmarks). Default: normal priority.
   int prio = 0, least = 0, greatest = 0;
@@ -1794,7 +1813,7 @@ int ensure_side_stream(cacto_sys* ms) {
   // device-scope events (CACTO_EVENT_SYSFENCE=1 restores the system-scope fence): every
   // producer and consumer of these dependencies is a kernel on this device
   const unsigned evf = hipEventDisableTiming | (std::getenv("CACTO_EVENT_SYSFENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
-  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], evf);
+  for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], evf);
   if (e != hipSuccess) {
     for (hipEvent_t x : ev)
       if (x) (void)hipEventDestroy(x);
@@ -1804,6 +1823,7 @@ int ensure_side_stream(cacto_sys* ms) {
   ms->ev_critic = ev[0];
   ms->ev_actor[0] = ev[1];
   ms->ev_actor[1] = ev[2];
+  ms->ev_actor[2] = ev[3];
   ms->side = side;
   return CACTO_OK;
 }
@@ -1819,16 +1839,20 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
   if (int e = ensure_side_stream(ms)) return e;
   const NetTopo& tc = sys->critic;
   const size_t nb_bytes = ((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256) * sizeof(float);
+  const size_t nb_stride = align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
   CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
+  CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow + nb_stride, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));  // everything the caller queued before
   CACTO_CHECK_HIP(hipStreamWaitEvent(ms->side, ms->ev_critic, 0));
-  // cbuf: the buffer (0 caller's, 1 workspace) holding the newest critic; on every exit, error or
+  // cbuf: the buffer (0 caller's, 1-2 workspace) holding the newest critic; on every exit, error or
   // not, the side stream joins the caller's stream and the newest critic lands in the caller's buffer
   int cbuf = 0;
   const int err = update_pipeline_body(sys, nets, cfg, storage_d, idx_d, per, K, B, w, st, &cbuf);
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, ms->side));
   CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
-  if (cbuf) CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow, nb_bytes, hipMemcpyDeviceToDevice, st));
+  if (cbuf)
+    CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow + (cbuf - 1) * nb_stride, nb_bytes,
+                                   hipMemcpyDeviceToDevice, st));
   return err;
 }
 
@@ -1837,17 +1861,18 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
                          const Workspace& w, hipStream_t st, int* cbuf) {
   cacto_sys* ms = const_cast<cacto_sys*>(sys);
   hipStream_t side = ms->side;
-  float* const buf[2] = {nets->critic_d, w.cshadow};
+  const size_t nb_stride = align64((size_t)flat_span(sys->critic) + (size_t)2 * sys->critic.blocks * 256);
+  float* const buf[3] = {nets->critic_d, w.cshadow, w.cshadow + nb_stride};
   float* const y = w.scal;
   float* const V = w.scal + w.Bp;
   const bool late_count = per && B >= cacto_per_mw_min();  // exp_counter += 1 just before the priority update
   for (int t = 0; t < K; ++t) {
-    // actor chain(t-2) read the critic buffer Adam(t) writes and (PER) the index buffer of update t
-    if (t >= 2) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t & 1], 0));
+    // actor chain(t-3) read the critic buffer Adam(t) writes and (PER) the index buffer of update t
+    if (t >= 3) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t % 3], 0));
     const int32_t* idx = idx_d + (size_t)t * B;
     const float* isw = nullptr;
     if (per) {
-      int32_t* pi = w.pidx + (size_t)(t & 1) * w.Bp;
+      int32_t* pi = w.pidx + (size_t)(t % 3) * w.Bp;
       if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
                                    per->uniforms + (size_t)t * B, B, pi, w.pisw, late_count ? nullptr : per->exp_counter, st))
         return e;
@@ -1855,11 +1880,11 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
       isw = w.pisw;
     }
     cacto_nets cur = *nets, nxt = *nets;
-    cur.critic_d = buf[t & 1];
-    nxt.critic_d = buf[(t + 1) & 1];
+    cur.critic_d = buf[t % 3];
+    nxt.critic_d = buf[(t + 1) % 3];
     if (int e = launch_critic_chain(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
     if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d)) return e;
-    *cbuf = (t + 1) & 1;
+    *cbuf = (t + 1) % 3;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
     if (per) {
       if (late_count)
@@ -1870,8 +1895,8 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     }
     CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
-    CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t & 1], side));
     if (int e = actor_step_tail(sys, nets, cfg, w, side)) return e;
+    CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t % 3], side));
   }
   return CACTO_OK;
 }

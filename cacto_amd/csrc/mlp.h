@@ -276,6 +276,35 @@ __device__ __forceinline__ void mm_layer_t_pre(const FragTile<KT>& F0, const flo
   }
 }
 
+// mm_layer_t_pre for a layer of exactly 4 NT out tiles (NT per wave), the wave's NT x KT fragments
+// streamed through a ring of R registers: fragment f = t KT + k is issued R fragments before its
+// MFMAs (the first KT come preloaded), so R, not 2 KT, fragments are live. Same arithmetic.
+template <int KT, int NT, int R, typename Epi>
+__device__ __forceinline__ void mm_layer_ring(const FragTile<KT>& F0, const float4* __restrict__ A, const float4* X,
+                                              int wave, int lane, Epi&& epi) {
+  static_assert(R >= KT && R <= NT * KT, "ring size");
+  constexpr int NF = NT * KT;
+  wave = uniform_wave(wave);
+  float4 ring[R];
+#pragma unroll
+  for (int f = 0; f < R; ++f)
+    ring[f] = f < KT ? F0.a[f] : ldfrag(A, (wave + CACTO_NWAVES * (f / KT)) * KT + f % KT, lane);
+  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int k = f % KT;
+    if (k == 0) c0 = c1 = c2 = c3 = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float4 b = X[k * 64 + lane];
+    const float4 a = ring[f % R];
+    c0 = mfma4(a.x, b.x, c0);
+    c1 = mfma4(a.y, b.y, c1);
+    c2 = mfma4(a.z, b.z, c2);
+    c3 = mfma4(a.w, b.w, c3);
+    if (f + R < NF) ring[f % R] = ldfrag(A, (wave + CACTO_NWAVES * ((f + R) / KT)) * KT + (f + R) % KT, lane);
+    if (k == KT - 1) epi(wave + CACTO_NWAVES * (f / KT), (c0 + c1) + (c2 + c3));
+  }
+}
+
 template <typename Epi>
 __device__ __forceinline__ void mm_layer(const float4* __restrict__ A, int OT, int KT, const float4* X, int wave,
                                          int lane, Epi&& epi, const float* __restrict__ bias = nullptr) {

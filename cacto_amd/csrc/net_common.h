@@ -273,21 +273,25 @@ __device__ void actor_forward_tile(const NetView& N, int na, const float4* X0, f
       out[ot * 64 + L.lane] = h4;
       hook(l, ot, z4, h4);
     };
-    if (l == 0 && F1 && N.t.KT[0] == 1 && N.t.OT[0] == 4 * CACTO_NWAVES) {
+    // the actor's fixed shape (NeuralNetwork.py: ns -> 256 -> 256 -> na, ns <= 16, na <= 16):
+    // layer 1 KT = 1, layer 2 KT = 16, 16 out tiles each (4 per wave)
+    if (l == 0 && F1)
       mm_layer1_pre<4>(*F1, in, L.wave, L.lane, epi, N.biasp(0));
-      __syncthreads();
-    } else {
-      layer(N.fwd(l), N.t.OT[l], N.t.KT[l], in, red, L, epi, N.biasp(l), N.t.out[l]);
-    }
+    else if (l == 0)
+      mm_layer_t<1>(N.fwd(0), 4 * CACTO_NWAVES, in, L.wave, L.lane, epi, N.biasp(0));
+    else
+      mm_layer_t<16>(N.fwd(1), 4 * CACTO_NWAVES, in, L.wave, L.lane, epi, N.biasp(1));
+    __syncthreads();
     PSTAMP(10 + l);
     in = out;
   }
-  layer(N.fwd(2), 1, N.t.KT[2], in, red, L, [&](int, floatx4 acc) {
+  mm_single_tile(N.fwd(2), 4 * CACTO_NWAVES, in, red, L, [&](int, floatx4 acc) {
     for (int r = 0; r < 4; ++r) {
       const int f = 4 * L.g + r;
       if (f < na) A[L.c * na + f] = acc[r];
     }
   }, N.biasp(2), na);
+  __syncthreads();
 }
 
 // Fill one input tile (16 features x 16 samples) from per-sample float32 states in LDS
