@@ -1577,10 +1577,10 @@ struct LaunchRollout {
     // the float64 6-joint chain dynamics need the registers that more slots would take
     constexpr int gmax = 4;
     if (groups <= 0) {
-      // about two episodes per slot; chains of 4+ joints at least 2 groups (their step time is set
-      // by the per-slot float64 dynamics, nearly independent of the slot count)
+      // about two episodes per slot. (UR5 at 2048 episodes: one group, two episodes per slot,
+      // 1.25 ms against 1.28 ms for two groups with one episode per slot, tools/ro_sched.py.)
       const int per = B / (2 * 4 * cus);
-      groups = std::min(gmax, per >= 4 ? 4 : per >= 2 ? 2 : NJ >= 4 ? 2 : 1);
+      groups = std::min(gmax, per >= 4 ? 4 : per >= 2 ? 2 : 1);
     }
     if (groups > gmax) {
       set_error("cacto_rollout_sched: groups above this system's maximum (1 for 6 joints)");
