@@ -577,7 +577,10 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
   q4_layer_pairs<16, true, Q4_NW>(Ac.fwd(1), H, wave, lane, lepi(1), Ac.biasp(1), W2);
   // the critic's forward fragments at s', in flight during the action layer and the dynamics (for
   // the revolute chains after the dynamics: their float64 recursions need the registers)
-  constexpr bool early_cf = NJ <= 2;
+#ifndef Q4_EARLY_CF_NJ
+#define Q4_EARLY_CF_NJ 2
+#endif
+  constexpr bool early_cf = NJ <= Q4_EARLY_CF_NJ;
   Q4CriticFwd<Q4_NW> CF;
   if (early_cf) CF.load<true>(C, wave, lane);
   __syncthreads();
