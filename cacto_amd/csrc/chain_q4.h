@@ -437,78 +437,11 @@ struct Q4ActorLds {
   SysDevice sys;
 };
 
-// env_simulate_derivative (env.h) of a revolute chain for the tile's 4 samples, spread over threads
-// (the 4-sample tile leaves most of the workgroup idle during the float64 dynamics): M(q) by CRBA
-// (wave 1) beside h(q, v) by RNEA (wave 0) — chain_mass / chain_nle, the two halves of chain_terms
-// in its operation order — then per sample NJ + 1 threads each factor M and solve one right-hand
-// side: a - h (the step) or e_j (column j of M^-1, a column of Fu). The same operations on the same
-// values as the one-thread path, so s' and Fu are bit-identical to it. Contains two barriers.
+// the revolute chains' dynamics of the tile's 4 samples spread over threads (chain_dynamics_spread,
+// learn_kernels.hip)
 template <int NJ>
 __device__ __forceinline__ void q4_chain_dynamics(Q4ActorLds& S, const SysDevice& sd, int wave, int lane) {
-  constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
-  const cacto_sys_params& p = sd.p;
-  if (wave < 2 && lane < Q4_TILE) {
-    const int c = lane;
-    double q[NJ], v[NJ];
-#pragma unroll
-    for (int i = 0; i < NJ; ++i) {
-      q[i] = (double)S.st[c * 16 + i];
-      v[i] = (double)S.st[c * 16 + NJ + i];
-    }
-    if (wave == 0) {
-      double h[NJ];
-      chain_nle<NJ>(sd, q, v, h);
-#pragma unroll
-      for (int i = 0; i < NJ; ++i) S.dh[c * NJ + i] = h[i];
-    } else {
-      double M[NJ * NJ];
-      chain_mass<NJ>(sd, q, M);
-#pragma unroll
-      for (int k = 0; k < NJ * NJ; ++k) S.dM[c * NJ * NJ + k] = M[k];
-    }
-  }
-  __syncthreads();
-  CSTAMP(12);
-  if (wave == 0 && lane < Q4_TILE * (NJ + 1)) {
-    const int c = lane / (NJ + 1), j = lane - c * (NJ + 1);
-    const double dt = p.dt;
-    double L[NJ * NJ], x[NJ];
-#pragma unroll
-    for (int k = 0; k < NJ * NJ; ++k) L[k] = S.dM[c * NJ * NJ + k];
-    (void)cholesky<NJ>(L);
-    if (j == 0) {
-#pragma unroll
-      for (int i = 0; i < NJ; ++i) x[i] = (double)S.A[c * NA + i] - S.dh[c * NJ + i];
-      chol_solve<NJ>(L, x);
-      float* sn = S.stn + c * 16;
-#pragma unroll
-      for (int i = 0; i < NJ; ++i) {  // env_simulate_derivative's f32in update
-        const double s = (double)S.st[c * 16 + i], vv = (double)S.st[c * 16 + NJ + i];
-        const float vdt = __fmul_rn((float)vv, (float)dt);
-        sn[i] = (float)(s + (double)vdt);
-        sn[NJ + i] = (float)(double)(float)(vv + x[i] * dt);
-      }
-      sn[2 * NJ] = (float)((double)S.st[c * 16 + 2 * NJ] + dt);
-#pragma unroll
-      for (int f = NS; f < 16; ++f) sn[f] = 0.f;
-    } else {
-      const int col = j - 1;
-#pragma unroll
-      for (int i = 0; i < NJ; ++i) x[i] = (i == col) ? 1.0 : 0.0;
-      chol_solve<NJ>(L, x);
-      float* F = S.Fu + c * CACTO_MAX_STATE * CACTO_MAX_ACTION;
-#pragma unroll
-      for (int r = 0; r < NS; ++r) {
-        double v = 0.0;
-        if (r >= NJ && r < 2 * NJ) {
-          v = x[r - NJ] * dt;
-          if (p.normalize) v *= sd.inv_norm[r];
-        }
-        F[r * NA + col] = (float)v;
-      }
-    }
-  }
-  __syncthreads();
+  chain_dynamics_spread<NJ, Q4_TILE>(sd, S.st, S.A, S.dM, S.dh, S.stn, S.Fu, wave * 64 + lane);
 }
 
 // one 4-sample tile of the actor chain (actor_chain's operations, F4 layout, 8 waves). The actor's

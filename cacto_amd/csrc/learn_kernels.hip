@@ -312,6 +312,83 @@ __global__ void __launch_bounds__(CACTO_THREADS)
   critic_chain(S, blockIdx.x, sdp, C, Tg, cs, storage, idx, isw, B, gb, y_out, V_out, Vt_out, step);
 }
 
+// env_simulate_derivative (env.h) of a revolute chain for a tile's T samples, spread over threads
+// (a tile leaves most of the workgroup idle during the float64 dynamics): M(q) by CRBA (wave 1)
+// beside h(q, v) by RNEA (wave 0) — chain_mass / chain_nle, the two halves of chain_terms in its
+// operation order — then per sample NJ + 1 threads each factor M and solve one right-hand side:
+// a - h (the step) or e_j (column j of M^-1, a column of Fu). The same operations on the same values
+// as the one-thread path, so s' and Fu are bit-identical to it. st / stn: [T][16] floats, A: [T][NA],
+// Fu: [T][CACTO_MAX_STATE * CACTO_MAX_ACTION], dM / dh: float64 scratch. Contains two barriers.
+template <int NJ, int T>
+__device__ __forceinline__ void chain_dynamics_spread(const SysDevice& sd, const float* st, const float* A,
+                                                      double* dM, double* dh, float* stn, float* Fu, int tid) {
+  constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
+  const cacto_sys_params& p = sd.p;
+  const int wave = tid >> 6, lane = tid & 63;
+  if (wave < 2 && lane < T) {
+    const int c = lane;
+    double q[NJ], v[NJ];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) {
+      q[i] = (double)st[c * 16 + i];
+      v[i] = (double)st[c * 16 + NJ + i];
+    }
+    if (wave == 0) {
+      double h[NJ];
+      chain_nle<NJ>(sd, q, v, h);
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) dh[c * NJ + i] = h[i];
+    } else {
+      double M[NJ * NJ];
+      chain_mass<NJ>(sd, q, M);
+#pragma unroll
+      for (int k = 0; k < NJ * NJ; ++k) dM[c * NJ * NJ + k] = M[k];
+    }
+  }
+  __syncthreads();
+  CSTAMP(12);
+  if (tid < T * (NJ + 1)) {
+    const int c = tid / (NJ + 1), j = tid - c * (NJ + 1);
+    const double dt = p.dt;
+    double L[NJ * NJ], x[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ * NJ; ++k) L[k] = dM[c * NJ * NJ + k];
+    (void)cholesky<NJ>(L);
+    if (j == 0) {
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) x[i] = (double)A[c * NA + i] - dh[c * NJ + i];
+      chol_solve<NJ>(L, x);
+      float* sn = stn + c * 16;
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {  // env_simulate_derivative's f32in update
+        const double s = (double)st[c * 16 + i], vv = (double)st[c * 16 + NJ + i];
+        const float vdt = __fmul_rn((float)vv, (float)dt);
+        sn[i] = (float)(s + (double)vdt);
+        sn[NJ + i] = (float)(double)(float)(vv + x[i] * dt);
+      }
+      sn[2 * NJ] = (float)((double)st[c * 16 + 2 * NJ] + dt);
+#pragma unroll
+      for (int f = NS; f < 16; ++f) sn[f] = 0.f;
+    } else {
+      const int col = j - 1;
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) x[i] = (i == col) ? 1.0 : 0.0;
+      chol_solve<NJ>(L, x);
+      float* F = Fu + c * CACTO_MAX_STATE * CACTO_MAX_ACTION;
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        double v = 0.0;
+        if (r >= NJ && r < 2 * NJ) {
+          v = x[r - NJ] * dt;
+          if (p.normalize) v *= sd.inv_norm[r];
+        }
+        F[r * NA + col] = (float)v;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------- actor chain (a12)
 // Waves per SIMD the large-batch actor chain is compiled for. 2 (<= 256 registers, some spilled)
 // lets one actor and one critic workgroup share a CU: manipulator B = 8192 5.86 k -> 7.14 k
@@ -384,7 +461,27 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   __syncthreads();
   CSTAMP(2);
   // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
-  if (L.tid < 16) {
+  if constexpr (NJ >= 4) {
+    // the 6-joint chain spread over the workgroup (one thread per sample held all of it and
+    // spilled); d reward / d a on wave 2 alongside. Its float64 scratch takes the start of the W
+    // region: the actor's h1 / h2 there are dead after the action layer, the critic pass at s'
+    // that fills it comes after.
+    if (L.tid >= 128 && L.tid < 144) {
+      constexpr int NA = Dims<NJ>::NA;
+      const int c = L.tid - 128;
+      float af[NA], g[NA];
+#pragma unroll
+      for (int i = 0; i < NA; ++i) af[i] = A[c * na + i];
+      const double tc = term_s[c];
+      const double w6 = 6 >= p.n_weights ? 0.0 : tc * p.w_terminal[6] + (1.0 - tc) * p.w_running[6];
+      (void)reward_batch_f32<NA>(p, w6, af, 0.0, g);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) dra[c * na + i] = g[i];
+    }
+    double* dM = reinterpret_cast<double*>(S.W);
+    static_assert(sizeof(double) * CACTO_TILE * (NJ * NJ + NJ) <= sizeof(S.W), "chain scratch in W");
+    chain_dynamics_spread<NJ, CACTO_TILE>(sd, st, A, dM, dM + CACTO_TILE * NJ * NJ, stn, Fu, L.tid);
+  } else if (L.tid < 16) {
     constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
     const int c = L.tid;
     double s[NS], a[NA], sn[NS], F[NS * NA];
