@@ -394,6 +394,9 @@ __device__ __forceinline__ void chain_dynamics_spread(const SysDevice& sd, const
 // lets one actor and one critic workgroup share a CU: manipulator B = 8192 5.86 k -> 7.14 k
 // updates/s, car_park 8.78 k -> 8.99 k; the DI (10.84 k -> 10.53 k) and UR5 (10.6 k -> 9.1 k:
 // 1.9 KB of spills) keep 1. AG_WPE overrides it for every system (A/B builds).
+#ifndef AG_SPREAD_NJ
+#define AG_SPREAD_NJ 4  // chains from this many joints take chain_dynamics_spread in the actor chain
+#endif
 #ifndef AG_RING
 #define AG_RING 24  // fragments in flight in the actor's W2^T pass (mm_layer_ring)
 #endif
@@ -461,8 +464,8 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   __syncthreads();
   CSTAMP(2);
   // dynamics at (s, a) in float64 from float32 tensors (environment.py:134-144, :353-362)
-  if constexpr (NJ >= 4) {
-    // the 6-joint chain spread over the workgroup (one thread per sample held all of it and
+  if constexpr (NJ >= AG_SPREAD_NJ) {
+    // revolute chains spread over the workgroup (one thread per sample held all of it; UR5
     // spilled); d reward / d a on wave 2 alongside. Its float64 scratch takes the start of the W
     // region: the actor's h1 / h2 there are dead after the action layer, the critic pass at s'
     // that fills it comes after.
