@@ -1983,9 +1983,19 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   float* const y = w.scal;
   float* const V = w.scal + w.Bp;
   const bool late_count = per && B >= cacto_per_mw_min();  // exp_counter += 1 just before the priority update
+  static const bool every2 = [] {  // CACTO_PIPE_EVERY2=1 (read once; benchmarks)
+    const char* e = std::getenv("CACTO_PIPE_EVERY2");
+    return e && e[0] == '1';
+  }();
   for (int t = 0; t < K; ++t) {
-    // actor chain(t-3) read the critic buffer Adam(t) writes and (PER) the index buffer of update t
-    if (t >= 3) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t % 3], 0));
+    // actor chain(t-3) read the critic buffer Adam(t) writes and (PER) the index buffer of update t.
+    // every2: the side stream records only at even iterations and the critic waits at even t for
+    // side iteration t-2 (which covers t-3 here and at t+1) — half the queue markers on each stream
+    if (every2) {
+      if (t >= 2 && (t & 1) == 0) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[((t - 2) >> 1) & 1], 0));
+    } else if (t >= 3) {
+      CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t % 3], 0));
+    }
     const int32_t* idx = idx_d + (size_t)t * B;
     const float* isw = nullptr;
     if (per) {
@@ -2013,7 +2023,10 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
     if (int e = actor_step_tail(sys, nets, cfg, w, side)) return e;
-    CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t % 3], side));
+    if (!every2)
+      CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t % 3], side));
+    else if ((t & 1) == 0)
+      CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[(t >> 1) & 1], side));
   }
   return CACTO_OK;
 }
