@@ -1983,10 +1983,14 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   float* const y = w.scal;
   float* const V = w.scal + w.Bp;
   const bool late_count = per && B >= cacto_per_mw_min();  // exp_counter += 1 just before the priority update
-  static const bool every2 = [] {  // CACTO_PIPE_EVERY2=1 (read once; benchmarks)
+  // every other iteration with PER (car_park B = 4096: 9.04 k -> 9.36 k updates/s), every iteration
+  // without (manipulator B = 8192 lost 8 % to the tighter wait); CACTO_PIPE_EVERY2=0 / 1 forces it
+  // (read once; benchmarks)
+  static const int every2_env = [] {
     const char* e = std::getenv("CACTO_PIPE_EVERY2");
-    return e && e[0] == '1';
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
+  const bool every2 = every2_env >= 0 ? every2_env == 1 : per != nullptr;
   for (int t = 0; t < K; ++t) {
     // actor chain(t-3) read the critic buffer Adam(t) writes and (PER) the index buffer of update t.
     // every2: the side stream records only at even iterations and the critic waits at even t for
