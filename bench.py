@@ -151,8 +151,12 @@ def dry_run(args):
         dist.all_gather_object(ranks, me)
         dist.destroy_process_group()
     if rank == 0:
+        # the PER loop a real run of this world size times (per_loop against the RL_AC method names)
+        from cacto_amd.rl import RL_AC
+        loop = per_loop(RL_AC.__new__(RL_AC), world)
         print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_requested": args.gpus, "ranks": ranks,
-                          "backend": os.environ.get("CACTO_DIST_BACKEND", "nccl")}))
+                          "backend": os.environ.get("CACTO_DIST_BACKEND", "nccl"),
+                          "per_loop": None if loop is None else loop.__name__}))
 
 
 def pmc_traffic(kernel=("k_rollout_ks<2", "k_rollout_tt<2", "k_rollout<2,")):
@@ -554,25 +558,27 @@ EXTRA = {
 }
 
 
+def per_loop(rl, world):
+    """The PER update loop learn_and_update runs (RL.py:122-137 between checkpoint saves): one rank
+    calls RL_AC.update_rows_n_per (cacto_update_n_per: sample -> update -> priorities, pipelined on
+    two streams); N ranks call RL_AC.update_rows_n_per_dp (rl.py learn_and_update: each rank samples
+    its shard against the union's (sum, min, rows), the paired critic/actor gradients all-reduced in
+    two stages). None with --graph (the sequential loop replayed as one HIP graph)."""
+    if USE_GRAPH and world == 1:
+        return None
+    return rl.update_rows_n_per if world == 1 else rl.update_rows_n_per_dp
+
+
 def per_update_phase(rl, buf, B, K, W, world, seed):
     """learn_and_update with PER (RL.py:122-137): sample (stratified, IS weights) -> update ->
-    priority update, with the per-step uniforms pre-drawn on the device."""
+    priority update, with the per-step uniforms pre-drawn on the device, through the loop the
+    product runs at this rank count (per_loop)."""
     gen = np.random.Generator(np.random.PCG64(seed))
     U = torch.as_tensor(gen.random((K + W, B)), device="cuda")
-    y = torch.empty(B, dtype=torch.float32, device="cuda")
-    V = torch.empty_like(y)
-
-    def step(i):
-        idx, w = buf.sample_device(U[i])
-        rl.update_rows(buf.storage, idx, w, y, V)
-        buf.update_priorities_device(idx, y, V)
-    pipelined = world == 1 and not USE_GRAPH
-    if pipelined:
-        rl.update_rows_n_per(buf, U[:W])        # warm-up on the timed path
-    else:
-        for i in range(W):
-            step(i)
-    graph = rl.capture_updates(None, None, per_buffer=buf, uniforms=U[W:]) if world == 1 and USE_GRAPH else None
+    loop = per_loop(rl, world)
+    if loop is not None:
+        loop(buf, U[:W])                    # warm-up on the timed path
+    graph = rl.capture_updates(None, None, per_buffer=buf, uniforms=U[W:]) if loop is None else None
     cuts = [W + j * K // 5 for j in range(6)]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     barrier(world)
@@ -583,17 +589,13 @@ def per_update_phase(rl, buf, B, K, W, world, seed):
         graph.replay()
     else:
         for j in range(5):
-            if pipelined:
-                rl.update_rows_n_per(buf, U[cuts[j]:cuts[j + 1]])   # sample -> update -> priorities, pipelined
-            else:
-                for i in range(cuts[j], cuts[j + 1]):
-                    step(i)
+            loop(buf, U[cuts[j]:cuts[j + 1]])       # sample -> update -> priorities, K/5 updates per call
             ev[j + 1].record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
     seg = None if graph is not None else update_segments(ev, cuts)
-    return max_over_ranks(t1 - t0, world), seg
+    return max_over_ranks(t1 - t0, world), seg, ("graph" if loop is None else loop.__name__)
 
 
 def extra_system(name, args, world, rank):
@@ -611,13 +613,14 @@ def extra_system(name, args, world, rank):
     ups = {}
     ns, na = conf.nb_state, conf.nb_action
     for B in cfg["batches"]:
+        loop = None
         if cfg["per"]:
             conf.BATCH_SIZE = B
-            wall, seg = per_update_phase(rl, buf, B, args.update_steps, 3, world, seed=300 + rank)
+            wall, seg, loop = per_update_phase(rl, buf, B, args.update_steps, 3, world, seed=300 + rank)
         else:
             wall, seg = update_phase(rl, buf, B, args.update_steps, 3, world, seed=200 + rank)
         flop = B * world * ((9 if cfg["w_S"] else 6) * fc_flops(ns) + 3 * fa_flops(ns, na))
-        ups["B=%d" % B] = dict(value=args.update_steps / wall, unit="critic-updates/s", global_batch=B * world,
+        ups["B=%d" % B] = dict(value=args.update_steps / wall, unit="critic-updates/s", global_batch=B * world, loop=loop,
                                ms_per_update=1e3 * wall / args.update_steps, segments=seg,
                                tflops=flop * args.update_steps / wall / 1e12,
                                mfma_frac=flop * args.update_steps / wall / (FP32_MFMA_PEAK * world))

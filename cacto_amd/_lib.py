@@ -101,7 +101,7 @@ _SIGS = {
     "cacto_per_sample_global": (C.c_int, [vp, vp, i64, i64, dbl, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp]),
     "cacto_per_update": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, dbl, dbl, dbl, vp, C.c_int, vp]),
     "cacto_per_set_leaves": (C.c_int, [vp, vp, i64, vp, vp, C.c_int, vp]),
-    "cacto_per_update_relo": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, dbl, dbl, dbl, vp, vp, C.c_int, vp]),
+    "cacto_per_update_relo": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, dbl, dbl, dbl, vp, vp, vp, C.c_int, vp]),
 }
 
 

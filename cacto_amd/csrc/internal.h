@@ -35,3 +35,6 @@ int cacto_build_wgrad_adam_items(cacto_sys* sys);  // learn_kernels.hip
 // reader), off the sample -> critic chain path
 int cacto_per_mw_min();
 int cacto_per_count_launch(const int32_t* idx_d, int B, double* exp_counter_d, hipStream_t st);
+int cacto_per_update_count(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                           const float* y_d, const float* V_d, double* exp_counter_d, double fresh_factor, double eps,
+                           double alpha, double* max_priority_d, int B, hipStream_t st);

@@ -1854,6 +1854,19 @@ struct PerArgs {
   double *exp_counter, *max_priority;
 };
 
+// The priority update of one PER step (RL.py:129-131). late_count: the sampler left its
+// exp_counter += 1 to this call (large batches), which applies it first, in the same launch. With
+// alpha == 0 the reference skips update_priorities (RL.py:130) — the count still happens.
+int per_priority_update(const PerArgs* per, const int32_t* idx, const float* y, const float* V, int B, bool late_count,
+                        hipStream_t st) {
+  if (per->alpha == 0.0) return late_count ? cacto_per_count_launch(idx, B, per->exp_counter, st) : CACTO_OK;
+  if (late_count)
+    return cacto_per_update_count(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
+                                  per->eps, per->alpha, per->max_priority, B, st);
+  return cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh, per->eps,
+                          per->alpha, per->max_priority, B, st);
+}
+
 // Small batches (fused_adam): one stream, K + 1 steps. Step t runs the critic chain of update t
 // and the actor chain of update t - 1 as one grid (k_chain_pair), then both GEMM + Adam steps as
 // one k_wgrad_adam launch:
@@ -1902,13 +1915,8 @@ int update_pipeline_pair(const cacto_sys* sys, const cacto_nets* nets, const cac
       if (int e = launch_actor_chain(sys, nets, cfg, storage_d, idx_prev, B, w, st)) return e;
       if (int e = launch_wgrad_adam(sys, 1, an, nullptr, nets->step_d, st)) return e;
     }
-    if (per && t < K) {
-      if (late_count)
-        if (int e = cacto_per_count_launch(idx, B, per->exp_counter, st)) return e;
-      if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
-                                   per->eps, per->alpha, per->max_priority, B, st))
-        return e;
-    }
+    if (per && t < K)
+      if (int e = per_priority_update(per, idx, y, V, B, late_count, st)) return e;
     idx_prev = idx;
   }
   return CACTO_OK;
@@ -2017,13 +2025,8 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d)) return e;
     *cbuf = (t + 1) % 3;
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
-    if (per) {
-      if (late_count)
-        if (int e = cacto_per_count_launch(idx, B, per->exp_counter, st)) return e;
-      if (int e = cacto_per_update(per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->fresh,
-                                   per->eps, per->alpha, per->max_priority, B, st))
-        return e;
-    }
+    if (per)
+      if (int e = per_priority_update(per, idx, y, V, B, late_count, st)) return e;
     CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
     if (int e = actor_step_tail(sys, nets, cfg, w, side)) return e;

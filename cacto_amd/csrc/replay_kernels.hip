@@ -261,7 +261,9 @@ __global__ void __launch_bounds__(256) k_per_leaves_mw(double* sum_tree, double*
                                                       const int32_t* __restrict__ idx, const double* __restrict__ vals,
                                                       int n, const float* __restrict__ y, const float* __restrict__ V,
                                                       const double* __restrict__ exp_counter, double fresh, double eps,
-                                                      double alpha, double* max_priority) {
+                                                      double alpha, double* max_priority,
+                                                      const int32_t* __restrict__ skip) {
+  if (skip && *skip) return;
   bool unsorted = false;
   for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) unsorted |= idx[i + 1] < idx[i];
   const bool sorted = !__syncthreads_or(unsorted);
@@ -357,6 +359,155 @@ __global__ void __launch_bounds__(256) k_per_subtrees(double* __restrict__ sum_t
   }
 }
 
+// A whole priority update as one launch over the subtrees of `sub` leaves (large batches): workgroup s
+// owns leaves [cap + s sub, cap + (s + 1) sub), so every sample whose index falls there — every write
+// of those leaves, of their exp_counter entries and of the subtree's internal nodes — belongs to one
+// workgroup, and no two workgroups write the same word. Per workgroup:
+//   1. its samples: with a sorted index list (the stratified sampler's output) the contiguous run
+//      [lower_bound(s sub), lower_bound((s + 1) sub)), two binary searches; otherwise a filter over
+//      the whole list (every workgroup checks the order itself, so all take the same branch);
+//   2. the leaves as k_per_set forms them (p = fresh^count |y - V| + eps in f32, p^alpha; or given
+//      values), duplicates last-write-wins, into the subtree staged in LDS and into the trees;
+//      count = 1 also applies the sampler's exp_counter += 1 first (numpy's fancy-index increment:
+//      once per distinct index; every occurrence reads the old count, the first one then writes
+//      old + 1 after a barrier), so the pipelined update needs no separate counting launch;
+//   3. the subtree's levels rebuilt in LDS and written back (as k_per_subtrees);
+//   4. the last workgroup to finish (a counter in the unused word sum_tree[0], reset to 0 = +0.0
+//      afterwards) rebuilds the nodes above the subtree roots (as k_per_top).
+// max_priority by the atomic bit-pattern max of k_per_leaves_mw. A set `skip` flag (the ReLO
+// priority rule's error status) leaves the trees, counters and max_priority unchanged. Every value
+// is formed as on the k_per_leaves_mw + k_per_count + k_per_subtrees + k_per_top path, so the
+// results are bit-identical to it (and to k_per_set).
+constexpr int PER_FUSED_MAX_ROOTS = PER_SUB;  // the top fits the subtree's LDS arrays
+__global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum_tree, double* __restrict__ min_tree,
+                                                       int64_t cap, int sub, const int32_t* __restrict__ idx,
+                                                       const double* __restrict__ vals, int n,
+                                                       const float* __restrict__ y, const float* __restrict__ V,
+                                                       double* __restrict__ exp_counter, int count, double fresh,
+                                                       double eps, double alpha, double* max_priority,
+                                                       const int32_t* __restrict__ skip) {
+  // 64 KiB: both subtrees and the index list (binary searches and neighbour tests in LDS); the
+  // unused heap slots ts[0] / tm[0] hold the run bounds and the last-workgroup flag
+  __shared__ double ts[2 * PER_SUB], tm[2 * PER_SUB];  // local node j (1-based heap of the subtree)
+  __shared__ int32_t id_s[PER_MAX_B];
+  int* run_s = reinterpret_cast<int*>(&ts[0]);
+  int* last_s = reinterpret_cast<int*>(&tm[0]);
+  if (skip && *skip) return;  // uniform: every workgroup returns, the counter stays 0
+  const int tid = threadIdx.x;
+  const int64_t id_lo = (int64_t)blockIdx.x * sub, id_hi = id_lo + sub;
+  const int64_t leaf0 = cap + id_lo;
+  for (int i = tid; i < n; i += blockDim.x) id_s[i] = idx[i];
+  for (int k = tid; k < sub; k += blockDim.x) {
+    ts[sub + k] = sum_tree[leaf0 + k];
+    tm[sub + k] = min_tree[leaf0 + k];
+  }
+  __syncthreads();
+  bool unsorted = false;
+  for (int i = tid; i + 1 < n; i += blockDim.x) unsorted |= id_s[i + 1] < id_s[i];
+  const bool sorted = !__syncthreads_or(unsorted);
+  if (sorted && tid < 2) {  // lower_bound of id_lo (thread 0) and id_hi (thread 1)
+    const int64_t key = tid ? id_hi : id_lo;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((int64_t)id_s[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    run_s[tid] = lo;
+  }
+  __syncthreads();
+  const int a = sorted ? run_s[0] : 0, b = sorted ? run_s[1] : n;
+  auto mine = [&](int i) {
+    if (sorted) return true;
+    const int64_t id = id_s[i];
+    return id >= id_lo && id < id_hi;
+  };
+  auto first_occ = [&](int i, int32_t id) {
+    if (sorted) return i == 0 || id_s[i - 1] != id;
+    for (int j = 0; j < i; ++j)
+      if (id_s[j] == id) return false;
+    return true;
+  };
+  auto last_occ = [&](int i, int32_t id) {
+    if (sorted) return i + 1 == n || id_s[i + 1] != id;
+    for (int j = i + 1; j < n; ++j)
+      if (id_s[j] == id) return false;
+    return true;
+  };
+  double my_max = -__builtin_inf();
+  for (int i = a + tid; i < b; i += blockDim.x) {
+    if (!mine(i)) continue;
+    const int32_t id = id_s[i];
+    double leaf;
+    if (vals) {
+      leaf = vals[i];
+    } else {
+      const double cnt = exp_counter[id] + (count ? 1.0 : 0.0);
+      const float td = fabsf(__fsub_rn(y[i], V[i]));
+      const float fd = (float)pow(fresh, cnt);
+      const float p = __fadd_rn(__fmul_rn(fd, td), (float)eps);
+      my_max = fmax(my_max, (double)p);
+      leaf = pow((double)p, alpha);
+    }
+    if (last_occ(i, id)) {
+      ts[sub + (id - id_lo)] = leaf;
+      tm[sub + (id - id_lo)] = leaf;
+      sum_tree[cap + id] = leaf;
+      min_tree[cap + id] = leaf;
+    }
+  }
+  if (max_priority) {
+    double m = my_max;
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+    if ((tid & 63) == 0 && m > 0.0)  // false for -inf (no leaf) and NaN
+      atomicMax(reinterpret_cast<unsigned long long*>(max_priority), (unsigned long long)__double_as_longlong(m));
+  }
+  __syncthreads();  // every occurrence has read its old count; the leaves are in LDS
+  if (count && exp_counter && !vals)
+    for (int i = a + tid; i < b; i += blockDim.x) {
+      if (!mine(i)) continue;
+      const int32_t id = id_s[i];
+      if (first_occ(i, id)) exp_counter[id] += 1.0;
+    }
+  int lvl = 0;
+  for (int lo = sub / 2; lo >= 1; lo /= 2) {
+    ++lvl;
+    for (int k = lo + tid; k < 2 * lo; k += blockDim.x) {
+      ts[k] = ts[2 * k] + ts[2 * k + 1];
+      tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
+      const int64_t g = (leaf0 >> lvl) + (k - lo);
+      sum_tree[g] = ts[k];
+      min_tree[g] = tm[k];
+    }
+    __syncthreads();
+  }
+  const int64_t nroot = cap / sub;
+  if (nroot == 1) return;
+  // last workgroup done: release this workgroup's node writes, count, and acquire the others'
+  __threadfence();
+  __syncthreads();
+  unsigned long long* done = reinterpret_cast<unsigned long long*>(sum_tree);
+  if (tid == 0) *last_s = atomicAdd(done, 1ull) == (unsigned long long)(gridDim.x - 1);
+  __syncthreads();
+  if (!*last_s) return;
+  __threadfence();
+  for (int64_t k = nroot + tid; k < 2 * nroot; k += blockDim.x) {
+    ts[k] = __hip_atomic_load(sum_tree + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tm[k] = __hip_atomic_load(min_tree + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  for (int64_t lo = nroot / 2; lo >= 1; lo /= 2) {
+    for (int64_t k = lo + tid; k < 2 * lo; k += blockDim.x) {
+      ts[k] = ts[2 * k] + ts[2 * k + 1];
+      tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
+      sum_tree[k] = ts[k];
+      min_tree[k] = tm[k];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *done = 0ull;  // the +0.0 of segment_tree.py's unused node 0
+}
+
 // The nodes above the subtree roots, [1, cap / sub), from the roots (one workgroup, LDS).
 __global__ void __launch_bounds__(PER_THREADS) k_per_top(double* __restrict__ sum_tree, double* __restrict__ min_tree,
                                                         int64_t nroot) {
@@ -394,8 +545,10 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_set(double* sum_tree, doubl
                                                         const int32_t* __restrict__ idx, const double* __restrict__ vals,
                                                         int n, const float* __restrict__ y, const float* __restrict__ V,
                                                         const double* __restrict__ exp_counter, double fresh, double eps,
-                                                        double alpha, double* max_priority, int leaves_only) {
+                                                        double alpha, double* max_priority, int leaves_only,
+                                                        const int32_t* __restrict__ skip) {
   __shared__ int32_t id_s[PER_MAX_B];
+  if (skip && *skip) return;
   __shared__ double maxp_s[PER_THREADS / 64];
   __shared__ double top_sum[TOP_NODES], top_min[TOP_NODES];
   double my_max = -__builtin_inf();
@@ -544,10 +697,11 @@ int per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int6
 }  // namespace
 
 namespace {
-// Batches of at least PER_MW_MIN samples take the multi-workgroup paths: the descents spread over
-// 64-thread workgroups (+ k_per_count), and the priority update's ancestor refresh as whole subtrees
-// in LDS (k_per_subtrees + k_per_top) after the leaf writes. Smaller batches keep the one-workgroup
-// kernels (fewer launches). Every path forms the same values (bit-identical indices, weights, trees).
+// Batches of at least PER_MW_MIN samples take the multi-workgroup paths: the descents one sample per
+// thread over 256-thread workgroups (+ k_per_count, or the count deferred into the priority update
+// of the pipelined loop), and the priority update as one launch over the subtrees (k_per_update_sub:
+// leaves, count, subtree rebuild in LDS, the top by the last workgroup). Smaller batches keep the
+// one-workgroup kernels (fewer launches). Every path forms the same values (bit-identical indices, weights, trees).
 // CACTO_PER_MW_MIN overrides the bound (read once; benchmarks).
 int per_mw_min() {
   static const int v = [] {
@@ -577,23 +731,43 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
   return CACTO_OK;
 }
 
+// count = 1: exp_counter += 1 (the sampler's count, deferred) applied inside the priority update;
+// skip_d: an int status that, when set, leaves everything unchanged (the ReLO rule's error flag)
 int launch_per_set(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
-                   const double* values_d, int n, const float* y_d, const float* V_d, const double* exp_counter_d,
-                   double fresh, double eps, double alpha, double* max_priority_d, hipStream_t st) {
+                   const double* values_d, int n, const float* y_d, const float* V_d, double* exp_counter_d,
+                   double fresh, double eps, double alpha, double* max_priority_d, hipStream_t st, int count = 0,
+                   const int32_t* skip_d = nullptr) {
+  const int64_t sub = std::min<int64_t>(PER_SUB, capacity), nroot = capacity / sub;
+  const bool mw = n >= per_mw_min();
+  // CACTO_PER_FUSED=0 selects the round-3 multi-workgroup chain (leaves, count, subtrees, top;
+  // read once; A/B and the bit-identity test)
+  static const bool fused_env = [] {
+    const char* e = std::getenv("CACTO_PER_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  if (mw && fused_env && nroot <= PER_FUSED_MAX_ROOTS) {
+    hipLaunchKernelGGL(k_per_update_sub, dim3((unsigned)nroot), dim3(256), 0, st, sum_tree_d, min_tree_d, capacity,
+                       (int)sub, idx_d, values_d, n, y_d, V_d, exp_counter_d, count, fresh, eps, alpha, max_priority_d,
+                       skip_d);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
+  if (count) {
+    hipLaunchKernelGGL(k_per_count, dim3((n + 255) / 256), dim3(256), 0, st, idx_d, n, exp_counter_d);
+    CACTO_CHECK_HIP(hipGetLastError());
+  }
   // k_per_top stages both trees' nroot subtree roots and their parents (4 nroot doubles) in
   // dynamic LDS, which is 64 KiB per workgroup without an opt-in attribute
   constexpr int64_t MW_MAX_ROOTS = 2048;
   static_assert(4 * MW_MAX_ROOTS * sizeof(double) <= 65536, "k_per_top: dynamic LDS above 64 KiB");
-  const int64_t sub = std::min<int64_t>(PER_SUB, capacity), nroot = capacity / sub;
-  const bool mw = n >= per_mw_min() && nroot <= MW_MAX_ROOTS;
-  if (!mw) {
+  if (!mw || nroot > MW_MAX_ROOTS) {
     hipLaunchKernelGGL(k_per_set, dim3(1), dim3(PER_THREADS), 0, st, sum_tree_d, min_tree_d, capacity, idx_d, values_d,
-                       n, y_d, V_d, exp_counter_d, fresh, eps, alpha, max_priority_d, 0);
+                       n, y_d, V_d, exp_counter_d, fresh, eps, alpha, max_priority_d, 0, skip_d);
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
   }
   hipLaunchKernelGGL(k_per_leaves_mw, dim3((n + 255) / 256), dim3(256), 0, st, sum_tree_d, min_tree_d, capacity, idx_d,
-                     values_d, n, y_d, V_d, exp_counter_d, fresh, eps, alpha, max_priority_d);
+                     values_d, n, y_d, V_d, exp_counter_d, fresh, eps, alpha, max_priority_d, skip_d);
   CACTO_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_per_subtrees, dim3((unsigned)nroot), dim3(256), 0, st, sum_tree_d, min_tree_d, capacity, (int)sub);
   CACTO_CHECK_HIP(hipGetLastError());
@@ -611,6 +785,15 @@ int cacto_per_count_launch(const int32_t* idx_d, int B, double* exp_counter_d, h
   hipLaunchKernelGGL(k_per_count, dim3((B + 255) / 256), dim3(256), 0, st, idx_d, B, exp_counter_d);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
+}
+
+// The pipelined PER loop's priority update with the sampler's deferred exp_counter += 1 applied
+// first (the count's only reader is this update): one launch from PER_MW_MIN samples on.
+int cacto_per_update_count(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
+                           const float* y_d, const float* V_d, double* exp_counter_d, double fresh_factor, double eps,
+                           double alpha, double* max_priority_d, int B, hipStream_t st) {
+  return launch_per_set(sum_tree_d, min_tree_d, capacity, idx_d, nullptr, B, y_d, V_d, exp_counter_d, fresh_factor, eps,
+                        alpha, max_priority_d, st, 1);
 }
 
 extern "C" int cacto_per_set_range(double* sum_tree_d, double* min_tree_d, int64_t capacity, int64_t ring_size,
@@ -666,8 +849,8 @@ extern "C" int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t 
   CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && y_d && V_d && exp_counter_d && max_priority_d && pow2(capacity),
                 "cacto_per_update: bad arguments");
   CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_update: 0 < B <= 8192");
-  return launch_per_set(sum_tree_d, min_tree_d, capacity, idx_d, nullptr, B, y_d, V_d, exp_counter_d, fresh_factor, eps,
-                        alpha, max_priority_d, as_stream(stream));
+  return launch_per_set(sum_tree_d, min_tree_d, capacity, idx_d, nullptr, B, y_d, V_d,
+                        const_cast<double*>(exp_counter_d), fresh_factor, eps, alpha, max_priority_d, as_stream(stream));
 }
 
 // update_priorities 'ReLO' (replay_buffer.py:193-196, :200-218; dead in the shipped reference,
@@ -676,38 +859,59 @@ extern "C" int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t 
 // it, np.minimum(np.maximum(td, 0), max(td)); then p = fresh^count (f64) * td_norm (f32 -> f64, numpy
 // promotion) + eps in f64 — unlike the 'PER' branch, whose TF tensor keeps p in f32. One workgroup
 // (B <= PER_MAX_B): the per-sample leaves p^alpha go to leaves[], max_priority takes the batch max.
+// The reference asserts p > 0 for every sample (replay_buffer.py:212). It fails when every td is
+// negative (np.clip's upper bound max(td) < 0 then gives p = fresh^c max(td) + eps, possibly <= 0) or
+// when any td is NaN (np.max propagates it, so every p is NaN): then *status = 1 and nothing is
+// written — no leaf, no max_priority — and the leaf pass that follows skips on the flag, so the
+// trees are unchanged. A set status (sticky until the host clears it) makes later calls no-ops too.
 __global__ void __launch_bounds__(PER_THREADS) k_per_relo(const int32_t* __restrict__ idx, const float* __restrict__ y,
                                                          const float* __restrict__ V, const float* __restrict__ Vt,
                                                          const double* __restrict__ exp_counter, double fresh,
                                                          double eps, double alpha, int B, double* __restrict__ leaves,
-                                                         double* __restrict__ max_priority) {
+                                                         double* __restrict__ max_priority, int32_t* status) {
   __shared__ float red_f[PER_THREADS / 64];
   __shared__ double red_d[PER_THREADS / 64];
+  if (*status) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   auto td_of = [&](int i) {
     const float d1 = __fsub_rn(V[i], y[i]), d2 = __fsub_rn(Vt[i], y[i]);
     return __fsub_rn(__fmul_rn(d1, d1), __fmul_rn(d2, d2));
   };
   float mx = -__builtin_inff();
-  for (int i = tid; i < B; i += blockDim.x) mx = fmaxf(mx, td_of(i));
+  bool nan_td = false;
+  for (int i = tid; i < B; i += blockDim.x) {
+    const float td = td_of(i);
+    nan_td |= td != td;
+    mx = fmaxf(mx, td);
+  }
   for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
   if (lane == 0) red_f[wv] = mx;
   __syncthreads();
   mx = red_f[0];
   for (int k = 1; k < (int)(blockDim.x / 64); ++k) mx = fmaxf(mx, red_f[k]);
   double pm = -__builtin_inf();
-  for (int i = tid; i < B; i += blockDim.x) {
+  bool bad = nan_td;
+  double leaf[PER_MAX_B / PER_THREADS];
+  int k = 0;
+  for (int i = tid; i < B; i += blockDim.x, ++k) {
     const float tn = fminf(fmaxf(td_of(i), 0.f), mx);
     const double p = pow(fresh, exp_counter[idx[i]]) * (double)tn + eps;
-    leaves[i] = pow(p, alpha);
+    bad |= !(p > 0.0);
+    leaf[k] = pow(p, alpha);
     pm = fmax(pm, p);
   }
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) *status = 1;
+    return;
+  }
+  k = 0;
+  for (int i = tid; i < B; i += blockDim.x, ++k) leaves[i] = leaf[k];
   for (int off = 32; off > 0; off >>= 1) pm = fmax(pm, __shfl_xor(pm, off));
   if (lane == 0) red_d[wv] = pm;
   __syncthreads();
   if (tid == 0) {
     double m = max_priority[0];
-    for (int k = 0; k < (int)(blockDim.x / 64); ++k) m = fmax(m, red_d[k]);
+    for (int q = 0; q < (int)(blockDim.x / 64); ++q) m = fmax(m, red_d[q]);
     max_priority[0] = m;
   }
 }
@@ -715,17 +919,18 @@ __global__ void __launch_bounds__(PER_THREADS) k_per_relo(const int32_t* __restr
 extern "C" int cacto_per_update_relo(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
                                      const float* y_d, const float* V_d, const float* Vt_d,
                                      const double* exp_counter_d, double fresh_factor, double eps, double alpha,
-                                     double* max_priority_d, double* leaves_ws_d, int B, void* stream) {
+                                     double* max_priority_d, double* leaves_ws_d, int32_t* status_d, int B,
+                                     void* stream) {
   CACTO_REQUIRE(sum_tree_d && min_tree_d && idx_d && y_d && V_d && Vt_d && exp_counter_d && max_priority_d &&
-                    leaves_ws_d && pow2(capacity),
+                    leaves_ws_d && status_d && pow2(capacity),
                 "cacto_per_update_relo: bad arguments");
   CACTO_REQUIRE(B > 0 && B <= PER_MAX_B, "cacto_per_update_relo: 0 < B <= 8192");
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(k_per_relo, dim3(1), dim3(PER_THREADS), 0, st, idx_d, y_d, V_d, Vt_d, exp_counter_d, fresh_factor,
-                     eps, alpha, B, leaves_ws_d, max_priority_d);
+                     eps, alpha, B, leaves_ws_d, max_priority_d, status_d);
   CACTO_CHECK_HIP(hipGetLastError());
   return launch_per_set(sum_tree_d, min_tree_d, capacity, idx_d, leaves_ws_d, B, nullptr, nullptr, nullptr, 0.0, 0.0,
-                        0.0, nullptr, st);
+                        0.0, nullptr, st, 0, status_d);
 }
 
 extern "C" int cacto_per_set_leaves(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,

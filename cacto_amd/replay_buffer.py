@@ -173,6 +173,7 @@ class PrioritizedReplayBuffer(ReplayBuffer):
         # rule of update_priorities (replay_buffer.py:193-196)
         self.RB_type = getattr(conf, "RB_type", "PER")
         self._relo_ws = None
+        self._relo_status = None    # device int32: the ReLO rule's failed `assert priority > 0`
 
     def _rows_added(self, start, n):
         # leaves = max_priority ** alpha (replay_buffer.py:133-135) with the host's Python float
@@ -234,15 +235,27 @@ class PrioritizedReplayBuffer(ReplayBuffer):
                 raise ValueError("update_priorities with RB_type 'ReLO' needs target_critic_value")
             if self._relo_ws is None or self._relo_ws.numel() < B:
                 self._relo_ws = torch.empty(B, dtype=torch.float64, device=DEVICE)
+            if self._relo_status is None:
+                self._relo_status = torch.zeros(1, dtype=torch.int32, device=DEVICE)
             L.lib().call("cacto_per_update_relo", dptr(self.sum_tree), dptr(self.min_tree), self.cap,
                          dptr(idx, torch.int32), dptr(y.reshape(-1).contiguous(), torch.float32),
                          dptr(V.reshape(-1).contiguous(), torch.float32),
                          dptr(Vt.reshape(-1).contiguous(), torch.float32), dptr(self.exp_counter), self.fresh,
-                         self.eps, self.alpha, dptr(self.max_priority), dptr(self._relo_ws), B, stream())
+                         self.eps, self.alpha, dptr(self.max_priority), dptr(self._relo_ws), dptr(self._relo_status),
+                         B, stream())
             return
         L.lib().call("cacto_per_update", dptr(self.sum_tree), dptr(self.min_tree), self.cap, dptr(idx, torch.int32),
                      dptr(y.reshape(-1).contiguous(), torch.float32), dptr(V.reshape(-1).contiguous(), torch.float32),
                      dptr(self.exp_counter), self.fresh, self.eps, self.alpha, dptr(self.max_priority), B, stream())
+
+    def check_priorities(self):
+        """The reference's `assert priority > 0` (replay_buffer.py:212) for the ReLO rule: the device
+        flags a batch with some p <= 0 or NaN and leaves the trees unchanged; this raises
+        AssertionError once per flagged update (one 4-byte read) and clears the flag."""
+        if self._relo_status is not None and int(self._relo_status.item()):
+            self._relo_status.zero_()
+            raise AssertionError("update_priorities (ReLO): a new priority is not > 0 (every td error negative, "
+                                 "or a NaN td error); the trees were left unchanged")
 
     def update_priorities(self, idxes, reward_to_go_batch, critic_value, target_critic_value=None):
         """replay_buffer.py:190-218 (RB_type 'PER', or 'ReLO' with target_critic_value)."""
@@ -252,6 +265,8 @@ class PrioritizedReplayBuffer(ReplayBuffer):
                                         device=DEVICE).reshape(-1).contiguous()
         self.update_priorities_device(idx, f32(reward_to_go_batch), f32(critic_value),
                                       None if target_critic_value is None else f32(target_critic_value))
+        if self.RB_type == "ReLO":
+            self.check_priorities()
 
     def set_leaves(self, idx, values):
         idx = torch.as_tensor(np.asarray(idx, dtype=np.int32), device=DEVICE)

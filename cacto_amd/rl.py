@@ -323,7 +323,8 @@ class RL_AC:
                 else:
                     idx, w = per_buffer.sample_device(uniforms[k])
                     self.update_rows(per_buffer.storage, idx, w, y, V)
-                    per_buffer.update_priorities_device(idx, y, V)
+                    if per_buffer.alpha != 0:       # RL.py:130
+                        per_buffer.update_priorities_device(idx, y, V)
         g.keep = (y, V)
         return g
 
@@ -420,8 +421,9 @@ class RL_AC:
             if a is not None:
                 L.lib().call("cacto_update_pair_grads_stage", *args, 1, stream())
                 yield "actor", g[Pc:]
-        dp_pipeline(K, stages, self._all_reduce_async,
-                    self._dp_apply(g, cfg, lambda c: buffer.update_priorities_device(drawn[c][0], y, V)))
+        # RL.py:130: no priority update with alpha == 0 (the sampler's count still happens)
+        prio = (lambda c: buffer.update_priorities_device(drawn[c][0], y, V)) if buffer.alpha != 0 else None
+        dp_pipeline(K, stages, self._all_reduce_async, self._dp_apply(g, cfg, prio))
 
     def _dp_grad_buf(self, n):
         if getattr(self, "_dp_g", None) is None or self._dp_g.numel() < n:
@@ -493,7 +495,9 @@ class RL_AC:
             U = torch.as_tensor(np.array([buffer.random.random() for _ in range(B)], dtype=np.float64), device=DEVICE)
             idx, w = buffer.sample_device(U)
             self.update_rows(buffer.storage, idx, w, y, V, Vt)
-            buffer.update_priorities_device(idx, y, V, Vt)
+            if buffer.alpha != 0:                   # RL.py:130
+                buffer.update_priorities_device(idx, y, V, Vt)
+                buffer.check_priorities()           # replay_buffer.py:212 assert priority > 0
             update_step_counter = self._after_step(update_step_counter)
         return update_step_counter
 

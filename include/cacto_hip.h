@@ -403,11 +403,14 @@ int cacto_per_update(double* sum_tree_d, double* min_tree_d, int64_t capacity, c
  * MeanSquaredError, reduction NONE), clipped as np.clip(td, 0, max(td)); p = fresh^count * td + eps
  * in f64; leaves p^alpha (duplicates last-write-wins), max_priority_d[0] = max(max_priority, p).
  * leaves_ws_d: B doubles of caller workspace. Replaces PrioritizedReplayBuffer.update_priorities
- * with RB_type == 'ReLO' (the reference asserts p > 0; the caller keeps that precondition). */
+ * with RB_type == 'ReLO'. The reference asserts p > 0 for every sample (replay_buffer.py:212): when
+ * some p <= 0 (every td negative) or is NaN (any td NaN), *status_d is set to 1 and the trees,
+ * counters and max_priority are left unchanged; a set status makes later calls no-ops until the
+ * caller clears it (the host raises the reference's AssertionError). status_d: one device int32. */
 int cacto_per_update_relo(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
                           const float* y_d, const float* V_d, const float* Vt_d, const double* exp_counter_d,
                           double fresh_factor, double eps, double alpha, double* max_priority_d, double* leaves_ws_d,
-                          int B, void* stream);
+                          int32_t* status_d, int B, void* stream);
 /* Set arbitrary leaves (already raised to alpha) and refresh ancestors; duplicates last-write-wins. */
 int cacto_per_set_leaves(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
                          const double* values_d, int n, void* stream);

@@ -38,6 +38,8 @@ def test_gpus_n_launches_n_ranks(n):
     assert all(x["world_size"] == n for x in d["ranks"])
     if n > 1:
         assert len({x["master"] for x in d["ranks"]}) == 1 and d["ranks"][0]["master"].startswith("127.0.0.1:")
+    # configs[3]'s PER phase times the loop learn_and_update runs at this rank count
+    assert d["per_loop"] == ("update_rows_n_per_dp" if n > 1 else "update_rows_n_per")
 
 
 def test_torchrun_world_is_taken_as_is():

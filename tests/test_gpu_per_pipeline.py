@@ -1,0 +1,105 @@
+"""The large-batch PER loop (configs[3]: car_park, B = 4096) pipelined (cacto_update_n_per) against
+the sequential sample -> update_rows -> update_priorities_device loop, bit for bit, under every
+build-time-free schedule knob the pipeline reads once per process — so each combination runs in
+its own child process:
+  * CACTO_PIPE_EVERY2 = 0 / 1: cross-stream markers every iteration / every other iteration (the
+    default with PER), with the three-buffer critic rotation and the pidx[t % 3] ring;
+  * CACTO_PER_FUSED = 0 / 1: the priority update (with the sampler's deferred exp_counter += 1) as
+    the one-launch subtree kernel k_per_update_sub, or the round-3 chain k_per_count ->
+    k_per_leaves_mw -> k_per_subtrees -> k_per_top.
+K = 6 and 7 (even / odd: the critic ends in the caller's buffer or a workspace copy). Every child
+also writes the trees after a priority update with an unsorted index list holding duplicates
+(B = 1024, the fused kernel's filter path), and all children must agree on every byte.
+replay_buffer.py:139-218, RL.py:120-143."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _child():
+    import torch
+    sys.path.insert(0, ROOT)
+    from cacto_amd.confs import load_conf
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.replay_buffer import PrioritizedReplayBuffer
+    from cacto_amd.rl import RL_AC
+    conf = load_conf("car_park", fresh=True)
+    conf.prioritized_replay_alpha = 0.6
+    env = make_env(conf)
+    ns = conf.nb_state
+    rng = np.random.default_rng(41)
+    N, B = 20000, 4096
+    S = np.column_stack([rng.uniform(-3, 3, (N, ns - 1)), rng.uniform(0, 4.9, N)])
+    rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.01, rng.normal(size=(N, ns)) * 0.3,
+                           np.zeros((N, 1)), np.zeros((N, 1))], axis=1)
+
+    def setup():
+        rl = RL_AC(env, NN(env, conf, w_S=0.0, seed=5), conf)
+        rl.setup_model()
+        buf = PrioritizedReplayBuffer(conf, env.sys)
+        buf.add_rows(rows)
+        return rl, buf
+
+    def state(rl, buf):
+        ts = [rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf, rl.actor_m, rl.actor_v, rl.critic_m,
+              rl.critic_v, rl.steps, buf.sum_tree, buf.min_tree, buf.exp_counter, buf.max_priority]
+        return [t.cpu().numpy() for t in ts]
+
+    out = {}
+    for K in (6, 7):
+        U = torch.as_tensor(np.random.default_rng(100 + K).uniform(size=(K, B)), device="cuda")
+        seq, sbuf = setup()
+        y = torch.empty(B, dtype=torch.float32, device="cuda")
+        V = torch.empty_like(y)
+        for k in range(K):
+            idx, w = sbuf.sample_device(U[k])
+            seq.update_rows(sbuf.storage, idx, w, y, V)
+            sbuf.update_priorities_device(idx, y, V)
+        pipe, pbuf = setup()
+        pipe.update_rows_n_per(pbuf, U)
+        torch.cuda.synchronize()
+        a, b = state(seq, sbuf), state(pipe, pbuf)
+        out["K%d_equal" % K] = all(np.array_equal(x, z) for x, z in zip(a, b))
+        out["K%d_hash" % K] = hashlib.sha256(b"".join(x.tobytes() for x in b)).hexdigest()
+    # an unsorted index list with duplicates through the public priority update
+    _, buf = setup()
+    idx = torch.as_tensor(np.random.default_rng(7).integers(0, 600, size=1024).astype(np.int32), device="cuda")
+    y = torch.as_tensor(np.random.default_rng(8).normal(size=1024).astype(np.float32), device="cuda")
+    V = torch.as_tensor(np.random.default_rng(9).normal(size=1024).astype(np.float32), device="cuda")
+    buf.update_priorities_device(idx, y, V)
+    torch.cuda.synchronize()
+    out["unsorted_hash"] = hashlib.sha256(b"".join(t.cpu().numpy().tobytes() for t in (
+        buf.sum_tree, buf.min_tree, buf.max_priority))).hexdigest()
+    print("RESULT " + json.dumps(out), flush=True)
+
+
+@pytest.mark.gpu
+def test_pipelined_per_b4096_equals_sequential_every_schedule():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = {}
+    for every2 in ("0", "1"):
+        for fused in ("1", "0"):
+            env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused)
+            r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
+                               timeout=300)
+            assert r.returncode == 0, r.stderr[-3000:]
+            line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+            res[(every2, fused)] = json.loads(line[len("RESULT "):])
+    for key, r in res.items():
+        assert r["K6_equal"] and r["K7_equal"], key
+    for field in ("K6_hash", "K7_hash", "unsorted_hash"):
+        assert len({r[field] for r in res.values()}) == 1, field
+
+
+if __name__ == "__main__":
+    _child()
