@@ -121,6 +121,7 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   for (hipEvent_t e : sys->ev_actor)
     if (e) (void)hipEventDestroy(e);
   if (sys->side) (void)hipStreamDestroy(sys->side);
+  if (sys->pipe_sig) (void)hipFree(sys->pipe_sig);
   delete sys;
   return CACTO_OK;
 }

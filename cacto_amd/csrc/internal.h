@@ -15,6 +15,12 @@ struct cacto_sys {
   hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its events
   hipEvent_t ev_critic = nullptr, ev_actor[3] = {nullptr, nullptr, nullptr};
   std::mutex pipe_mu;  // one two-stream pipeline at a time per handle (they share side / events)
+  // device-side ordering of the two-stream pipeline (CACTO_PIPE_DEVWAIT): pipe_sig[0] counts the actor
+  // iterations whose chain has finished, [2] the critic Adam steps finished (both monotonic over the
+  // handle's life), [1] latches a wait that timed out, [3] is k_adam's last-workgroup counter;
+  // pipe_seq is the host's count of pipeline iterations issued before this call
+  unsigned long long* pipe_sig = nullptr;
+  unsigned long long pipe_seq = 0;
   // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (layer << 16 | net << 15 | item, -1 = none), for
   // the critic alone, the actor alone and both (built at creation, cacto_build_wgrad_adam_items)
   int32_t* wa_items[3] = {nullptr, nullptr, nullptr};

@@ -50,7 +50,25 @@ struct ChainScalars {
   int MC;
   int B_global;
   int want_vt;
+  // the two-stream pipeline's device-side ordering (CACTO_PIPE_DEVWAIT): the actor chain waits, before
+  // its critic pass at s', until *wait_p >= wait_v (the critic's Adam of the same update has run)
+  const unsigned long long* wait_p;
+  unsigned long long wait_v;
 };
+
+// The device-side waits of the pipeline: until *wait_p >= wait_v (normally already true: one load).
+// Bounded: after ~2^22 polls (seconds) the wait gives up and latches the timeout word, so an
+// ordering bug cannot hang the GPU. The signal words live in cacto_sys::pipe_sig: [0] actor chains
+// finished, [1] timeout latch, [2] critic Adam steps finished, [3] k_adam's last-workgroup counter.
+__device__ __forceinline__ void pipe_wait(const unsigned long long* wait_p, unsigned long long wait_v,
+                                          unsigned long long* latch) {
+  if (!wait_p) return;
+  for (int k = 0; k < (1 << 22); ++k) {
+    if (__hip_atomic_load(wait_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= wait_v) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __hip_atomic_store(latch, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void store_panel(float* base, int ld, int row, int t, int g, float4 v) {
   float* p = base + (size_t)(16 * t + 4 * g) * ld + row;
@@ -524,6 +542,10 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   __syncthreads();
   CSTAMP(3);
   if (L.wave == 0) fill_input_tile(p, stn, XS, L);
+  if (cs.wait_p) {  // pipeline: the critic this pass reads is written by the other stream's Adam
+    if (L.tid == 0) pipe_wait(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
+    __threadfence();  // acquire at agent scope: no stale L1 / L2 line of that critic buffer
+  }
   __syncthreads();
   // critic (already updated) at s': V and dV/dx0 (NeuralNetwork.py:190-195)
   float4* HC = H;            // 16 tiles
@@ -664,10 +686,17 @@ constexpr int WG_BLK = 4;
 // one; observed dealing, so it decides only which L2 serves a re-read): chunk (b / 8 / tpc) * 8 +
 // b % 8, item (b / 8) % tpc. The 4 (resp. nbi) blocks that read one LT (RT) slice then read it from
 // one L2 instead of up to four; the grid is padded to whole groups of 8 chunks.
-__global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab, int xcd) {
+//
+// sig_p (the pipeline's device-side ordering): this launch follows the actor chain of an iteration
+// on its stream, so that chain has finished; block 0 publishes sig_v = (iterations done) for the
+// critic stream's Adam, which must not overwrite a critic buffer the chain read (k_adam's wait_p).
+__global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab, int xcd,
+                                               unsigned long long* sig_p, unsigned long long sig_v) {
   // 32 KiB: the 16 tiles are reduced in two rounds of 8, so a GEMM workgroup fits on a CU beside
   // a chain workgroup — the pipelined update runs the two concurrently
   __shared__ float4 part[4 * (WG_BLK * WG_BLK / 2) * 64];
+  if (sig_p && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   int chunk, rem;
   if (xcd) {
     const int sl = blockIdx.x >> 3;
@@ -860,11 +889,31 @@ __device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int
 // m, v, the weight and the target value, so a thread waits for one memory latency instead of one per
 // group of 8 chunks plus one per leftover chunk (B = 4096: 32 chunks, ~11 dependent rounds, 11 us);
 // the partials are still summed in chunk order (bit-identical). NCH = 0: any chunk count.
+//
+// wait_p / wait_v: the pipeline's wait before overwriting a critic buffer an actor chain of the other
+// stream read (k_wgrad's sig_p publishes those chains). sig_p / sig_v: after its stores the last
+// workgroup to finish publishes sig_p[2] = sig_v (this Adam step done) for the actor chain's wait.
+__device__ __forceinline__ void adam_publish(unsigned long long* sig_p, unsigned long long sig_v) {
+  if (!sig_p) return;
+  __shared__ int last;
+  __threadfence();  // release this workgroup's stores at agent scope
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(sig_p + 3, 1ull) == (unsigned long long)(gridDim.x - 1);
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    sig_p[3] = 0ull;
+    __threadfence();
+    __hip_atomic_store(sig_p + 2, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int NCH>
 __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, int nch, NetTopo t, const float* src,
                                               float* netbuf, float4* packed, float* __restrict__ m, float* __restrict__ v,
                                               const int32_t* __restrict__ step, AdamArgs a, float* target,
-                                              float4* target_packed) {
+                                              float4* target_packed, const unsigned long long* wait_p,
+                                              unsigned long long wait_v, unsigned long long* sig_p,
+                                              unsigned long long sig_v) {
   if constexpr (NCH > 0) {
     const int p0 = blockIdx.x * blockDim.x + threadIdx.x;
     float q[NCH], mm = 0.f, vv = 0.f, th0 = 0.f, tg0 = 0.f;
@@ -876,23 +925,26 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
     th0 = src[pc];
     if (a.soft) tg0 = target[pc];
     const AdamScalars s = adam_scalars(a, step);
-    if (p0 >= t.params) return;
-    float g = q[0];
+    pipe_wait(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);  // the loads above are in flight
+    if (p0 < t.params) {
+      float g = q[0];
 #pragma unroll
-    for (int k = 1; k < NCH; ++k)
-      if (k < nch) g += q[k];
-    mm = fadd(mm, fmul(fsub(g, mm), s.c1));
-    vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
-    const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
-    m[p0] = mm;
-    v[p0] = vv;
-    netbuf[p0] = th;
-    write_packed(packed, t, p0, th);
-    if (a.soft) {
-      const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
-      target[p0] = tg;
-      write_packed(target_packed, t, p0, tg);
+      for (int k = 1; k < NCH; ++k)
+        if (k < nch) g += q[k];
+      mm = fadd(mm, fmul(fsub(g, mm), s.c1));
+      vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
+      const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
+      m[p0] = mm;
+      v[p0] = vv;
+      netbuf[p0] = th;
+      write_packed(packed, t, p0, th);
+      if (a.soft) {
+        const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
+        target[p0] = tg;
+        write_packed(target_packed, t, p0, tg);
+      }
     }
+    adam_publish(sig_p, sig_v);
     return;
   }
   const int it = step[a.which];  // = Keras iterations + 1
@@ -908,6 +960,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
   const float alpha = fdiv(fmul((float)lr, __fsqrt_rn(fsub(1.f, b2p))), fsub(1.f, b1p));
   const float c1 = (float)(1.0 - a.beta1), c2 = (float)(1.0 - a.beta2), eps = (float)a.eps;
   const float tau = (float)a.tau, omt = (float)(1.0 - a.tau);
+  pipe_wait(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < t.params; p += gridDim.x * blockDim.x) {
     // chunk partials summed in chunk order; loads issued 8 at a time so they overlap
     float g = slab[p];
@@ -934,6 +987,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
       write_packed(target_packed, t, p, tg);
     }
   }
+  adam_publish(sig_p, sig_v);
 }
 
 __global__ void __launch_bounds__(256) k_soft(NetTopo t, const float* __restrict__ src, float* target,
@@ -1269,6 +1323,16 @@ inline int q4_max_bp() {
   return v;
 }
 inline int chain_tile(int Bp) { return Bp <= q4_max_bp() ? Q4_TILE : CACTO_TILE; }
+inline int cu_count() {
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    return (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+               ? v
+               : 256;
+  }();
+  return cus;
+}
 template <int NJ>
 struct LaunchActorChain {
   static int run(const cacto_sys* sys, NetView Ac, NetView C, ChainScalars cs, const double* storage,
@@ -1344,7 +1408,7 @@ struct Workspace {
   float* slab;    // critic weight-gradient slabs
   float* slab_a;  // actor's (a separate region: cacto_update_n overlaps the two steps)
   float* cshadow; // two more critic net buffers (cacto_update_n rotates the critic over three)
-  int32_t* pidx;  // cacto_update_n_per: sampled indices, two buffers of Bp
+  int32_t* pidx;  // cacto_update_n_per: sampled indices, a ring of four buffers of Bp
   float* pisw;    // and the IS weights of the current update
   float* scal;  // y, V, Vt scratch (3 * Bp)
   size_t bytes;
@@ -1390,7 +1454,7 @@ Workspace plan(const cacto_sys* sys, int B, char* base) {
   w.cshadow = f ? f + off : nullptr;
   off += 2 * align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
   w.pidx = f ? reinterpret_cast<int32_t*>(f + off) : nullptr;
-  off += align64((size_t)3 * Bp);
+  off += align64((size_t)4 * Bp);
   w.pisw = f ? f + off : nullptr;
   off += align64((size_t)Bp);
   w.scal = f ? f + off : nullptr;
@@ -1422,7 +1486,7 @@ WgArgs wg_args(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int
 
 // the weight-gradient GEMM of one network into its slabs; returns the chunk count k_adam sums
 int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int bias_r0, float* slab,
-                 hipStream_t st, int* nch) {
+                 hipStream_t st, int* nch, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
   const WgArgs a = wg_args(t, gb, r_begin, r_end, bias_r0);
   // chunks grouped by XCD from 8 chunks on (CACTO_WG_XCD=0 / 1 forces it off / on; benchmarks)
   static const int forced = [] {
@@ -1431,7 +1495,7 @@ int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, i
   }();
   const int xcd = forced >= 0 ? forced : a.nch >= 8;
   const int grid = xcd ? 8 * ceil_div(a.nch, 8) * a.tpc : a.nch * a.tpc;
-  hipLaunchKernelGGL(k_wgrad, dim3(grid), dim3(256), 0, st, a, slab, xcd);
+  hipLaunchKernelGGL(k_wgrad, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
   CACTO_CHECK_HIP(hipGetLastError());
   *nch = a.nch;
   return CACTO_OK;
@@ -1443,6 +1507,8 @@ ChainScalars chain_scalars(const cacto_update_cfg* cfg, int B) {
   cs.MC = cfg->MC;
   cs.B_global = cfg->B_global > 0 ? cfg->B_global : B;
   cs.want_vt = cfg->want_target_V;
+  cs.wait_p = nullptr;
+  cs.wait_v = 0;
   return cs;
 }
 
@@ -1496,10 +1562,13 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
 }
 
 int launch_actor_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
-                       const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st) {
+                       const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
+                       const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0) {
   NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
   NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
-  const ChainScalars cs = chain_scalars(cfg, B);
+  ChainScalars cs = chain_scalars(cfg, B);
+  cs.wait_p = wait_p;
+  cs.wait_v = wait_v;
   return dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st);
 }
 
@@ -1513,7 +1582,9 @@ int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, c
 // src: the weights the step starts from (nullptr = in place; cacto_update_n steps the critic from one
 // buffer into the other)
 int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, int which,
-                const float* slab, int nch, int soft, hipStream_t st, const float* src = nullptr) {
+                const float* slab, int nch, int soft, hipStream_t st, const float* src = nullptr,
+                const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0,
+                unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
   const NetTopo& t = topo(sys, which);
   float* nb = which == CACTO_NET_CRITIC ? nets->critic_d : nets->actor_d;
   float* m = which == CACTO_NET_CRITIC ? nets->critic_m_d : nets->actor_m_d;
@@ -1526,7 +1597,7 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
   const int full = (t.params + 255) / 256;
   auto go = [&](auto kern, int grid) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, slab, nch, t, s0, nb, pk, m, v, nets->step_d, aa,
-                       nets->target_d, tpk);
+                       nets->target_d, tpk, wait_p, wait_v, sig_p, sig_v);
   };
   if (nch <= 8) go(k_adam<8>, full);
   else if (nch <= 16) go(k_adam<16>, full);
@@ -1597,7 +1668,8 @@ int launch_wgrad_adam(const cacto_sys* sys, int mode, const AdamNet& n0, const A
 
 // critic step after its chain: GEMM + Adam (+ soft update) from src into nb
 int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
-                     hipStream_t st, const float* src, float* nb) {
+                     hipStream_t st, const float* src, float* nb, const unsigned long long* wait_p = nullptr,
+                     unsigned long long wait_v = 0, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
   const int soft = cfg->MC ? 0 : 1;
   if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 0, critic_adam_net(sys, nets, cfg, w, soft, src, nb), nullptr,
                                                  nets->step_d, st);
@@ -1606,14 +1678,14 @@ int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_u
   if (int e = launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, &nch)) return e;
   cacto_nets dst = *nets;
   dst.critic_d = nb;
-  return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, nch, soft, st, src);
+  return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, nch, soft, st, src, wait_p, wait_v, sig_p, sig_v);
 }
 
 int actor_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
-                    hipStream_t st) {
+                    hipStream_t st, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
   if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 1, actor_adam_net(sys, nets, cfg, w), nullptr, nets->step_d, st);
   int nch = 0;
-  if (int e = launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, st, &nch)) return e;
+  if (int e = launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, st, &nch, sig_p, sig_v)) return e;
   return launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, w.slab_a, nch, 0, st);
 }
 
@@ -1945,6 +2017,18 @@ int ensure_side_stream(cacto_sys* ms) {
     if (side) (void)hipStreamDestroy(side);
     return hip_fail(e, "cacto_update_n: side stream / events");
   }
+  unsigned long long* sig = nullptr;
+  if (e == hipSuccess) e = hipMalloc(&sig, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(sig, 0, 4 * sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    if (sig) (void)hipFree(sig);
+    for (hipEvent_t x : ev)
+      if (x) (void)hipEventDestroy(x);
+    if (side) (void)hipStreamDestroy(side);
+    return hip_fail(e, "cacto_update_n: pipeline signal");
+  }
+  ms->pipe_sig = sig;
+  ms->pipe_seq = 0;
   ms->ev_critic = ev[0];
   ms->ev_actor[0] = ev[1];
   ms->ev_actor[1] = ev[2];
@@ -1999,11 +2083,31 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
   const bool every2 = every2_env >= 0 ? every2_env == 1 : per != nullptr;
+  // CACTO_PIPE_DEVWAIT=1: the critic stream's ordering against the side stream without queue
+  // markers — the actor's GEMM (the launch after each actor chain) publishes the count of finished
+  // actor chains on the device, and the critic's Adam(t) polls it (pipe_wait) before overwriting the
+  // buffer actor chain(t-3) read; the PER index ring has four buffers, so the sampler of update t
+  // overwrites the one actor chain(t-4) read, which Adam(t-1)'s wait covers. Read once; A/B.
+  static const bool devwait = [] {
+    const char* e = std::getenv("CACTO_PIPE_DEVWAIT");
+    return e && e[0] == '1';
+  }();
+  // ... and the side stream's wait on the critic's Adam too (k_adam's last workgroup publishes, the
+  // actor chain polls just before its critic pass at s' — its actor forward, dynamics and d r / d a
+  // run first), where that cannot starve the critic stream of CUs: 16-sample actor tiles (the q4
+  // chains take no wait), at most one actor workgroup per CU (a CU holding one actor workgroup still
+  // fits a critic chain, GEMM or Adam workgroup beside it, so the critic stream always progresses),
+  // and no PER (the actor chain gathers the sampled rows at its start).
+  const bool devwait_actor = devwait && !per && chain_tile(w.Bp) == CACTO_TILE && w.Bp / CACTO_TILE <= cu_count();
+  unsigned long long* const sig = ms->pipe_sig;
+  const unsigned long long base = ms->pipe_seq;
+  ms->pipe_seq = base + K;  // reserved up front: no later call's waits can be satisfied by this call's values
   for (int t = 0; t < K; ++t) {
     // actor chain(t-3) read the critic buffer Adam(t) writes and (PER) the index buffer of update t.
     // every2: the side stream records only at even iterations and the critic waits at even t for
     // side iteration t-2 (which covers t-3 here and at t+1) — half the queue markers on each stream
-    if (every2) {
+    if (devwait) {
+    } else if (every2) {
       if (t >= 2 && (t & 1) == 0) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[((t - 2) >> 1) & 1], 0));
     } else if (t >= 3) {
       CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t % 3], 0));
@@ -2011,7 +2115,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     const int32_t* idx = idx_d + (size_t)t * B;
     const float* isw = nullptr;
     if (per) {
-      int32_t* pi = w.pidx + (size_t)(t % 3) * w.Bp;
+      int32_t* pi = w.pidx + (size_t)(t % (devwait ? 4 : 3)) * w.Bp;
       if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
                                    per->uniforms + (size_t)t * B, B, pi, w.pisw, late_count ? nullptr : per->exp_counter, st))
         return e;
@@ -2022,22 +2126,38 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     cur.critic_d = buf[t % 3];
     nxt.critic_d = buf[(t + 1) % 3];
     if (int e = launch_critic_chain(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
-    if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d)) return e;
+    const bool dw = devwait && t >= 3;
+    if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d, dw ? sig : nullptr, base + t - 2,
+                                 devwait_actor ? sig : nullptr, base + t + 1))
+      return e;
     *cbuf = (t + 1) % 3;
-    CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+    if (!devwait_actor) CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
     if (per)
       if (int e = per_priority_update(per, idx, y, V, B, late_count, st)) return e;
-    CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
-    if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
-    if (int e = actor_step_tail(sys, nets, cfg, w, side)) return e;
-    if (!every2)
+    if (!devwait_actor) CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+    if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side, devwait_actor ? sig + 2 : nullptr,
+                                   base + t + 1))
+      return e;
+    if (int e = actor_step_tail(sys, nets, cfg, w, side, devwait ? sig : nullptr, base + t + 1)) return e;
+    if (devwait) {
+    } else if (!every2) {
       CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t % 3], side));
-    else if ((t & 1) == 0)
+    } else if ((t & 1) == 0) {
       CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[(t >> 1) & 1], side));
+    }
   }
   return CACTO_OK;
 }
 }  // namespace
+
+extern "C" int cacto_pipeline_status(const cacto_sys* sys, unsigned long long* out4_h) {
+  CACTO_REQUIRE(sys && out4_h, "cacto_pipeline_status: bad arguments");
+  for (int k = 0; k < 4; ++k) out4_h[k] = 0;
+  if (!sys->pipe_sig) return CACTO_OK;
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpy(out4_h, sys->pipe_sig, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return CACTO_OK;
+}
 
 extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                               const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,

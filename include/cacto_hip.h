@@ -234,6 +234,11 @@ int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_updat
                  float* y_d, float* V_d, float* Vt_d, void* workspace_d, size_t workspace_bytes,
                  void* stream);
 
+/* Diagnostic: the two-stream pipeline's device-side ordering words (CACTO_PIPE_DEVWAIT=1): out4_h[0]
+ * actor chains finished, [1] 1 if a device-side wait ever timed out (an ordering bug; the waits are
+ * bounded so that it cannot hang the GPU), [2] critic Adam steps finished, [3] 0. Synchronizes the
+ * device. All zero before the first pipelined call. */
+int cacto_pipeline_status(const cacto_sys* sys, unsigned long long* out4_h);
 /* K consecutive updates on minibatch indices idx_d [K][B] (learn_and_update's loop with its
  * minibatches drawn up front, RL.py:120-143; no IS weights). Bit-identical to K cacto_update calls.
  * The critic step of update t+1 overlaps the actor step of update t (the critic step never reads

@@ -4,10 +4,13 @@ build-time-free schedule knob the pipeline reads once per process — so each co
 its own child process:
   * CACTO_PIPE_EVERY2 = 0 / 1: cross-stream markers every iteration / every other iteration (the
     default with PER), with the three-buffer critic rotation and the pidx[t % 3] ring;
+  * CACTO_PIPE_DEVWAIT = 1: that ordering on the device (the actor's GEMM publishes finished
+    chains, the critic's Adam polls) instead of queue markers, with a four-buffer PER index ring;
   * CACTO_PER_FUSED = 0 / 1: the priority update (with the sampler's deferred exp_counter += 1) as
     the one-launch subtree kernel k_per_update_sub, or the round-3 chain k_per_count ->
     k_per_leaves_mw -> k_per_subtrees -> k_per_top.
-K = 6 and 7 (even / odd: the critic ends in the caller's buffer or a workspace copy). Every child
+K = 6 and 7 (even / odd: the critic ends in the caller's buffer or a workspace copy), and the
+non-PER loop (DI, B = 1024, K = 7) against sequential updates under the same knobs. Every child
 also writes the trees after a priority update with an unsorted index list holding duplicates
 (B = 1024, the fused kernel's filter path), and all children must agree on every byte.
 replay_buffer.py:139-218, RL.py:120-143."""
@@ -69,6 +72,36 @@ def _child():
         a, b = state(seq, sbuf), state(pipe, pbuf)
         out["K%d_equal" % K] = all(np.array_equal(x, z) for x, z in zip(a, b))
         out["K%d_hash" % K] = hashlib.sha256(b"".join(x.tobytes() for x in b)).hexdigest()
+    # the non-PER two-stream loop (DI, B = 1024) under the same knobs
+    dconf = load_conf("double_integrator", fresh=True)
+    denv = make_env(dconf)
+    dS = np.column_stack([rng.uniform(-3, 3, (N, 4)), rng.uniform(0, 4.9, N)])
+    drows = np.concatenate([dS, rng.normal(size=(N, 1)), dS + 0.01, rng.normal(size=(N, 5)) * 0.3,
+                            (rng.uniform(size=(N, 1)) < 0.1).astype(float), np.zeros((N, 1))], axis=1)
+    storage = torch.as_tensor(drows, device="cuda")
+    didx = torch.as_tensor(rng.integers(0, N, size=(7, 1024)).astype(np.int32), device="cuda")
+    runs = []
+    for pipelined in (False, True):
+        rl = RL_AC(denv, NN(denv, dconf, w_S=1e-2, seed=3), dconf)
+        rl.setup_model()
+        if pipelined:
+            rl.update_rows_n(storage, didx)
+        else:
+            for k in range(7):
+                rl.update_rows(storage, didx[k])
+        torch.cuda.synchronize()
+        runs.append([t.cpu().numpy() for t in (rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf,
+                                               rl.actor_m, rl.critic_v, rl.steps)])
+    out["di_equal"] = all(np.array_equal(x, z) for x, z in zip(*runs))
+    # no device-side wait of the pipeline ever timed out (cacto_pipeline_status word 1)
+    import ctypes
+    from cacto_amd import _lib as L
+    latch = 0
+    for sysobj in (env.sys, denv.sys, rl.sys):
+        st = (ctypes.c_ulonglong * 4)()
+        L.lib().call("cacto_pipeline_status", sysobj.handle, st)
+        latch |= int(st[1])
+    out["latch"] = latch
     # an unsorted index list with duplicates through the public priority update
     _, buf = setup()
     idx = torch.as_tensor(np.random.default_rng(7).integers(0, 600, size=1024).astype(np.int32), device="cuda")
@@ -87,16 +120,15 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = {}
-    for every2 in ("0", "1"):
-        for fused in ("1", "0"):
-            env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused)
-            r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
-                               timeout=300)
-            assert r.returncode == 0, r.stderr[-3000:]
-            line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
-            res[(every2, fused)] = json.loads(line[len("RESULT "):])
+    for every2, fused, devwait in (("0", "1", "0"), ("1", "1", "0"), ("1", "0", "0"), ("0", "1", "1")):
+        env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait)
+        r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+        res[(every2, fused, devwait)] = json.loads(line[len("RESULT "):])
     for key, r in res.items():
-        assert r["K6_equal"] and r["K7_equal"], key
+        assert r["K6_equal"] and r["K7_equal"] and r["di_equal"] and r["latch"] == 0, key
     for field in ("K6_hash", "K7_hash", "unsorted_hash"):
         assert len({r[field] for r in res.values()}) == 1, field
 
