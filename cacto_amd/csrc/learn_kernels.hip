@@ -681,6 +681,102 @@ constexpr int WG_BLK = 4;
 #define WG_PF 1
 #endif
 
+// One workgroup's block of NI x NO output tiles (of a layer) over the rows [lo, hi) of one chunk:
+// the 4 waves split the rows, each keeping NI x NO accumulator tiles, then reduce through LDS in a
+// fixed order ((p0 + p1) + p2) + p3 (deterministic), in rounds of 8 tiles. ni, no: the tiles that
+// exist (<= NI, NO; the generic 4 x 4 instance runs edge blocks on clamped duplicate tiles).
+template <int NI, int NO>
+__device__ __forceinline__ void wg_block(const WgArgs& a, const WgLayer& Ly, int lo, int hi, int it0, int ot0, int ni,
+                                         int no, float* __restrict__ out, float4* part) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int span = ((hi - lo) / 16 + 3) / 4 * 16;  // rows per wave, multiple of 16
+  const int r0 = lo + wave * span, r1 = min(hi, r0 + span);
+  floatx4 acc[NI][NO];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int o = 0; o < NO; ++o) acc[i][o] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float* ap = Ly.LT + (size_t)(16 * it0 + c) * a.ld + 4 * g;
+  const float* bp = Ly.RT + (size_t)(16 * ot0 + c) * a.ld + 4 * g;
+  // panel slices of the next WG_PF 16-row steps are in flight while a step's MFMAs run; the steps
+  // are summed in row order whatever the depth
+  float4 As[WG_PF][NI], Bs[WG_PF][NO];
+  auto fetch = [&](float4 (&An)[NI], float4 (&Bn)[NO], int r) {
+    const int rr = min(r, r1 - 16);  // clamped (branch-free); a past-the-end fetch is unused
+#pragma unroll
+    for (int i = 0; i < NI; ++i) An[i] = *reinterpret_cast<const float4*>(ap + (size_t)16 * min(i, ni - 1) * a.ld + rr);
+#pragma unroll
+    for (int o = 0; o < NO; ++o) Bn[o] = *reinterpret_cast<const float4*>(bp + (size_t)16 * min(o, no - 1) * a.ld + rr);
+  };
+  auto step = [&](const float4 (&A)[NI], const float4 (&Bv)[NO]) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int o = 0; o < NO; ++o) acc[i][o] = mfma4(A[i].x, Bv[o].x, acc[i][o]);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int o = 0; o < NO; ++o) acc[i][o] = mfma4(A[i].y, Bv[o].y, acc[i][o]);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int o = 0; o < NO; ++o) acc[i][o] = mfma4(A[i].z, Bv[o].z, acc[i][o]);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int o = 0; o < NO; ++o) acc[i][o] = mfma4(A[i].w, Bv[o].w, acc[i][o]);
+  };
+  if (r0 < r1) {
+#pragma unroll
+    for (int d = 0; d < WG_PF; ++d) fetch(As[d], Bs[d], r0 + 16 * d);
+  }
+  for (int r = r0; r < r1; r += 16 * WG_PF) {
+#pragma unroll
+    for (int d = 0; d < WG_PF; ++d) {
+      if (r + 16 * d < r1) {
+        float4 A[NI], Bv[NO];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) A[i] = As[d][i];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) Bv[o] = Bs[d][o];
+        fetch(As[d], Bs[d], r + 16 * (d + WG_PF));
+        step(A, Bv);
+      }
+    }
+  }
+  constexpr int NT = NI * NO, HT = NT < 8 ? NT : 8;  // tiles, tiles per round
+  constexpr int NR = (NT + HT - 1) / HT;
+#pragma unroll
+  for (int h = 0; h < NR; ++h) {
+    if (h) __syncthreads();  // the previous round's partials are consumed
+#pragma unroll
+    for (int t = h * HT; t < h * HT + HT && t < NT; ++t) part[(wave * HT + (t - h * HT)) * 64 + lane] = f4(acc[t / NO][t % NO]);
+    __syncthreads();
+    // wave w finishes the round's tiles 2w, 2w + 1: ((p0 + p1) + p2) + p3
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int tl = wave * 2 + k, t = h * HT + tl, i = t / NO, o = t % NO;
+      if (tl >= HT || t >= NT || i >= ni || o >= no) continue;
+      float4 s4 = part[(0 * HT + tl) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float4 q = part[(w * HT + tl) * 64 + lane];
+        s4.x += q.x;
+        s4.y += q.y;
+        s4.z += q.z;
+        s4.w += q.w;
+      }
+      const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+      const int oc = 16 * (ot0 + o) + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ii = 16 * (it0 + i) + 4 * g + q;
+        if (ii < Ly.in && oc < Ly.out) out[Ly.woff + ii * Ly.out + oc] = sv[q];
+      }
+    }
+  }
+}
+
 //
 // xcd = 1: the items of one chunk run on blocks that share an XCD (blocks b and b + 8 are dealt to
 // one; observed dealing, so it decides only which L2 serves a re-read): chunk (b / 8 / tpc) * 8 +
@@ -690,7 +786,7 @@ constexpr int WG_BLK = 4;
 // sig_p (the pipeline's device-side ordering): this launch follows the actor chain of an iteration
 // on its stream, so that chain has finished; block 0 publishes sig_v = (iterations done) for the
 // critic stream's Adam, which must not overwrite a critic buffer the chain read (k_adam's wait_p).
-__global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ slab, int xcd,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wgrad(WgArgs a, float* __restrict__ slab, int xcd,
                                                unsigned long long* sig_p, unsigned long long sig_v) {
   // 32 KiB: the 16 tiles are reduced in two rounds of 8, so a GEMM workgroup fits on a CU beside
   // a chain workgroup — the pipelined update runs the two concurrently
@@ -718,96 +814,13 @@ __global__ void __launch_bounds__(256) k_wgrad(WgArgs a, float* __restrict__ sla
   if (rem < nbi * nbo) {
     const int it0 = (rem / nbo) * WG_BLK, ot0 = (rem % nbo) * WG_BLK;
     const int ni = min(WG_BLK, Ly.IT - it0), no = min(WG_BLK, Ly.OT - ot0);
-    const int span = ((hi - lo) / 16 + 3) / 4 * 16;  // rows per wave, multiple of 16
-    const int r0 = lo + wave * span, r1 = min(hi, r0 + span);
-    floatx4 acc[WG_BLK][WG_BLK];
-#pragma unroll
-    for (int i = 0; i < WG_BLK; ++i)
-#pragma unroll
-      for (int o = 0; o < WG_BLK; ++o) acc[i][o] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* ap = Ly.LT + (size_t)(16 * it0 + c) * a.ld + 4 * g;
-    const float* bp = Ly.RT + (size_t)(16 * ot0 + c) * a.ld + 4 * g;
-    // panel slices of the next WG_PF 16-row steps are in flight while a step's 64 MFMAs run; the
-    // steps are summed in row order whatever the depth
-    float4 As[WG_PF][WG_BLK], Bs[WG_PF][WG_BLK];
-    auto fetch = [&](float4 (&An)[WG_BLK], float4 (&Bn)[WG_BLK], int r) {
-      const int rr = min(r, r1 - 16);  // clamped (branch-free); a past-the-end fetch is unused
-#pragma unroll
-      for (int i = 0; i < WG_BLK; ++i)
-        An[i] = *reinterpret_cast<const float4*>(ap + (size_t)16 * min(i, ni - 1) * a.ld + rr);
-#pragma unroll
-      for (int o = 0; o < WG_BLK; ++o)
-        Bn[o] = *reinterpret_cast<const float4*>(bp + (size_t)16 * min(o, no - 1) * a.ld + rr);
-    };
-    auto step = [&](const float4 (&A)[WG_BLK], const float4 (&Bv)[WG_BLK]) {
-#pragma unroll
-      for (int i = 0; i < WG_BLK; ++i)
-#pragma unroll
-        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].x, Bv[o].x, acc[i][o]);
-#pragma unroll
-      for (int i = 0; i < WG_BLK; ++i)
-#pragma unroll
-        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].y, Bv[o].y, acc[i][o]);
-#pragma unroll
-      for (int i = 0; i < WG_BLK; ++i)
-#pragma unroll
-        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].z, Bv[o].z, acc[i][o]);
-#pragma unroll
-      for (int i = 0; i < WG_BLK; ++i)
-#pragma unroll
-        for (int o = 0; o < WG_BLK; ++o) acc[i][o] = mfma4(A[i].w, Bv[o].w, acc[i][o]);
-    };
-    if (r0 < r1) {
-#pragma unroll
-      for (int d = 0; d < WG_PF; ++d) fetch(As[d], Bs[d], r0 + 16 * d);
-    }
-    for (int r = r0; r < r1; r += 16 * WG_PF) {
-#pragma unroll
-      for (int d = 0; d < WG_PF; ++d) {
-        if (r + 16 * d < r1) {
-          float4 A[WG_BLK], Bv[WG_BLK];
-#pragma unroll
-          for (int i = 0; i < WG_BLK; ++i) {
-            A[i] = As[d][i];
-            Bv[i] = Bs[d][i];
-          }
-          fetch(As[d], Bs[d], r + 16 * (d + WG_PF));
-          step(A, Bv);
-        }
-      }
-    }
-    constexpr int HT = WG_BLK * WG_BLK / 2;  // tiles per round
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h) __syncthreads();  // round 0's partials are consumed
-#pragma unroll
-      for (int i = 2 * h; i < 2 * h + 2; ++i)
-#pragma unroll
-        for (int o = 0; o < WG_BLK; ++o) part[(wave * HT + (i - 2 * h) * WG_BLK + o) * 64 + lane] = f4(acc[i][o]);
-      __syncthreads();
-      // wave w finishes tiles t = 8h + 2w, 8h + 2w + 1: ((p0 + p1) + p2) + p3, as in one round
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int tl = wave * 2 + k, t = h * HT + tl, i = t / WG_BLK, o = t % WG_BLK;
-        if (i >= ni || o >= no) continue;
-        float4 s4 = part[(0 * HT + tl) * 64 + lane];
-#pragma unroll
-        for (int w = 1; w < 4; ++w) {
-          const float4 q = part[(w * HT + tl) * 64 + lane];
-          s4.x += q.x;
-          s4.y += q.y;
-          s4.z += q.z;
-          s4.w += q.w;
-        }
-        const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
-        const int oc = 16 * (ot0 + o) + c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int ii = 16 * (it0 + i) + 4 * g + q;
-          if (ii < Ly.in && oc < Ly.out) out[Ly.woff + ii * Ly.out + oc] = sv[q];
-        }
-      }
-    }
+    // the block shapes the networks have, compiled for their size (an edge block of the input or
+    // output layer loads and multiplies only its own tiles); any other shape runs the 4 x 4 code
+    // on clamped duplicate tiles (unused)
+    if (ni == WG_BLK && no == WG_BLK) wg_block<WG_BLK, WG_BLK>(a, Ly, lo, hi, it0, ot0, ni, no, out, part);
+    else if (ni == 1 && no == WG_BLK) wg_block<1, WG_BLK>(a, Ly, lo, hi, it0, ot0, ni, no, out, part);
+    else if (ni == WG_BLK && no == 1) wg_block<WG_BLK, 1>(a, Ly, lo, hi, it0, ot0, ni, no, out, part);
+    else wg_block<WG_BLK, WG_BLK>(a, Ly, lo, hi, it0, ot0, ni, no, out, part);
   } else {
     const int ot = (rem - nbi * nbo) * WG_BLK + wave;
     if (ot >= Ly.OT) return;
