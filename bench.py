@@ -856,20 +856,24 @@ def main():
     roll_bytes = (roll["steps_per_call"] * (8 * ns + 4 * na + 8 + 24) + n_ep * (8 * ns + 24 + 8 * ns + 4)
                   + 4 * rl.actor_model.P)
     upd_roof = None
+    upd_roofs = {}
     if updates:
-        # the update at the first batch (the reference's B = 128): SURVEY §8(d) algorithmic FLOP and
-        # bytes per update, against the measured rate and the PMC counter bytes of its kernels
-        Bu = [int(b) for b in args.batches.split(",") if b][0]
-        u = updates["B=%d" % Bu]
+        # per batch: SURVEY §8(d) algorithmic FLOP and bytes per update, against the measured rate and
+        # the PMC counter bytes of its kernels; `update` (in the roofline object) is the first batch's
+        # (the reference's B = 128)
         PA, PC = rl.actor_model.P, rl.critic_model.P
-        fl = Bu * world * (9 * fc_flops(ns) + 3 * fa_flops(ns, na)) + 12 * (PA + PC) + 3 * PC
-        by = Bu * world * ((3 * ns + 3) * 4 + 8) + 36 * (PA + PC) + 12 * PC
-        ctr, per, src = pmc_update_traffic(Bu)
-        upd_roof = {"batch": Bu, "flop_per_update": fl, "algorithmic_bytes_per_update": by,
-                    "ms_per_update": u["ms_per_update"], "achieved_tflops": fl / (u["ms_per_update"] * 1e-3) / 1e12,
-                    "mfma_frac": fl / (u["ms_per_update"] * 1e-3) / (FP32_MFMA_PEAK * world),
-                    "counter_bytes_per_update": ctr, "counter_bytes_by_kernel": per,
-                    "counter_over_algorithmic": (ctr / by) if ctr else None, "traffic_source": src}
+        for Bu in [int(b) for b in args.batches.split(",") if b]:
+            u = updates["B=%d" % Bu]
+            fl = Bu * world * (9 * fc_flops(ns) + 3 * fa_flops(ns, na)) + 12 * (PA + PC) + 3 * PC
+            by = Bu * world * ((3 * ns + 3) * 4 + 8) + 36 * (PA + PC) + 12 * PC
+            ctr, per, src = pmc_update_traffic(Bu)
+            upd_roofs[Bu] = {"batch": Bu, "flop_per_update": fl, "algorithmic_bytes_per_update": by,
+                             "ms_per_update": u["ms_per_update"],
+                             "achieved_tflops": fl / (u["ms_per_update"] * 1e-3) / 1e12,
+                             "mfma_frac": fl / (u["ms_per_update"] * 1e-3) / (FP32_MFMA_PEAK * world),
+                             "counter_bytes_per_update": ctr, "counter_bytes_by_kernel": per,
+                             "counter_over_algorithmic": (ctr / by) if ctr else None, "traffic_source": src}
+        upd_roof = upd_roofs[[int(b) for b in args.batches.split(",") if b][0]]
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -907,7 +911,8 @@ def main():
                          "batch_traffic": (traffic + rw_traffic) if traffic and rw_traffic else None,
                          "batch_traffic_over_algorithmic": ((traffic + rw_traffic) / roll_bytes
                                                             if traffic and rw_traffic else None),
-                         "update": upd_roof},
+                         "update": upd_roof,
+                         "update_by_batch": {str(k): v for k, v in upd_roofs.items()}},
             "critic_updates": updates,
             "episode_to_buffer": e2b,
             "ddp_labels": ddp,
@@ -917,6 +922,9 @@ def main():
             "config0": c0,
         }
         line.update(flat_summary(updates, upd_roof, extra, world))
+        for Bu, r in upd_roofs.items():     # flat per-batch copies (a record that keeps only scalars)
+            line["di_update_counter_over_algorithmic_b%d" % Bu] = r["counter_over_algorithmic"]
+            line["di_update_counter_bytes_b%d" % Bu] = r["counter_bytes_per_update"]
         print(json.dumps(line))
     if world > 1:
         import torch.distributed as dist
