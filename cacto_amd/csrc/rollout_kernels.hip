@@ -1355,6 +1355,262 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
 #undef KMARK
 }
 
+// ---------------------------------------------------------------- actor waves beside dynamics waves
+// k_rollout_sw (revolute chains with 3 joints: the manipulator). The per-step float64 dynamics of a
+// chain whose M depends on q (RNEA, CRBA, Cholesky: ~9 k cycles of dependent f64 work, one lane per
+// slot) left the matrix cores idle for 40 % of k_rollout's step. Here an 8-wave workgroup gives the
+// two kinds of work their own waves — waves 0-3 run the actor (layer-2 rows 64 w + lane of W2 in
+// their registers, the rest in LDS), waves 4-7 the dynamics (RNEA on wave 4, the CRBA columns on
+// waves 5-7, as k_rollout's waves 0-3) — so every SIMD holds one wave of each and issues MFMAs for one
+// while the other waits on f64 latency. The 16 episode slots form two halves of two groups; in
+// half-step k the actor waves run the actor of half X = k & 1 while the dynamics waves step half
+// Y = 1 - X with the actions the actor produced for it in half-step k - 1: each half advances one
+// env step every two half-steps. Each role synchronises with a team barrier (an LDS arrival counter),
+// the two roles meet at one workgroup barrier per half-step. Every per-slot value is formed by the
+// functions k_rollout<3, 4> uses, in the same order (ro_actor / ro_layer2 without SPLIT, ro_chain_nle,
+// ro_chain_mass_cols, chain_step, ro_advance, ro_refill), so results are bit-identical to it.
+template <int NJ>
+struct RoSwCfg {
+  static constexpr int NG = 4, SL = 16, NH = 2, SH = 8;  // groups and slots; per half
+  // layer-2 rows: [0, REGK) in the actor waves' registers, [REGK, REGK + LDSK) in LDS, the rest
+  // streamed from L2 at every actor pass (the dynamics, not the actor, bound the half-step)
+#ifdef RO_SW_REGK
+  static constexpr int REGK = RO_SW_REGK;
+#else
+  static constexpr int REGK = 160;  // 176 / 80 and 192 / 64 measured no fewer spills (16 B, the dynamics role)
+#endif
+#ifdef RO_SW_LDSK
+  static constexpr int LDSK = RO_SW_LDSK;
+#else
+  static constexpr int LDSK = 96;
+#endif
+  static_assert(REGK % 16 == 0 && LDSK % 16 == 0 && REGK + LDSK <= 256, "row split");
+};
+
+template <int NJ>
+struct RoSwShared {
+  static constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA, SL = RoSwCfg<NJ>::SL, SH = RoSwCfg<NJ>::SH;
+  using H = RoCfg<RoSwCfg<NJ>::NH>;  // per-half actor layout (8 slots)
+  struct {
+    float4 w2[RoSwCfg<NJ>::LDSK / 4 * 4 * 64];  // W2[REGK + 4kq + j][64w + lane] at (kq*4 + w)*64 + lane
+    float w3[na * 256];
+    float b3[8];
+    float h1[2 * RoSwCfg<NJ>::NH * 4 * H::H1B];  // per half: its groups' layer-1 output
+    float h2[2 * SH * H::H2S];
+    float x0[2 * RoSwCfg<NJ>::NH * 64];  // slot c at (c >> 2) * 64 + 4q + (c & 3): ro_refill's layout
+    float a[2 * SH * na];
+  } W;
+  double sS[SL * ns];
+  double MS[SL * NJ * NJ], hS[SL * NJ];
+  RoChain<NJ, SL> ch;
+  int sb[SL], sn[SL], st[SL], sact[SL];
+  int any[2][2];  // [half-step parity][half]: a slot of the half is active
+  int bar_a, bar_d;
+};
+
+#ifdef CACTO_STAMPS
+__device__ unsigned long long g_swacc[1024 * 2 * 6];  // k_rollout_sw: [workgroup][role][phase 0-4, half-steps]
+#endif
+
+template <int NJ>
+__global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
+    k_rollout_sw(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
+                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
+                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
+  using Cf = RoSwCfg<NJ>;
+  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA, SL = Cf::SL, SH = Cf::SH, NH = Cf::NH;
+  constexpr int REGK = Cf::REGK, LDSK = Cf::LDSK;
+  using H = RoCfg<NH>;
+  __shared__ RoSwShared<NJ> Sh;
+  const SysDevice& sd = *sdp;
+  const cacto_sys_params& p = sd.p;
+  const bool dyn = threadIdx.x >= 4 * CACTO_WAVE;  // role, uniform per wave
+  Lane L;  // team-local: tid 0..255, wave 0..3 within the role
+  L.tid = threadIdx.x & 255;
+  L.wave = L.tid >> 6;
+  if (dyn && use_actor) {
+    const float* W2 = N.flat + N.t.woff[1];
+    const float* W3 = N.flat + N.t.woff[2];
+    for (int e = L.tid; e < LDSK * 64; e += CACTO_THREADS) {
+      const int lane = e & 63, w = (e >> 6) & 3, kq = e >> 8;
+      const int k = REGK + 4 * kq, col = 64 * w + lane;
+      Sh.W.w2[e] = make_float4(W2[k * 256 + col], W2[(k + 1) * 256 + col], W2[(k + 2) * 256 + col],
+                               W2[(k + 3) * 256 + col]);
+    }
+    for (int e = L.tid; e < na * 256; e += CACTO_THREADS) Sh.W.w3[e] = W3[(e & 255) * na + (e >> 8)];
+    if (L.tid < 8) Sh.W.b3[L.tid] = L.tid < na ? N.bias(2, L.tid) : 0.f;
+  }
+  for (int e = threadIdx.x; e < 2 * NH * 64; e += 8 * CACTO_WAVE) Sh.W.x0[e] = 0.f;
+  for (int e = threadIdx.x; e < SL * ns; e += 8 * CACTO_WAVE) Sh.sS[e] = 0.0;
+  if (threadIdx.x < SL) Sh.sact[threadIdx.x] = 0;
+  if (threadIdx.x == 0) Sh.bar_a = Sh.bar_d = 0;
+  __syncthreads();
+  const int G = gridDim.x, vb = (int)blockIdx.x;
+  int head = 0;  // queue position (dynamics wave 0, uniform)
+  const RoNorm<ns> nrm(p);
+  const bool d0 = dyn && L.wave == 0;
+  const int c = L.lane % SL;  // dynamics wave 0: lane c <-> slot c
+  RoSlotRegs<NJ, RoSwCfg<NJ>::NG> sr;
+  if (d0) {
+    ro_refill<NJ, RoSwCfg<NJ>::NG>(L.lane < SL, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L, vb);
+    const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
+    if (L.lane == 0) {
+      Sh.any[0][0] = (m & 0xffull) != 0;
+      Sh.any[0][1] = (m & 0xff00ull) != 0;
+    }
+    sr.load(Sh, c, false);
+  }
+  __syncthreads();
+  RoTeamBar abar{&Sh.bar_a, 0, L.lane}, dbar{&Sh.bar_d, 0, L.lane};
+  const float* W2g = N.flat + N.t.woff[1];
+  // per-phase cycles (CACTO_STAMPS): actor role [0] actor, [1] end barrier; dynamics role [0]
+  // placements + team barrier, [1] RNEA / CRBA + team barrier, [2] step, stores, refill, next input,
+  // [3] end barrier; [5] half-steps
+#ifdef CACTO_STAMPS
+  unsigned long long wacc[5] = {0, 0, 0, 0, 0}, wprev = __builtin_amdgcn_s_memtime();
+  int wsteps = 0;
+  auto wmark = [&](int ph) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (k == ph) wacc[k] += now - wprev;
+    wprev = now;
+  };
+#define SWMARK(k) wmark(k)
+#else
+#define SWMARK(k) \
+  do {            \
+  } while (0)
+#endif
+  // The two roles run separate loops (so the actor's register-resident weights are not live across
+  // the dynamics code); both leave at the same half-step (the flags they read are the same) and meet
+  // at the one workgroup barrier of every half-step.
+  if (!dyn) {
+    RoActorRegs<ns, REGK> R;
+    if (use_actor) {
+      const float* W1 = N.flat + N.t.woff[0];
+      const float* W2 = N.flat + N.t.woff[1];
+      const int f = 64 * L.wave + L.lane;
+#pragma unroll
+      for (int k = 0; k < REGK; ++k) R.w2[k] = W2[k * 256 + f];
+#pragma unroll
+      for (int q = 0; q < ns; ++q) R.w1[q] = W1[q * 256 + f];
+      R.b1 = N.bias(0, f);
+      R.b2 = N.bias(1, f);
+    }
+    for (int it = 0;; ++it) {
+      const int par = it & 1, X = par, Y = 1 - par;
+      const bool anyX = Sh.any[par][X] != 0, anyY = Sh.any[par][Y] != 0;
+      if (!anyX && !anyY) break;
+      if (anyX && use_actor) {
+        RoTeamView<na> V{Sh.W.w2, Sh.W.w3, Sh.W.b3, Sh.W.h1 + X * NH * 4 * H::H1B, Sh.W.h2 + X * SH * H::H2S,
+                         Sh.W.x0 + X * NH * 64, Sh.W.a + X * SH * na};
+        ro_actor<NH, ns, na, REGK, LDSK, false, false>(R, V, W2g, L, it, abar);
+      }
+      SWMARK(0);
+      __syncthreads();
+      SWMARK(1);
+#ifdef CACTO_STAMPS
+      ++wsteps;
+#endif
+    }
+  } else {
+    for (int it = 0;; ++it) {
+      const int par = it & 1, Y = 1 - par;
+      const bool anyX = Sh.any[par][par] != 0, anyY = Sh.any[par][Y] != 0;
+      if (!anyX && !anyY) break;
+      // the dynamics of half Y, from the actions its actor pass wrote in half-step it - 1
+      const bool run = anyY && it > 0;
+      if (run) {
+        const int lc = L.tid;  // placements: item (slot Y*8 + lc % 8, joint lc / 8)
+        if (lc < SH * NJ) {
+          const int cc = Y * SH + lc % SH, i = lc / SH;
+          if (Sh.sact[cc])
+            se3_st<SL>(Sh.ch.X + i * 12 * SL + cc,
+                       joint_placement(JointView{sd.joints + i * CACTO_JOINT_COLS}, Sh.sS[cc * ns + i]));
+        }
+        dbar();
+      }
+      SWMARK(0);
+      const int cy = Y * SH + (L.lane & (SH - 1));  // this lane's slot of half Y
+      const bool act_y = run && L.lane < SH && Sh.sact[cy] != 0;
+      if (run) {
+        if (L.wave == 0) {
+          if (act_y) ro_chain_nle<NJ, SL>(sd, Sh.ch, cy, Sh.sS + cy * ns, Sh.sS + cy * ns + NJ, Sh.hS + cy);
+        } else if (act_y) {
+          ro_chain_mass_cols<NJ, SL>(sd, Sh.ch, cy, Sh.MS + cy, RoMassCols<NJ>::lo(L.wave), RoMassCols<NJ>::hi(L.wave));
+        }
+        dbar();
+      }
+      SWMARK(1);
+      if (d0) {
+        // lane c holds slot c's registers; the lanes of half Y step their slots
+        const bool mine = run && L.lane < SL && (c / SH) == Y;
+        const bool active = mine && sr.act;
+        bool fin = false;
+        float a[na];
+        if (active) {
+          double ad[na], sn[ns], M[NJ * NJ], h[NJ];
+#pragma unroll
+          for (int i = 0; i < na; ++i) {
+            a[i] = use_actor ? Sh.W.a[(Y * SH + (c - Y * SH)) * na + i] : 0.f;
+            ad[i] = (double)a[i];
+          }
+#pragma unroll
+          for (int k = 0; k < NJ * NJ; ++k) M[k] = Sh.MS[k * SL + c];
+#pragma unroll
+          for (int i = 0; i < NJ; ++i) h[i] = Sh.hS[i * SL + c];
+          chain_step<NJ>(sd, sr.s, ad, M, h, sn);
+#pragma unroll
+          for (int i = 0; i < ns; ++i) {
+            Sh.sS[c * ns + i] = sn[i];
+            sr.s[i] = sn[i];
+          }
+        }
+        if (run) {
+          // the next actor input of half Y's slots from s_{t+1} (one (slot, feature) item per lane);
+          // a slot refilled below gets its s_0 row from ro_refill afterwards (later in program order)
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          if (L.lane < SH * ns) {
+            const int cc = Y * SH + L.lane % SH, f = L.lane / SH;
+            float nf = 1.f;
+#pragma unroll
+            for (int q = 0; q < ns; ++q) nf = f == q ? nrm.n[q] : nf;
+            const float q = fdiv((float)Sh.sS[cc * ns + f], nf);
+            const float v = f == ns - 1 ? fsub(fmul(q, 2.0f), 1.0f) : q;
+            Sh.W.x0[(cc >> 2) * 64 + 4 * f + (cc & 3)] = nrm.on ? v : (float)Sh.sS[cc * ns + f];
+          }
+        }
+        if (active) {
+          fin = ro_advance<NJ, RoSwCfg<NJ>::NG>(c, sr.b, sr.t, sr.s, a, sd, T, Straj, Atraj, status, nrm, sr.n);
+          sr.t += 1;
+        }
+        ro_refill<NJ, RoSwCfg<NJ>::NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L, vb);
+        if (fin) sr.load(Sh, c, false);
+        const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
+        if (L.lane == 0) {
+          Sh.any[1 - par][0] = (m & 0xffull) != 0;
+          Sh.any[1 - par][1] = (m & 0xff00ull) != 0;
+        }
+      }
+      SWMARK(2);
+      __syncthreads();
+      SWMARK(3);
+#ifdef CACTO_STAMPS
+      ++wsteps;
+#endif
+    }
+  }
+#ifdef CACTO_STAMPS
+  if (L.lane == 0 && L.wave == 0) {
+    unsigned long long* o = g_swacc + ((size_t)blockIdx.x * 2 + (dyn ? 1 : 0)) * 6;
+    for (int k = 0; k < 5; ++k) o[k] = wacc[k];
+    o[5] = wsteps;
+  }
+#endif
+#undef SWMARK
+}
+
 // Rewards and end-effector positions of every recorded step (Env.step's reward and
 // get_end_effector_position, environment.py:70-78, :146-156): one thread per (episode, t),
 // r_t = reward(w, s_t, a_t) for t < n, EE_t = EE(s_t) for t <= n; NaN states (a dropped episode)
@@ -1574,6 +1830,27 @@ struct LaunchRollout {
       if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
       return CACTO_OK;
     }
+    // 3-joint revolute chains (the manipulator): actor waves beside dynamics waves (k_rollout_sw),
+    // on request (groups == -4) or automatically with CACTO_RO_SW=1 (A/B; bit-identical to k_rollout<3, 4>)
+    static const bool sw_env = [] {
+      const char* e = std::getenv("CACTO_RO_SW");
+      return e && e[0] == '1';
+    }();
+    if constexpr (NJ == 3) {
+      if (groups == -4 || (groups == 0 && sw_env && !sys->host.p.const_dyn)) {
+        if (wgs <= 0) wgs = std::min(cus, ceil_div(B, RoSwCfg<NJ>::SL));
+        wgs = std::max(1, std::min(wgs, ceil_div(B, RoSwCfg<NJ>::SL)));
+        hipLaunchKernelGGL(k_rollout_sw<NJ>, dim3(wgs), dim3(8 * CACTO_WAVE), 0, st, sys->dev, v, S0, n, T, use_actor,
+                           S, A, status, order, B);
+        CACTO_CHECK_HIP(hipGetLastError());
+        if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
+        return CACTO_OK;
+      }
+    }
+    if (groups == -4) {
+      set_error("cacto_rollout_sched: groups -4 (actor waves beside dynamics waves) needs a 3-joint revolute chain");
+      return CACTO_EINVAL;
+    }
     // the float64 6-joint chain dynamics need the registers that more slots would take
     constexpr int gmax = 4;
     if (groups <= 0) {
@@ -1624,6 +1901,12 @@ extern "C" int cacto_debug_rollout_ws_acc(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_wsacc), sizeof(unsigned long long) * 1024 * 8 * 7));
   return CACTO_OK;
 }
+// k_rollout_sw's accumulated phase cycles: 1024 x 2 x 6 values (see the kernel)
+extern "C" int cacto_debug_rollout_sw_acc(unsigned long long* out_h) {
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_swacc), sizeof(unsigned long long) * 1024 * 2 * 6));
+  return CACTO_OK;
+}
 // k_rollout_tt's accumulated phase cycles: 1024 x 2 x 2 x 10 values (see the kernel)
 extern "C" int cacto_debug_rollout_tt_acc(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipDeviceSynchronize());
@@ -1638,9 +1921,10 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
                                    const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
-  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -3,
-                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams) or -3 (one slot per wave, layer 2 "
-                "split over K)");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -3 ||
+                    groups == -4,
+                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams), -3 (one slot per wave, layer 2 "
+                "split over K) or -4 (actor waves beside dynamics waves, 3-joint chains)");
   CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
   CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
                 "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");
