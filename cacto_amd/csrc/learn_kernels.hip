@@ -844,6 +844,168 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 }
 
+// ---------------------------------------------------------------- weight-gradient GEMM, large batches
+// k_wgrad_big (rows > 1024: the B >= 1024 updates). The same items as k_wgrad (a block of up to 4 x 4
+// output tiles of one layer over one row chunk, or up to 4 bias tiles, slab[chunk][P] out), but the
+// 4 waves split the block's TILES instead of its rows: wave w owns A tile w (NI = 4; B tile w when
+// NI = 1) and walks every 16-row step of the chunk, so each wave's accumulators cover the whole chunk
+// and are written straight to the slab (no cross-wave LDS reduction). The workgroup stages each
+// step's panel slices (NI + NO slices of 16 features x 16 rows, 2 float4 per thread) through a
+// 2-buffer LDS ring, with the global loads issued WGB_AHEAD steps ahead into registers, so the
+// latency of a step's loads hides behind WGB_AHEAD steps of MFMAs (k_wgrad: one step, and a wave
+// covered only 2-4 steps of its chunk, so its time was mostly load latency: 18-21 us per launch at
+// B = 4096 alone, 0.17 of the MFMA peak). Each tile's sum runs over the chunk's rows in row order
+// (one MFMA accumulator chain; four k-phase chains for the 1-tile waves of edge blocks) — a
+// different, fixed order than k_wgrad's four row spans, so the batch sizes that take this kernel
+// form their own, schedule-independent, sums.
+#ifndef WGB_AHEAD
+#define WGB_AHEAD 3
+#endif
+constexpr int WGB_FS = 20;                    // floats per staged feature row (16 rows + 4 pad: LDS banks)
+constexpr int WGB_SLICE = 16 * WGB_FS;        // one 16 x 16 panel slice
+constexpr int WGB_STAGE = 8 * WGB_SLICE;      // up to 4 A + 4 B slices
+
+template <int NI, int NO>
+__device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo, int hi, int it0, int ot0,
+                                          float* __restrict__ out, float* stage) {
+  static_assert((NI == 4 && (NO == 4 || NO == 1)) || (NI == 1 && NO == 4), "block shape");
+  constexpr int NS = NI + NO;  // staged slices per step
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  // the loader's part of a step: slice sl = tid >> 5 (if < NS), feature f = (tid >> 1) & 15, rows
+  // [8 h, 8 h + 8) of the step, h = tid & 1
+  const int sl = tid >> 5, f = (tid >> 1) & 15, h = tid & 1;
+  const bool loader = sl < NS;
+  const float* src = nullptr;
+  if (loader) {
+    const int slc = sl < NI ? sl : sl - NI;
+    const float* base = sl < NI ? Ly.LT + (size_t)(16 * (it0 + slc)) * ld : Ly.RT + (size_t)(16 * (ot0 + slc)) * ld;
+    src = base + (size_t)f * ld + 8 * h;
+  }
+  const int nsteps = (hi - lo) / 16;  // chunks are multiples of 16 rows
+  // landing registers of the next WGB_AHEAD steps (named, not an array: an array passed by
+  // reference went to scratch)
+  float4 r0a, r0b, r1a, r1b, r2a, r2b;
+  // clamped, branch-free loads (a past-the-end or non-loader load rereads a valid address; unused)
+  const float* src_c = loader ? src : Ly.RT;
+  auto load = [&](float4& ra, float4& rb, int s) {
+    const float4* p = reinterpret_cast<const float4*>(src_c + lo + 16 * min(s, nsteps - 1));
+    ra = p[0];
+    rb = p[1];
+  };
+  load(r0a, r0b, 0);
+  load(r1a, r1b, 1);
+  load(r2a, r2b, 2);
+  // this wave's tiles: NI = 4 -> (w, 0..NO-1); NI = 1 -> (0, w)
+  constexpr int NT = NI == 4 ? NO : 1;
+  // accumulator chains per tile: one when the wave has 4 tiles (their MFMAs interleave), one per
+  // k-phase when it has one
+  constexpr int NC = NT == 1 ? 4 : 1;
+  floatx4 acc[NT][NC];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int k = 0; k < NC; ++k) acc[t][k] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int ai = NI == 4 ? wave : 0;
+  // one step from landing registers r: stage them, refill r with step s + WGB_AHEAD, MFMAs
+  auto step = [&](float4& ra, float4& rb, int s) {
+    float* st = stage + (s & 1) * WGB_STAGE;
+    if (loader) {
+      float4* q = reinterpret_cast<float4*>(st + sl * WGB_SLICE + f * WGB_FS + 8 * h);
+      q[0] = ra;
+      q[1] = rb;
+    }
+    load(ra, rb, s + WGB_AHEAD);
+    __syncthreads();
+    // operands: lane (g, c) = feature c, rows 4g .. 4g + 3 of the step (the k_wgrad layout)
+    const float4 av = *reinterpret_cast<const float4*>(st + ai * WGB_SLICE + c * WGB_FS + 4 * g);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int bo = NI == 4 ? t : wave;
+      const float4 bv = *reinterpret_cast<const float4*>(st + (NI + bo) * WGB_SLICE + c * WGB_FS + 4 * g);
+      acc[t][0] = mfma4(av.x, bv.x, acc[t][0]);
+      acc[t][1 % NC] = mfma4(av.y, bv.y, acc[t][1 % NC]);
+      acc[t][2 % NC] = mfma4(av.z, bv.z, acc[t][2 % NC]);
+      acc[t][3 % NC] = mfma4(av.w, bv.w, acc[t][3 % NC]);
+    }
+  };
+  static_assert(WGB_AHEAD == 3, "the step loop below is unrolled by hand for 3 landing buffers");
+  int s = 0;
+  for (; s + 3 <= nsteps; s += 3) {
+    step(r0a, r0b, s);
+    step(r1a, r1b, s + 1);
+    step(r2a, r2b, s + 2);
+  }
+  if (s < nsteps) step(r0a, r0b, s);
+  if (s + 1 < nsteps) step(r1a, r1b, s + 1);
+  // tile sums (four k-phase chains: (c0 + c1) + (c2 + c3)), straight to the slab
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int i = NI == 4 ? wave : 0, o = NI == 4 ? t : wave;
+    floatx4 sm = acc[t][0];
+    if constexpr (NC == 4) sm = (acc[t][0] + acc[t][1 % NC]) + (acc[t][2 % NC] + acc[t][3 % NC]);
+    const int oc = 16 * (ot0 + o) + c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ii = 16 * (it0 + i) + 4 * g + q;
+      if (ii < Ly.in && oc < Ly.out) out[Ly.woff + ii * Ly.out + oc] = sm[q];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wgrad_big(WgArgs a, float* __restrict__ slab, int xcd,
+                                                   unsigned long long* sig_p, unsigned long long sig_v) {
+  __shared__ __attribute__((aligned(16))) float stage[2 * WGB_STAGE];  // 20 KiB
+  if (sig_p && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  int chunk, rem;
+  if (xcd) {
+    const int sl = blockIdx.x >> 3;
+    chunk = (sl / a.tpc) * 8 + (blockIdx.x & 7);
+    rem = sl % a.tpc;
+    if (chunk >= a.nch) return;
+  } else {
+    chunk = blockIdx.x / a.tpc;
+    rem = blockIdx.x - chunk * a.tpc;
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  int li = 0;
+  while (rem >= a.toff[li + 1]) ++li;
+  const WgLayer& Ly = a.l[li];
+  rem -= a.toff[li];
+  const int lo = a.r_begin + chunk * a.CH, hi = min(a.r_end, lo + a.CH);
+  float* out = slab + (size_t)chunk * a.P;
+  const int nbi = (Ly.IT + WG_BLK - 1) / WG_BLK, nbo = (Ly.OT + WG_BLK - 1) / WG_BLK;
+  if (rem < nbi * nbo) {
+    const int it0 = (rem / nbo) * WG_BLK, ot0 = (rem % nbo) * WG_BLK;
+    const int ni = min(WG_BLK, Ly.IT - it0), no = min(WG_BLK, Ly.OT - ot0);
+    const WgLayer lv{Ly.LT, Ly.RT, Ly.in, Ly.out, Ly.IT, Ly.OT, Ly.woff, Ly.boff};
+    if (ni == 4 && no == 4) wgb_block<4, 4>(a.ld, lv, lo, hi, it0, ot0, out, stage);
+    else if (ni == 1 && no == 4) wgb_block<1, 4>(a.ld, lv, lo, hi, it0, ot0, out, stage);
+    else if (ni == 4 && no == 1) wgb_block<4, 1>(a.ld, lv, lo, hi, it0, ot0, out, stage);
+    // (the host checks that every block of the network has one of these shapes)
+  } else {
+    const int ot = (rem - nbi * nbo) * WG_BLK + wave;
+    if (ot >= Ly.OT) return;
+    const float* bp = Ly.RT + (size_t)(16 * ot + c) * a.ld + 4 * g;
+    float s = 0.f;
+    int r = max(lo, a.bias_r0);
+    for (; r + 64 <= hi; r += 64) {  // 4 loads in flight, summed in row order
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(bp + r + 16 * k);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+    for (; r < hi; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(bp + r);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (g == 0 && 16 * ot + c < Ly.out) out[Ly.boff + 16 * ot + c] = s;
+  }
+}
+
 // ---------------------------------------------------------------- Adam (+ packed refresh, soft update)
 struct AdamArgs {
   double beta1, beta2, eps, tau;
@@ -1497,6 +1659,25 @@ WgArgs wg_args(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int
   return a;
 }
 
+// k_wgrad_big for more than 1024 gradient rows (B > 512 for the actor, the critic's two halves), when
+// every 4 x 4 tile block of the network is 4 x 4, 1 x 4 or 4 x 1 tiles (all the configs' networks).
+// A function of the network and the row count only, so every path of one batch size takes the same
+// kernel. CACTO_WG_BIG=0 keeps k_wgrad (A/B; read once).
+bool wgrad_big(const NetTopo& t, int rows) {
+  static const bool env_on = [] {
+    const char* e = std::getenv("CACTO_WG_BIG");
+    return !(e && e[0] == '0');
+  }();
+  if (!env_on || rows <= 1024) return false;
+  for (int l = 0; l < t.L; ++l)
+    for (int i0 = 0; i0 < t.KT[l]; i0 += WG_BLK)
+      for (int o0 = 0; o0 < t.OT[l]; o0 += WG_BLK) {
+        const int ni = std::min(WG_BLK, t.KT[l] - i0), no = std::min(WG_BLK, t.OT[l] - o0);
+        if (!((ni == 4 && (no == 4 || no == 1)) || (ni == 1 && no == 4))) return false;
+      }
+  return true;
+}
+
 // the weight-gradient GEMM of one network into its slabs; returns the chunk count k_adam sums
 int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int bias_r0, float* slab,
                  hipStream_t st, int* nch, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
@@ -1508,7 +1689,10 @@ int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, i
   }();
   const int xcd = forced >= 0 ? forced : a.nch >= 8;
   const int grid = xcd ? 8 * ceil_div(a.nch, 8) * a.tpc : a.nch * a.tpc;
-  hipLaunchKernelGGL(k_wgrad, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
+  if (wgrad_big(t, r_end - r_begin))
+    hipLaunchKernelGGL(k_wgrad_big, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
+  else
+    hipLaunchKernelGGL(k_wgrad, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
   CACTO_CHECK_HIP(hipGetLastError());
   *nch = a.nch;
   return CACTO_OK;
