@@ -60,11 +60,15 @@ struct ChainScalars {
 // Bounded: after ~2^22 polls (seconds) the wait gives up and latches the timeout word, so an
 // ordering bug cannot hang the GPU. The signal words live in cacto_sys::pipe_sig: [0] actor chains
 // finished, [1] timeout latch, [2] critic Adam steps finished, [3] k_adam's last-workgroup counter.
+// ACQ = false: a write-after-read order (the critic's Adam may overwrite what an actor chain read
+// once that chain has finished) — no data flows, so relaxed polls suffice and no L2 maintenance is
+// paid. ACQ = true: the actor chain reads what the critic's Adam wrote (acquire; the caller fences).
+template <bool ACQ>
 __device__ __forceinline__ void pipe_wait(const unsigned long long* wait_p, unsigned long long wait_v,
                                           unsigned long long* latch) {
   if (!wait_p) return;
   for (int k = 0; k < (1 << 22); ++k) {
-    if (__hip_atomic_load(wait_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= wait_v) return;
+    if (__hip_atomic_load(wait_p, ACQ ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= wait_v) return;
     __builtin_amdgcn_s_sleep(2);
   }
   __hip_atomic_store(latch, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -543,7 +547,7 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   CSTAMP(3);
   if (L.wave == 0) fill_input_tile(p, stn, XS, L);
   if (cs.wait_p) {  // pipeline: the critic this pass reads is written by the other stream's Adam
-    if (L.tid == 0) pipe_wait(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
+    if (L.tid == 0) pipe_wait<true>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
     __threadfence();  // acquire at agent scope: no stale L1 / L2 line of that critic buffer
   }
   __syncthreads();
@@ -791,8 +795,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
   // 32 KiB: the 16 tiles are reduced in two rounds of 8, so a GEMM workgroup fits on a CU beside
   // a chain workgroup — the pipelined update runs the two concurrently
   __shared__ float4 part[4 * (WG_BLK * WG_BLK / 2) * 64];
-  if (sig_p && blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (sig_p && blockIdx.x == 0 && threadIdx.x == 0)  // write-after-read order only: relaxed
+    __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int chunk, rem;
   if (xcd) {
     const int sl = blockIdx.x >> 3;
@@ -955,8 +959,8 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wgrad_big(WgArgs a, float* __restrict__ slab, int xcd,
                                                    unsigned long long* sig_p, unsigned long long sig_v) {
   __shared__ __attribute__((aligned(16))) float stage[2 * WGB_STAGE];  // 20 KiB
-  if (sig_p && blockIdx.x == 0 && threadIdx.x == 0)
-    __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (sig_p && blockIdx.x == 0 && threadIdx.x == 0)  // write-after-read order only: relaxed
+    __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int chunk, rem;
   if (xcd) {
     const int sl = blockIdx.x >> 3;
@@ -1100,7 +1104,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
     th0 = src[pc];
     if (a.soft) tg0 = target[pc];
     const AdamScalars s = adam_scalars(a, step);
-    pipe_wait(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);  // the loads above are in flight
+    pipe_wait<false>(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);  // the loads above are in flight
     if (p0 < t.params) {
       float g = q[0];
 #pragma unroll
@@ -1135,7 +1139,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
   const float alpha = fdiv(fmul((float)lr, __fsqrt_rn(fsub(1.f, b2p))), fsub(1.f, b1p));
   const float c1 = (float)(1.0 - a.beta1), c2 = (float)(1.0 - a.beta2), eps = (float)a.eps;
   const float tau = (float)a.tau, omt = (float)(1.0 - a.tau);
-  pipe_wait(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);
+  pipe_wait<false>(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < t.params; p += gridDim.x * blockDim.x) {
     // chunk partials summed in chunk order; loads issued 8 at a time so they overlap
     float g = slab[p];
@@ -2285,17 +2289,21 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   // actor chains on the device, and the critic's Adam(t) polls it (pipe_wait) before overwriting the
   // buffer actor chain(t-3) read; the PER index ring has four buffers, so the sampler of update t
   // overwrites the one actor chain(t-4) read, which Adam(t-1)'s wait covers. Read once; A/B.
-  static const bool devwait = [] {
+  static const int devwait_env = [] {
     const char* e = std::getenv("CACTO_PIPE_DEVWAIT");
-    return e && e[0] == '1';
+    return e ? std::atoi(e) : 0;
   }();
+  const bool devwait = devwait_env >= 1;
   // ... and the side stream's wait on the critic's Adam too (k_adam's last workgroup publishes, the
   // actor chain polls just before its critic pass at s' — its actor forward, dynamics and d r / d a
   // run first), where that cannot starve the critic stream of CUs: 16-sample actor tiles (the q4
   // chains take no wait), at most one actor workgroup per CU (a CU holding one actor workgroup still
   // fits a critic chain, GEMM or Adam workgroup beside it, so the critic stream always progresses),
   // and no PER (the actor chain gathers the sampled rows at its start).
-  const bool devwait_actor = devwait && !per && chain_tile(w.Bp) == CACTO_TILE && w.Bp / CACTO_TILE <= cu_count();
+  // (CACTO_PIPE_DEVWAIT=2; measured r05: DI B = 4096 10.8 k -> 7.5 k updates/s — the acquire side's
+  // agent-scope L2 invalidations and the Adam's releases cost more than the queue marker they replace)
+  const bool devwait_actor = devwait_env >= 2 && !per && chain_tile(w.Bp) == CACTO_TILE &&
+                             w.Bp / CACTO_TILE <= cu_count();
   unsigned long long* const sig = ms->pipe_sig;
   const unsigned long long base = ms->pipe_seq;
   ms->pipe_seq = base + K;  // reserved up front: no later call's waits can be satisfied by this call's values

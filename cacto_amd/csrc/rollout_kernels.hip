@@ -1800,7 +1800,7 @@ struct LaunchRollout {
     // automatic only where it measured faster: the prismatic chain (DI 0.75 -> 0.72 ms at 4096
     // episodes); car_park's step was slower on two teams (0.42 -> 0.50 ms)
     const bool tt_auto = tt_sys && NJ > 0;
-    if (groups < 0 && !tt_sys) {
+    if ((groups == -1 || groups == -3) && !tt_sys) {
       set_error("cacto_rollout_sched: groups -1 / -3 need a system without configuration-dependent M");
       return CACTO_EINVAL;
     }

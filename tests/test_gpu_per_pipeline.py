@@ -6,6 +6,8 @@ its own child process:
     default with PER), with the three-buffer critic rotation and the pidx[t % 3] ring;
   * CACTO_PIPE_DEVWAIT = 1: that ordering on the device (the actor's GEMM publishes finished
     chains, the critic's Adam polls) instead of queue markers, with a four-buffer PER index ring;
+    = 2: also the actor chain's wait on the critic's Adam (the critic's Adam publishes, the chain
+    polls before its critic pass; not with PER);
   * CACTO_PER_FUSED = 0 / 1: the priority update (with the sampler's deferred exp_counter += 1) as
     the one-launch subtree kernel k_per_update_sub, or the round-3 chain k_per_count ->
     k_per_leaves_mw -> k_per_subtrees -> k_per_top.
@@ -120,7 +122,8 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = {}
-    for every2, fused, devwait in (("0", "1", "0"), ("1", "1", "0"), ("1", "0", "0"), ("0", "1", "1")):
+    for every2, fused, devwait in (("0", "1", "0"), ("1", "1", "0"), ("1", "0", "0"), ("0", "1", "1"),
+                                   ("0", "1", "2")):
         env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait)
         r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                            timeout=300)
