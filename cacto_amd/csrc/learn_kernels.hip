@@ -2284,14 +2284,17 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
   const bool every2 = every2_env >= 0 ? every2_env == 1 : per != nullptr;
-  // CACTO_PIPE_DEVWAIT=1: the critic stream's ordering against the side stream without queue
+  // CACTO_PIPE_DEVWAIT >= 1: the critic stream's ordering against the side stream without queue
   // markers — the actor's GEMM (the launch after each actor chain) publishes the count of finished
   // actor chains on the device, and the critic's Adam(t) polls it (pipe_wait) before overwriting the
   // buffer actor chain(t-3) read; the PER index ring has four buffers, so the sampler of update t
   // overwrites the one actor chain(t-4) read, which Adam(t-1)'s wait covers. Read once; A/B.
+  // default 1 (measured r05, 1 MI355X, updates/s: DI B = 4096 12.3 k -> 12.7 k, car_park PER
+  // B = 4096 9.88 k -> 9.98 k, manipulator B = 8192 7.70 k -> 7.68 k); CACTO_PIPE_DEVWAIT=0 restores
+  // the queue markers
   static const int devwait_env = [] {
     const char* e = std::getenv("CACTO_PIPE_DEVWAIT");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 1;
   }();
   const bool devwait = devwait_env >= 1;
   // ... and the side stream's wait on the critic's Adam too (k_adam's last workgroup publishes, the

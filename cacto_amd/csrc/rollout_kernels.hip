@@ -1366,7 +1366,10 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
 // half-step k the actor waves run the actor of half X = k & 1 while the dynamics waves step half
 // Y = 1 - X with the actions the actor produced for it in half-step k - 1: each half advances one
 // env step every two half-steps. Each role synchronises with a team barrier (an LDS arrival counter),
-// the two roles meet at one workgroup barrier per half-step. Every per-slot value is formed by the
+// the two roles meet at one workgroup barrier per half-step. The actor waves also compute the joint
+// placements of the half they just ran, for its dynamics in the next half-step (r05 stamps: on the
+// dynamics waves they were 7.1 k of a 16.3 k-cycle dynamics half-step; the actor waves waited 9.1 k of
+// theirs at the end barrier). Every per-slot value is formed by the
 // functions k_rollout<3, 4> uses, in the same order (ro_actor / ro_layer2 without SPLIT, ro_chain_nle,
 // ro_chain_mass_cols, chain_step, ro_advance, ro_refill), so results are bit-identical to it.
 template <int NJ>
@@ -1463,9 +1466,9 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
   __syncthreads();
   RoTeamBar abar{&Sh.bar_a, 0, L.lane}, dbar{&Sh.bar_d, 0, L.lane};
   const float* W2g = N.flat + N.t.woff[1];
-  // per-phase cycles (CACTO_STAMPS): actor role [0] actor, [1] end barrier; dynamics role [0]
-  // placements + team barrier, [1] RNEA / CRBA + team barrier, [2] step, stores, refill, next input,
-  // [3] end barrier; [5] half-steps
+  // per-phase cycles (CACTO_STAMPS): actor role [0] actor + placements, [1] end barrier; dynamics role
+  // [0] loop test, [1] RNEA / CRBA + team barrier, [2] step, stores, refill, next input, [3] end
+  // barrier; [5] half-steps
 #ifdef CACTO_STAMPS
   unsigned long long wacc[5] = {0, 0, 0, 0, 0}, wprev = __builtin_amdgcn_s_memtime();
   int wsteps = 0;
@@ -1507,6 +1510,17 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
                          Sh.W.x0 + X * NH * 64, Sh.W.a + X * SH * na};
         ro_actor<NH, ns, na, REGK, LDSK, false, false>(R, V, W2g, L, it, abar);
       }
+      // the joint placements X(q_i) of half X's slots for its dynamics in the next half-step (s_t of
+      // the half is final: its last dynamics pass was in half-step it - 1), spread over the 4 waves
+      if (anyX) {
+        const int e = L.lane * 4 + L.wave;  // item (slot X*8 + e % 8, joint e / 8)
+        if (e < SH * NJ) {
+          const int cc = X * SH + e % SH, i = e / SH;
+          if (Sh.sact[cc])
+            se3_st<SL>(Sh.ch.X + i * 12 * SL + cc,
+                       joint_placement(JointView{sd.joints + i * CACTO_JOINT_COLS}, Sh.sS[cc * ns + i]));
+        }
+      }
       SWMARK(0);
       __syncthreads();
       SWMARK(1);
@@ -1520,17 +1534,8 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
       const bool anyX = Sh.any[par][par] != 0, anyY = Sh.any[par][Y] != 0;
       if (!anyX && !anyY) break;
       // the dynamics of half Y, from the actions its actor pass wrote in half-step it - 1
+      // (its joint placements were computed by the actor waves at the end of that actor pass)
       const bool run = anyY && it > 0;
-      if (run) {
-        const int lc = L.tid;  // placements: item (slot Y*8 + lc % 8, joint lc / 8)
-        if (lc < SH * NJ) {
-          const int cc = Y * SH + lc % SH, i = lc / SH;
-          if (Sh.sact[cc])
-            se3_st<SL>(Sh.ch.X + i * 12 * SL + cc,
-                       joint_placement(JointView{sd.joints + i * CACTO_JOINT_COLS}, Sh.sS[cc * ns + i]));
-        }
-        dbar();
-      }
       SWMARK(0);
       const int cy = Y * SH + (L.lane & (SH - 1));  // this lane's slot of half Y
       const bool act_y = run && L.lane < SH && Sh.sact[cy] != 0;

@@ -31,8 +31,9 @@ def main():
     a, d = v[used, 0], v[used, 1]
     hs = a[:, 5].sum()
     print("%s %d k_rollout_sw, %d workgroups, %.0f half-steps each" % (system, R, used.sum(), a[:, 5].mean()))
-    print("   actor waves per half-step: actor %.0f, end barrier %.0f" % (a[:, 0].sum() / hs, a[:, 1].sum() / hs))
-    print("   dynamics waves per half-step: placements + bar %.0f, RNEA / CRBA + bar %.0f, step + stores + refill "
+    print("   actor waves per half-step: actor + placements %.0f, end barrier %.0f" % (a[:, 0].sum() / hs,
+                                                                                  a[:, 1].sum() / hs))
+    print("   dynamics waves per half-step: loop test %.0f, RNEA / CRBA + bar %.0f, step + stores + refill "
           "+ next input %.0f, end barrier %.0f" % tuple(d[:, k].sum() / hs for k in range(4)))
 
 
