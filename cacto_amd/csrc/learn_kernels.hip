@@ -672,6 +672,7 @@ struct WgArgs {
   WgLayer l[MAX_LAYERS];
   int nl, ld, r_begin, r_end, bias_r0, CH, nch, P, tpc;
   int toff[MAX_LAYERS + 1];
+  unsigned char perm[64];  // k_wgrad_big: the items of a chunk by decreasing work (full 4 x 4 blocks first)
 };
 
 // One workgroup per (row chunk, item). An item is a block of up to 4 x 4 output tiles of one layer
@@ -956,6 +957,11 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
   }
 }
 
+//
+// Grid order: block b runs on XCD b % 8 (observed dealing), which owns chunks x, x + 8, ...; its j-th
+// block (j = b / 8) takes item perm[j / cpx] of its chunk j % cpx — every XCD starts with the full
+// 4 x 4 blocks of all its chunks, one per CU, before the lighter items fill in (with the work dealt
+// chunk-major, two heavy items could share a CU's matrix cores while others idled).
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wgrad_big(WgArgs a, float* __restrict__ slab, int xcd,
                                                    unsigned long long* sig_p, unsigned long long sig_v) {
   __shared__ __attribute__((aligned(16))) float stage[2 * WGB_STAGE];  // 20 KiB
@@ -963,13 +969,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int chunk, rem;
   if (xcd) {
-    const int sl = blockIdx.x >> 3;
-    chunk = (sl / a.tpc) * 8 + (blockIdx.x & 7);
-    rem = sl % a.tpc;
-    if (chunk >= a.nch) return;
+    const int j = blockIdx.x >> 3, cpx = (a.nch + 7) >> 3;
+    const int pi = j / cpx;
+    chunk = (j - pi * cpx) * 8 + (blockIdx.x & 7);
+    if (chunk >= a.nch || pi >= a.tpc) return;
+    rem = a.perm[pi];
   } else {
     chunk = blockIdx.x / a.tpc;
-    rem = blockIdx.x - chunk * a.tpc;
+    rem = a.perm[blockIdx.x - chunk * a.tpc];
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   int li = 0;
@@ -1660,6 +1667,24 @@ WgArgs wg_args(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int
   }
   a.toff[t.L] = tpc;
   a.tpc = tpc;
+  // items by decreasing work: 4 x 4 tile blocks, then edge blocks, then bias groups (stable)
+  std::vector<std::pair<int, int>> cost;
+  for (int l = 0; l < t.L; ++l) {
+    const int nbi = ceil_div(t.KT[l], WG_BLK), nbo = ceil_div(t.OT[l], WG_BLK);
+    for (int k = 0; k < nbi * nbo; ++k) {
+      const int ni = std::min(WG_BLK, t.KT[l] - (k / nbo) * WG_BLK), no = std::min(WG_BLK, t.OT[l] - (k % nbo) * WG_BLK);
+      cost.push_back({-ni * no, a.toff[l] + k});
+    }
+    for (int k = 0; k < nbo; ++k) cost.push_back({0, a.toff[l] + nbi * nbo + k});
+  }
+  std::stable_sort(cost.begin(), cost.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
+    return x.first < y.first;
+  });
+  static const bool perm_on = [] {  // CACTO_WG_PERM=0: chunk-major item order (A/B; read once)
+    const char* e = std::getenv("CACTO_WG_PERM");
+    return !(e && e[0] == '0');
+  }();
+  for (int k = 0; k < 64; ++k) a.perm[k] = k < tpc ? (unsigned char)(perm_on ? cost[k].second : k) : 0;
   return a;
 }
 
