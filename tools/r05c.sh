@@ -14,3 +14,9 @@ for e in "CACTO_RO_SW=1" "CACTO_RO_SW=0" "CACTO_WG_PERM=0" "CACTO_WG_CHUNK=128" 
   echo "== $i $e" >> gpurun_out/r05c/summary.txt; python3 tools/bench_summary.py gpurun_out/r05c/bench_${i}.log >> gpurun_out/r05c/summary.txt || true
 done
 cat gpurun_out/r05c/summary.txt
+for e in "CACTO_PER_PRIO=1" "CACTO_PER_PRIO=0"; do
+  i=$((i+1))
+  step 300 gpurun_out/r05c/bench_${i}.log env $e python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-config0 --no-diagnostics --long-steps 0 --update-steps 400 --batches 4096 --extra-systems car_park
+  echo "== $i $e" >> gpurun_out/r05c/summary.txt; python3 tools/bench_summary.py gpurun_out/r05c/bench_${i}.log >> gpurun_out/r05c/summary.txt || true
+done
+cat gpurun_out/r05c/summary.txt
