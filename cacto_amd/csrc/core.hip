@@ -122,6 +122,7 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
     if (e) (void)hipEventDestroy(e);
   if (sys->side) (void)hipStreamDestroy(sys->side);
   if (sys->pipe_sig) (void)hipFree(sys->pipe_sig);
+  if (sys->pipe_wsig) (void)hipFree(sys->pipe_wsig);
   delete sys;
   return CACTO_OK;
 }

@@ -20,6 +20,7 @@ struct cacto_sys {
   // handle's life), [1] latches a wait that timed out, [3] is k_adam's last-workgroup counter;
   // pipe_seq is the host's count of pipeline iterations issued before this call
   unsigned long long* pipe_sig = nullptr;
+  unsigned long long* pipe_wsig = nullptr;  // CACTO_PIPE_SIGNAL: hipStreamWaitValue64 word (signal memory)
   unsigned long long pipe_seq = 0;
   // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (layer << 16 | net << 15 | item, -1 = none), for
   // the critic alone, the actor alone and both (built at creation, cacto_build_wgrad_adam_items)

@@ -2253,6 +2253,20 @@ int ensure_side_stream(cacto_sys* ms) {
     if (side) (void)hipStreamDestroy(side);
     return hip_fail(e, "cacto_update_n: pipeline signal");
   }
+  // the side stream's wait word for CACTO_PIPE_SIGNAL (stream memory operations need signal memory);
+  // optional: without it the events are used
+  unsigned long long* wsig = nullptr;
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&wsig), sizeof(unsigned long long), hipMallocSignalMemory) ==
+      hipSuccess) {
+    if (hipMemset(wsig, 0, sizeof(unsigned long long)) != hipSuccess) {
+      (void)hipFree(wsig);
+      wsig = nullptr;
+    }
+  } else {
+    wsig = nullptr;
+    (void)hipGetLastError();
+  }
+  ms->pipe_wsig = wsig;
   ms->pipe_sig = sig;
   ms->pipe_seq = 0;
   ms->ev_critic = ev[0];
@@ -2333,6 +2347,13 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   const bool devwait_actor = devwait_env >= 2 && !per && chain_tile(w.Bp) == CACTO_TILE &&
                              w.Bp / CACTO_TILE <= cu_count();
   unsigned long long* const sig = ms->pipe_sig;
+  // CACTO_PIPE_SIGNAL=1: the side stream's wait on the critic's Adam as a stream write / wait-value
+  // pair on a signal-memory word instead of an event record / wait (A/B; read once)
+  static const bool sig_env = [] {
+    const char* e = std::getenv("CACTO_PIPE_SIGNAL");
+    return e && e[0] == '1';
+  }();
+  const bool streamval = sig_env && ms->pipe_wsig && !devwait_actor;
   const unsigned long long base = ms->pipe_seq;
   ms->pipe_seq = base + K;  // reserved up front: no later call's waits can be satisfied by this call's values
   for (int t = 0; t < K; ++t) {
@@ -2364,10 +2385,14 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
                                  devwait_actor ? sig : nullptr, base + t + 1))
       return e;
     *cbuf = (t + 1) % 3;
-    if (!devwait_actor) CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+    if (streamval) CACTO_CHECK_HIP(hipStreamWriteValue64(st, ms->pipe_wsig, base + t + 1, 0));
+    else if (!devwait_actor) CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
     if (per)
       if (int e = per_priority_update(per, idx, y, V, B, late_count, st)) return e;
-    if (!devwait_actor) CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+    if (streamval)
+      CACTO_CHECK_HIP(hipStreamWaitValue64(side, ms->pipe_wsig, base + t + 1, hipStreamWaitValueGte));
+    else if (!devwait_actor)
+      CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side, devwait_actor ? sig + 2 : nullptr,
                                    base + t + 1))
       return e;

@@ -8,6 +8,8 @@ its own child process:
     chains, the critic's Adam polls) instead of queue markers, with a four-buffer PER index ring;
     = 2: also the actor chain's wait on the critic's Adam (the critic's Adam publishes, the chain
     polls before its critic pass; not with PER);
+  * CACTO_PIPE_SIGNAL = 1: the side stream's wait on the critic's Adam as a stream write-value /
+    wait-value pair instead of an event;
   * CACTO_PER_FUSED = 0 / 1: the priority update (with the sampler's deferred exp_counter += 1) as
     the one-launch subtree kernel k_per_update_sub, or the round-3 chain k_per_count ->
     k_per_leaves_mw -> k_per_subtrees -> k_per_top.
@@ -122,14 +124,15 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = {}
-    for every2, fused, devwait in (("0", "1", "0"), ("1", "1", "0"), ("1", "0", "0"), ("0", "1", "1"),
-                                   ("0", "1", "2")):
-        env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait)
+    for every2, fused, devwait, signal in (("0", "1", "0", "0"), ("1", "1", "0", "0"), ("1", "0", "0", "0"),
+                                           ("0", "1", "1", "0"), ("0", "1", "2", "0"), ("0", "1", "1", "1")):
+        env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait,
+                   CACTO_PIPE_SIGNAL=signal)
         r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
-        res[(every2, fused, devwait)] = json.loads(line[len("RESULT "):])
+        res[(every2, fused, devwait, signal)] = json.loads(line[len("RESULT "):])
     for key, r in res.items():
         assert r["K6_equal"] and r["K7_equal"] and r["di_equal"] and r["latch"] == 0, key
     for field in ("K6_hash", "K7_hash", "unsorted_hash"):
