@@ -1584,9 +1584,13 @@ inline int wg_chunk_big() {
   }();
   return v;
 }
+// Row chunk of the weight-gradient GEMM. From 4096 rows on 256-row chunks: k_wgrad_big walks a whole
+// chunk per wave, so longer chunks amortise its pipeline fill (r05, updates/s: DI B = 4096 — the actor's
+// 4096 rows — 12.97 k at 128 rows, 13.25 k at 256; car_park PER B = 4096 10.14 k / 9.86 k; 512 rows
+// 12.49 k); CACTO_WG_CHUNK overrides it above 1024 rows (read once; benchmarks).
 inline int wg_chunk(int rows) {
   if (rows > 1024 && wg_chunk_big() > 0) return wg_chunk_big();
-  return rows <= 1024 ? 64 : rows <= 4096 ? 128 : 256;
+  return rows <= 1024 ? 64 : rows < 4096 ? 128 : 256;
 }
 
 struct Workspace {
