@@ -54,7 +54,20 @@ struct ChainScalars {
   // its critic pass at s', until *wait_p >= wait_v (the critic's Adam of the same update has run)
   const unsigned long long* wait_p;
   unsigned long long wait_v;
+  // 1: the 16-sample tiles dealt so that the tiles of one 256-row GEMM chunk run on the XCD that
+  // k_wgrad_big runs that chunk on (chain_tile_of)
+  int xcd_tiles;
 };
+
+// Block b -> tile of a 16-sample chain grid. xcd_tiles (ntiles % 128 == 0): block b runs on XCD
+// b % 8 (the dispatcher's round robin), which k_wgrad_big gives the 256-row chunks x, x + 8, ... —
+// 16 tiles each — so XCD x takes the tiles of exactly those chunks and their panel rows are written
+// into the L2 the GEMM reads them from. Which block runs a tile changes no value.
+__device__ __forceinline__ int chain_tile_of(int b, int ntiles, int xcd_tiles) {
+  if (!xcd_tiles) return b;
+  const int x = b & 7, j = b >> 3;
+  return ((j >> 4) * 8 + x) * 16 + (j & 15);
+}
 
 // The device-side waits of the pipeline: until *wait_p >= wait_v (normally already true: one load).
 // Bounded: after ~2^22 polls (seconds) the wait gives up and latches the timeout word, so an
@@ -331,7 +344,8 @@ __global__ void __launch_bounds__(CACTO_THREADS)
                   int B, GradBufs gb, float* __restrict__ y_out, float* __restrict__ V_out, float* __restrict__ Vt_out,
                   int32_t* __restrict__ step) {
   __shared__ CriticLds S;
-  critic_chain(S, blockIdx.x, sdp, C, Tg, cs, storage, idx, isw, B, gb, y_out, V_out, Vt_out, step);
+  critic_chain(S, chain_tile_of(blockIdx.x, gridDim.x, cs.xcd_tiles), sdp, C, Tg, cs, storage, idx, isw, B, gb, y_out,
+               V_out, Vt_out, step);
 }
 
 // env_simulate_derivative (env.h) of a revolute chain for a tile's T samples, spread over threads
@@ -631,7 +645,7 @@ __global__ void __launch_bounds__(CACTO_THREADS) __attribute__((amdgpu_waves_per
                  const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
                  int32_t* __restrict__ step) {
   __shared__ ActorLds S;
-  actor_chain<NJ>(S, blockIdx.x, sdp, Ac, C, cs, storage, idx, B, gb, step);
+  actor_chain<NJ>(S, chain_tile_of(blockIdx.x, gridDim.x, cs.xcd_tiles), sdp, Ac, C, cs, storage, idx, B, gb, step);
 }
 
 // The critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the
@@ -1739,6 +1753,13 @@ ChainScalars chain_scalars(const cacto_update_cfg* cfg, int B) {
   cs.want_vt = cfg->want_target_V;
   cs.wait_p = nullptr;
   cs.wait_v = 0;
+  // CACTO_CHAIN_XCD=0 keeps the tiles in block order (A/B; read once)
+  static const bool xcd_env = [] {
+    const char* e = std::getenv("CACTO_CHAIN_XCD");
+    return !(e && e[0] == '0');
+  }();
+  const int Bp = (B + 15) / 16 * 16;
+  cs.xcd_tiles = xcd_env && (Bp / CACTO_TILE) % 128 == 0 && wg_chunk(Bp) == 256 && wg_chunk(2 * Bp) == 256;
   return cs;
 }
 

@@ -375,7 +375,8 @@ __global__ void __launch_bounds__(256) k_per_subtrees(double* __restrict__ sum_t
 //      old + 1 after a barrier), so the pipelined update needs no separate counting launch;
 //   3. the subtree's levels rebuilt in LDS and written back (as k_per_subtrees);
 //   4. the last workgroup to finish (a counter in the unused word sum_tree[0], reset to 0 = +0.0
-//      afterwards) rebuilds the nodes above the subtree roots (as k_per_top).
+//      afterwards) rebuilds the nodes above the subtree roots (as k_per_top); the roots are stored
+//      at agent scope and counted after their stores completed, so no L2-wide fence is needed.
 // max_priority by the atomic bit-pattern max of k_per_leaves_mw. A set `skip` flag (the ReLO
 // priority rule's error status) leaves the trees, counters and max_priority unchanged. Every value
 // is formed as on the k_per_leaves_mw + k_per_count + k_per_subtrees + k_per_top path, so the
@@ -472,6 +473,7 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
       const int32_t id = id_s[i];
       if (first_occ(i, id)) exp_counter[id] += 1.0;
     }
+  const int64_t nroot = cap / sub;
   int lvl = 0;
   for (int lo = sub / 2; lo >= 1; lo /= 2) {
     ++lvl;
@@ -479,21 +481,29 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
       ts[k] = ts[2 * k] + ts[2 * k + 1];
       tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
       const int64_t g = (leaf0 >> lvl) + (k - lo);
-      sum_tree[g] = ts[k];
-      min_tree[g] = tm[k];
+      if (k == 1 && nroot > 1) {
+        // the subtree root, read by the last workgroup below: stored at agent scope (coherent
+        // across the XCDs' L2s) instead of releasing the whole L2 with a fence — a fence's L2
+        // write-back here also flushed the concurrent chains' panel writes (29 us per launch)
+        __hip_atomic_store(sum_tree + g, ts[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(min_tree + g, tm[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        sum_tree[g] = ts[k];
+        min_tree[g] = tm[k];
+      }
     }
     __syncthreads();
   }
-  const int64_t nroot = cap / sub;
   if (nroot == 1) return;
-  // last workgroup done: release this workgroup's node writes, count, and acquire the others'
-  __threadfence();
-  __syncthreads();
+  // last workgroup done: the root stores have completed (vmcnt 0) before the count
   unsigned long long* done = reinterpret_cast<unsigned long long*>(sum_tree);
-  if (tid == 0) *last_s = atomicAdd(done, 1ull) == (unsigned long long)(gridDim.x - 1);
+  if (tid == 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    *last_s = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              (unsigned long long)(gridDim.x - 1);
+  }
   __syncthreads();
   if (!*last_s) return;
-  __threadfence();
   for (int64_t k = nroot + tid; k < 2 * nroot; k += blockDim.x) {
     ts[k] = __hip_atomic_load(sum_tree + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tm[k] = __hip_atomic_load(min_tree + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -508,7 +518,7 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
     }
     __syncthreads();
   }
-  if (tid == 0) *done = 0ull;  // the +0.0 of segment_tree.py's unused node 0
+  if (tid == 0) __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // +0.0, node 0
 }
 
 // The nodes above the subtree roots, [1, cap / sub), from the roots (one workgroup, LDS).
