@@ -553,6 +553,48 @@ def test_per_sample_global_matches_oracle(ref_vectors):
         np.testing.assert_allclose(w.cpu().numpy(), ow.astype(np.float32), rtol=1e-6)
 
 
+@pytest.mark.parametrize("cap", [2, 1024, 8192, 16384, 1 << 18, 1 << 20])
+def test_per_sample_multi_workgroup_every_depth(cap):
+    """The multi-workgroup sampler (B >= 512) at every split of the descent: all levels staged in
+    LDS (cap <= 8192), a 1..4-level tail below the staged top, and three-level rounds above the
+    tail (2^18, 2^20). Indices bit-exact, IS weights and exp_counter against the oracle."""
+    from cacto_amd import _lib as L
+    from cacto_amd.system import dptr, stream
+    rng = np.random.default_rng(cap)
+    leaves = rng.uniform(0.01, 2.0, size=cap) ** 0.6
+    leaves[rng.integers(0, cap, size=max(1, cap // 7))] = 0.0  # empty slots (never sampled)
+    st, mt = np.zeros(2 * cap), np.full(2 * cap, np.inf)
+    st[cap:], mt[cap:] = leaves, np.where(leaves > 0, leaves, np.inf)
+    lo = cap // 2
+    while lo >= 1:  # parent = op(left, right) level by level, as SegmentTree.__setitem__ leaves it
+        k = np.arange(lo, 2 * lo)
+        st[k] = st[2 * k] + st[2 * k + 1]
+        mt[k] = np.where(mt[2 * k + 1] < mt[2 * k], mt[2 * k + 1], mt[2 * k])
+        lo //= 2
+    o = obuf.PrioritizedReplayBuffer(cap, 1, 0.6, 0.6, 1e-2, 0.95, 0)
+    o.it_sum.value, o.it_min.value = list(st), list(mt)
+    max_idx = cap if cap <= 8192 else cap - 5
+    o.N, o.next_idx, o.full = cap, max_idx % cap, max_idx == cap
+    assert o.max_idx() == max_idx
+    for B in (512, 1000):
+        o.B = B
+        u = rng.uniform(size=B)
+        oidx = o.sample_proportional(list(u))
+        ow = o.sample_weights(oidx)
+        sd, md = torch.as_tensor(st, device="cuda"), torch.as_tensor(mt, device="cuda")
+        ud = torch.as_tensor(u, device="cuda")
+        idx = torch.empty(B, dtype=torch.int32, device="cuda")
+        w = torch.empty(B, dtype=torch.float32, device="cuda")
+        cnt = torch.zeros(cap, dtype=torch.float64, device="cuda")
+        L.lib().call("cacto_per_sample", dptr(sd), dptr(md), cap, max_idx, 0.6, dptr(ud), B, dptr(idx), dptr(w),
+                     dptr(cnt), stream())
+        np.testing.assert_array_equal(idx.cpu().numpy(), oidx)
+        np.testing.assert_allclose(w.cpu().numpy(), ow.astype(np.float32), rtol=1e-6)
+        ref_cnt = np.zeros(cap)
+        ref_cnt[oidx] += 1
+        np.testing.assert_array_equal(cnt.cpu().numpy(), ref_cnt)
+
+
 def test_per_update_priorities_matches_oracle():
     from cacto_amd.replay_buffer import PrioritizedReplayBuffer
     from cacto_amd.system import System
