@@ -870,24 +870,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 // NI = 1) and walks every 16-row step of the chunk, so each wave's accumulators cover the whole chunk
 // and are written straight to the slab (no cross-wave LDS reduction). The workgroup stages each
 // step's panel slices (NI + NO slices of 16 features x 16 rows, 2 float4 per thread) through a
-// 2-buffer LDS ring, with the global loads issued WGB_AHEAD steps ahead into registers, so the
-// latency of a step's loads hides behind WGB_AHEAD steps of MFMAs (k_wgrad: one step, and a wave
+// 2-buffer LDS ring, with the global loads issued AH steps ahead into registers, so the
+// latency of a step's loads hides behind AH steps of MFMAs (k_wgrad: one step, and a wave
 // covered only 2-4 steps of its chunk, so its time was mostly load latency: 18-21 us per launch at
 // B = 4096 alone, 0.17 of the MFMA peak). Each tile's sum runs over the chunk's rows in row order
 // (one MFMA accumulator chain; four k-phase chains for the 1-tile waves of edge blocks) — a
 // different, fixed order than k_wgrad's four row spans, so the batch sizes that take this kernel
 // form their own, schedule-independent, sums.
-#ifndef WGB_AHEAD
-#define WGB_AHEAD 3
-#endif
 constexpr int WGB_FS = 20;                    // floats per staged feature row (16 rows + 4 pad: LDS banks)
 constexpr int WGB_SLICE = 16 * WGB_FS;        // one 16 x 16 panel slice
 constexpr int WGB_STAGE = 8 * WGB_SLICE;      // up to 4 A + 4 B slices
 
-template <int NI, int NO>
+template <int NI, int NO, int AH>
 __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo, int hi, int it0, int ot0,
                                           float* __restrict__ out, float* stage) {
   static_assert((NI == 4 && (NO == 4 || NO == 1)) || (NI == 1 && NO == 4), "block shape");
+  static_assert(AH == 3 || AH == 6, "the step loop below is unrolled by hand for 3 or 6 landing buffers");
   constexpr int NS = NI + NO;  // staged slices per step
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
   // the loader's part of a step: slice sl = tid >> 5 (if < NS), feature f = (tid >> 1) & 15, rows
@@ -901,9 +899,9 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
     src = base + (size_t)f * ld + 8 * h;
   }
   const int nsteps = (hi - lo) / 16;  // chunks are multiples of 16 rows
-  // landing registers of the next WGB_AHEAD steps (named, not an array: an array passed by
-  // reference went to scratch)
-  float4 r0a, r0b, r1a, r1b, r2a, r2b;
+  // landing registers of the next AH steps (named, not an array: an array passed by reference
+  // went to scratch)
+  float4 r0a, r0b, r1a, r1b, r2a, r2b, r3a, r3b, r4a, r4b, r5a, r5b;
   // clamped, branch-free loads (a past-the-end or non-loader load rereads a valid address; unused)
   const float* src_c = loader ? src : Ly.RT;
   auto load = [&](float4& ra, float4& rb, int s) {
@@ -914,6 +912,11 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
   load(r0a, r0b, 0);
   load(r1a, r1b, 1);
   load(r2a, r2b, 2);
+  if constexpr (AH == 6) {
+    load(r3a, r3b, 3);
+    load(r4a, r4b, 4);
+    load(r5a, r5b, 5);
+  }
   // this wave's tiles: NI = 4 -> (w, 0..NO-1); NI = 1 -> (0, w)
   constexpr int NT = NI == 4 ? NO : 1;
   // accumulator chains per tile: one when the wave has 4 tiles (their MFMAs interleave), one per
@@ -925,7 +928,7 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
 #pragma unroll
     for (int k = 0; k < NC; ++k) acc[t][k] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int ai = NI == 4 ? wave : 0;
-  // one step from landing registers r: stage them, refill r with step s + WGB_AHEAD, MFMAs
+  // one step from landing registers r: stage them, refill r with step s + AH, MFMAs
   auto step = [&](float4& ra, float4& rb, int s) {
     float* st = stage + (s & 1) * WGB_STAGE;
     if (loader) {
@@ -933,7 +936,7 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
       q[0] = ra;
       q[1] = rb;
     }
-    load(ra, rb, s + WGB_AHEAD);
+    load(ra, rb, s + AH);
     __syncthreads();
     // operands: lane (g, c) = feature c, rows 4g .. 4g + 3 of the step (the k_wgrad layout)
     const float4 av = *reinterpret_cast<const float4*>(st + ai * WGB_SLICE + c * WGB_FS + 4 * g);
@@ -947,15 +950,24 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
       acc[t][3 % NC] = mfma4(av.w, bv.w, acc[t][3 % NC]);
     }
   };
-  static_assert(WGB_AHEAD == 3, "the step loop below is unrolled by hand for 3 landing buffers");
   int s = 0;
-  for (; s + 3 <= nsteps; s += 3) {
+  for (; s + AH <= nsteps; s += AH) {
     step(r0a, r0b, s);
     step(r1a, r1b, s + 1);
     step(r2a, r2b, s + 2);
+    if constexpr (AH == 6) {
+      step(r3a, r3b, s + 3);
+      step(r4a, r4b, s + 4);
+      step(r5a, r5b, s + 5);
+    }
   }
   if (s < nsteps) step(r0a, r0b, s);
   if (s + 1 < nsteps) step(r1a, r1b, s + 1);
+  if constexpr (AH == 6) {
+    if (s + 2 < nsteps) step(r2a, r2b, s + 2);
+    if (s + 3 < nsteps) step(r3a, r3b, s + 3);
+    if (s + 4 < nsteps) step(r4a, r4b, s + 4);
+  }
   // tile sums (four k-phase chains: (c0 + c1) + (c2 + c3)), straight to the slab
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -976,6 +988,7 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
 // block (j = b / 8) takes item perm[j / cpx] of its chunk j % cpx — every XCD starts with the full
 // 4 x 4 blocks of all its chunks, one per CU, before the lighter items fill in (with the work dealt
 // chunk-major, two heavy items could share a CU's matrix cores while others idled).
+template <int AH>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wgrad_big(WgArgs a, float* __restrict__ slab, int xcd,
                                                    unsigned long long* sig_p, unsigned long long sig_v) {
   __shared__ __attribute__((aligned(16))) float stage[2 * WGB_STAGE];  // 20 KiB
@@ -1004,9 +1017,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int it0 = (rem / nbo) * WG_BLK, ot0 = (rem % nbo) * WG_BLK;
     const int ni = min(WG_BLK, Ly.IT - it0), no = min(WG_BLK, Ly.OT - ot0);
     const WgLayer lv{Ly.LT, Ly.RT, Ly.in, Ly.out, Ly.IT, Ly.OT, Ly.woff, Ly.boff};
-    if (ni == 4 && no == 4) wgb_block<4, 4>(a.ld, lv, lo, hi, it0, ot0, out, stage);
-    else if (ni == 1 && no == 4) wgb_block<1, 4>(a.ld, lv, lo, hi, it0, ot0, out, stage);
-    else if (ni == 4 && no == 1) wgb_block<4, 1>(a.ld, lv, lo, hi, it0, ot0, out, stage);
+    if (ni == 4 && no == 4) wgb_block<4, 4, AH>(a.ld, lv, lo, hi, it0, ot0, out, stage);
+    else if (ni == 1 && no == 4) wgb_block<1, 4, AH>(a.ld, lv, lo, hi, it0, ot0, out, stage);
+    else if (ni == 4 && no == 1) wgb_block<4, 1, AH>(a.ld, lv, lo, hi, it0, ot0, out, stage);
     // (the host checks that every block of the network has one of these shapes)
   } else {
     const int ot = (rem - nbi * nbo) * WG_BLK + wave;
@@ -1736,8 +1749,20 @@ int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, i
   }();
   const int xcd = forced >= 0 ? forced : a.nch >= 8;
   const int grid = xcd ? 8 * ceil_div(a.nch, 8) * a.tpc : a.nch * a.tpc;
-  if (wgrad_big(t, r_end - r_begin))
-    hipLaunchKernelGGL(k_wgrad_big, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
+  // k_wgrad_big's load lead in 16-row steps: 3, or 6 with CACTO_WGB_AHEAD=6 (same sums). Measured
+  // (updates/s, two runs each): DI B = 4096 13.41 / 13.38 k at 6 against 13.33 / 13.37 k at 3,
+  // manipulator B = 8192 8.29 / 8.26 k against 8.36 / 8.34 k — inside the pipeline the GEMM is not
+  // waiting on its loads, so the lighter form stays.
+  static const int ahead = [] {
+    const char* e = std::getenv("CACTO_WGB_AHEAD");
+    return e && std::atoi(e) == 6 ? 6 : 3;
+  }();
+  if (wgrad_big(t, r_end - r_begin)) {
+    if (ahead == 3)
+      hipLaunchKernelGGL(k_wgrad_big<3>, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
+    else
+      hipLaunchKernelGGL(k_wgrad_big<6>, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
+  }
   else
     hipLaunchKernelGGL(k_wgrad, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
   CACTO_CHECK_HIP(hipGetLastError());

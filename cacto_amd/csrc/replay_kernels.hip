@@ -615,10 +615,31 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
   const int tid = threadIdx.x;
   const int64_t id_lo = (int64_t)blockIdx.x * sub, id_hi = id_lo + sub;
   const int64_t leaf0 = cap + id_lo;
-  for (int i = tid; i < n; i += blockDim.x) id_s[i] = idx[i];
-  for (int k = tid; k < sub; k += blockDim.x) {
-    ts[sub + k] = sum_tree[leaf0 + k];
-    tm[sub + k] = min_tree[leaf0 + k];
+  // the index list and both subtrees' leaves: every load in flight before the first LDS write (a
+  // plain staging loop waited for each load in turn: 16 + 4 dependent memory latencies at B = 4096)
+  {
+    constexpr int NI = PER_MAX_B / 256, NL = PER_SUB / 256;
+    int iv[NI];
+    double sv[NL], mv[NL];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) iv[j] = tid + 256 * j < n ? idx[tid + 256 * j] : 0;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int k = tid + 256 * j;
+      sv[j] = k < sub ? sum_tree[leaf0 + k] : 0.0;
+      mv[j] = k < sub ? min_tree[leaf0 + k] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      if (tid + 256 * j < n) id_s[tid + 256 * j] = iv[j];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int k = tid + 256 * j;
+      if (k < sub) {
+        ts[sub + k] = sv[j];
+        tm[sub + k] = mv[j];
+      }
+    }
   }
   __syncthreads();
   bool unsorted = false;
