@@ -15,6 +15,10 @@ struct cacto_sys {
   hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its events
   hipEvent_t ev_critic = nullptr, ev_actor[3] = {nullptr, nullptr, nullptr};
   std::mutex pipe_mu;  // one two-stream pipeline at a time per handle (they share side / events)
+  // the PER pipeline's third stream (priority update + next sample beside the critic's GEMM and Adam)
+  // and its two events: the critic chain finished / the next sample is drawn
+  hipStream_t per_st = nullptr;
+  hipEvent_t ev_chain = nullptr, ev_samp = nullptr;
   // device-side ordering of the two-stream pipeline (CACTO_PIPE_DEVWAIT): pipe_sig[0] counts the actor
   // iterations whose chain has finished, [2] the critic Adam steps finished (both monotonic over the
   // handle's life), [1] latches a wait that timed out, [3] is k_adam's last-workgroup counter;
@@ -45,3 +49,6 @@ int cacto_per_count_launch(const int32_t* idx_d, int B, double* exp_counter_d, h
 int cacto_per_update_count(double* sum_tree_d, double* min_tree_d, int64_t capacity, const int32_t* idx_d,
                            const float* y_d, const float* V_d, double* exp_counter_d, double fresh_factor, double eps,
                            double alpha, double* max_priority_d, int B, hipStream_t st);
+int cacto_per_sample_runs_launch(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
+                                 double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
+                                 int32_t* runs_d, hipStream_t st);

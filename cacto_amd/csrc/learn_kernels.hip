@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "net_common.h"
+#include "per_device.h"
 
 #ifdef CACTO_STAMPS
 __device__ unsigned long long g_cstamps[32];
@@ -989,21 +990,20 @@ __device__ __forceinline__ void wgb_block(const int ld, const WgLayer Ly, int lo
 // 4 x 4 blocks of all its chunks, one per CU, before the lighter items fill in (with the work dealt
 // chunk-major, two heavy items could share a CU's matrix cores while others idled).
 template <int AH>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wgrad_big(WgArgs a, float* __restrict__ slab, int xcd,
-                                                   unsigned long long* sig_p, unsigned long long sig_v) {
-  __shared__ __attribute__((aligned(16))) float stage[2 * WGB_STAGE];  // 20 KiB
-  if (sig_p && blockIdx.x == 0 && threadIdx.x == 0)  // write-after-read order only: relaxed
+__device__ __forceinline__ void wgrad_big_body(const int blk, const WgArgs& a, float* __restrict__ slab, int xcd,
+                                               unsigned long long* sig_p, unsigned long long sig_v, float* stage) {
+  if (sig_p && blk == 0 && threadIdx.x == 0)  // write-after-read order only: relaxed
     __hip_atomic_store(sig_p, sig_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   int chunk, rem;
   if (xcd) {
-    const int j = blockIdx.x >> 3, cpx = (a.nch + 7) >> 3;
+    const int j = blk >> 3, cpx = (a.nch + 7) >> 3;
     const int pi = j / cpx;
-    chunk = (j - pi * cpx) * 8 + (blockIdx.x & 7);
+    chunk = (j - pi * cpx) * 8 + (blk & 7);
     if (chunk >= a.nch || pi >= a.tpc) return;
     rem = a.perm[pi];
   } else {
-    chunk = blockIdx.x / a.tpc;
-    rem = a.perm[blockIdx.x - chunk * a.tpc];
+    chunk = blk / a.tpc;
+    rem = a.perm[blk - chunk * a.tpc];
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   int li = 0;
@@ -1042,6 +1042,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     s += __shfl_xor(s, 32);
     if (g == 0 && 16 * ot + c < Ly.out) out[Ly.boff + 16 * ot + c] = s;
   }
+}
+
+template <int AH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wgrad_big(WgArgs a, float* __restrict__ slab, int xcd,
+                                                   unsigned long long* sig_p, unsigned long long sig_v) {
+  __shared__ __attribute__((aligned(16))) float stage[2 * WGB_STAGE];  // 20 KiB
+  wgrad_big_body<AH>(blockIdx.x, a, slab, xcd, sig_p, sig_v, stage);
+}
+
+// The pipelined PER loop's critic GEMM with the priority update of the same update in one grid:
+// blocks [0, nwg) are k_wgrad_big's (the same XCD dealing: nwg is its grid), the next nroot run
+// per_update_run_body over the subtrees. Both need only the critic chain before them, and the next
+// sample needs both (the trees, and this stream's order). LDS: the GEMM's 20 KiB ring, the priority
+// update's 10 KiB in the same bytes.
+template <int AH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
+k_wgrad_big_per(WgArgs a, float* __restrict__ slab, int xcd, int nwg, PerRunArgs pa, int nroot) {
+  static_assert(sizeof(PerRunLds) <= 2 * WGB_STAGE * sizeof(float), "LDS union");
+  __shared__ __attribute__((aligned(16))) float stage[2 * WGB_STAGE];  // 20 KiB
+  if ((int)blockIdx.x < nwg) wgrad_big_body<AH>(blockIdx.x, a, slab, xcd, nullptr, 0, stage);
+  else per_update_run_body(blockIdx.x - nwg, nroot, pa, *reinterpret_cast<PerRunLds*>(stage));
 }
 
 // ---------------------------------------------------------------- Adam (+ packed refresh, soft update)
@@ -1120,6 +1141,64 @@ __device__ __forceinline__ void adam_publish(unsigned long long* sig_p, unsigned
   }
 }
 
+// One parameter per thread, workgroup blk (NCH > 0).
+template <int NCH>
+__device__ __forceinline__ void adam_nch_body(const int blk, const float* __restrict__ slab, int nch, const NetTopo& t,
+                                              const float* src, float* netbuf, float4* packed, float* __restrict__ m,
+                                              float* __restrict__ v, const int32_t* __restrict__ step, const AdamArgs& a,
+                                              float* target, float4* target_packed, const unsigned long long* wait_p,
+                                              unsigned long long wait_v) {
+  const int p0 = blk * 256 + threadIdx.x;
+  float q[NCH], mm = 0.f, vv = 0.f, th0 = 0.f, tg0 = 0.f;
+  const int pc = min(p0, t.params - 1);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) q[k] = slab[(size_t)min(k, nch - 1) * t.params + pc];
+  mm = m[pc];
+  vv = v[pc];
+  th0 = src[pc];
+  if (a.soft) tg0 = target[pc];
+  const AdamScalars s = adam_scalars(a, step);
+  pipe_wait<false>(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);  // the loads above are in flight
+  if (p0 < t.params) {
+    float g = q[0];
+#pragma unroll
+    for (int k = 1; k < NCH; ++k)
+      if (k < nch) g += q[k];
+    mm = fadd(mm, fmul(fsub(g, mm), s.c1));
+    vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
+    const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
+    m[p0] = mm;
+    v[p0] = vv;
+    netbuf[p0] = th;
+    write_packed(packed, t, p0, th);
+    if (a.soft) {
+      const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
+      target[p0] = tg;
+      write_packed(target_packed, t, p0, tg);
+    }
+  }
+}
+
+// The pipelined PER loop's critic Adam step with the next update's sample in one grid: blocks
+// [0, nadam) are k_adam<NCH>'s, the rest run per_sample_body (4,096-node top, recording the runs for
+// the next priority update). The sample needs the trees this update's priority update left (the
+// launch before on this stream); the next critic chain needs both.
+template <int NCH>
+__global__ void __launch_bounds__(256) k_adam_sample(const float* __restrict__ slab, int nch, NetTopo t, const float* src,
+                                                     float* netbuf, float4* packed, float* __restrict__ m,
+                                                     float* __restrict__ v, const int32_t* __restrict__ step, AdamArgs a,
+                                                     float* target, float4* target_packed,
+                                                     const unsigned long long* wait_p, unsigned long long wait_v,
+                                                     int nadam, PerSampleArgs sa) {
+  __shared__ double top_s[PER_FUSED_TOP];
+  __shared__ double scal_s[4];
+  if ((int)blockIdx.x < nadam)
+    adam_nch_body<NCH>(blockIdx.x, slab, nch, t, src, netbuf, packed, m, v, step, a, target, target_packed, wait_p,
+                       wait_v);
+  else
+    per_sample_body<PER_FUSED_TOP>(blockIdx.x - nadam, sa, top_s, scal_s);
+}
+
 template <int NCH>
 __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, int nch, NetTopo t, const float* src,
                                               float* netbuf, float4* packed, float* __restrict__ m, float* __restrict__ v,
@@ -1128,35 +1207,8 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
                                               unsigned long long wait_v, unsigned long long* sig_p,
                                               unsigned long long sig_v) {
   if constexpr (NCH > 0) {
-    const int p0 = blockIdx.x * blockDim.x + threadIdx.x;
-    float q[NCH], mm = 0.f, vv = 0.f, th0 = 0.f, tg0 = 0.f;
-    const int pc = min(p0, t.params - 1);
-#pragma unroll
-    for (int k = 0; k < NCH; ++k) q[k] = slab[(size_t)min(k, nch - 1) * t.params + pc];
-    mm = m[pc];
-    vv = v[pc];
-    th0 = src[pc];
-    if (a.soft) tg0 = target[pc];
-    const AdamScalars s = adam_scalars(a, step);
-    pipe_wait<false>(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);  // the loads above are in flight
-    if (p0 < t.params) {
-      float g = q[0];
-#pragma unroll
-      for (int k = 1; k < NCH; ++k)
-        if (k < nch) g += q[k];
-      mm = fadd(mm, fmul(fsub(g, mm), s.c1));
-      vv = fadd(vv, fmul(fsub(fmul(g, g), vv), s.c2));
-      const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
-      m[p0] = mm;
-      v[p0] = vv;
-      netbuf[p0] = th;
-      write_packed(packed, t, p0, th);
-      if (a.soft) {
-        const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
-        target[p0] = tg;
-        write_packed(target_packed, t, p0, tg);
-      }
-    }
+    adam_nch_body<NCH>(blockIdx.x, slab, nch, t, src, netbuf, packed, m, v, step, a, target, target_packed, wait_p,
+                       wait_v);
     adam_publish(sig_p, sig_v);
     return;
   }
@@ -1625,8 +1677,9 @@ struct Workspace {
   float* slab;    // critic weight-gradient slabs
   float* slab_a;  // actor's (a separate region: cacto_update_n overlaps the two steps)
   float* cshadow; // two more critic net buffers (cacto_update_n rotates the critic over three)
-  int32_t* pidx;  // cacto_update_n_per: sampled indices, a ring of four buffers of Bp
+  int32_t* pidx;  // cacto_update_n_per: sampled indices, a ring of five buffers of Bp
   float* pisw;    // and the IS weights of the current update
+  int32_t* runs;  // the overlapped PER loop's per-subtree sample runs (2 x PER_RUN_SUB ints)
   float* scal;  // y, V, Vt scratch (3 * Bp)
   size_t bytes;
   int Bp;
@@ -1671,9 +1724,11 @@ Workspace plan(const cacto_sys* sys, int B, char* base) {
   w.cshadow = f ? f + off : nullptr;
   off += 2 * align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
   w.pidx = f ? reinterpret_cast<int32_t*>(f + off) : nullptr;
-  off += align64((size_t)4 * Bp);
+  off += align64((size_t)5 * Bp);
   w.pisw = f ? f + off : nullptr;
   off += align64((size_t)Bp);
+  w.runs = f ? reinterpret_cast<int32_t*>(f + off) : nullptr;
+  off += align64((size_t)2 * PER_RUN_SUB);
   w.scal = f ? f + off : nullptr;
   off += align64((size_t)3 * Bp);
   w.bytes = off * sizeof(float);
@@ -1740,7 +1795,8 @@ bool wgrad_big(const NetTopo& t, int rows) {
 
 // the weight-gradient GEMM of one network into its slabs; returns the chunk count k_adam sums
 int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, int bias_r0, float* slab,
-                 hipStream_t st, int* nch, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
+                 hipStream_t st, int* nch, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0,
+                 const PerRunArgs* per_run = nullptr) {
   const WgArgs a = wg_args(t, gb, r_begin, r_end, bias_r0);
   // chunks grouped by XCD from 8 chunks on (CACTO_WG_XCD=0 / 1 forces it off / on; benchmarks)
   static const int forced = [] {
@@ -1757,7 +1813,13 @@ int launch_wgrad(const NetTopo& t, const GradBufs& gb, int r_begin, int r_end, i
     const char* e = std::getenv("CACTO_WGB_AHEAD");
     return e && std::atoi(e) == 6 ? 6 : 3;
   }();
-  if (wgrad_big(t, r_end - r_begin)) {
+  if (per_run) {  // the PER loop's fused form (the caller checked wgrad_big and the tree's shape)
+    const int nroot = (int)(per_run->cap / PER_RUN_SUB);
+    if (ahead == 3)
+      hipLaunchKernelGGL(k_wgrad_big_per<3>, dim3(grid + nroot), dim3(256), 0, st, a, slab, xcd, grid, *per_run, nroot);
+    else
+      hipLaunchKernelGGL(k_wgrad_big_per<6>, dim3(grid + nroot), dim3(256), 0, st, a, slab, xcd, grid, *per_run, nroot);
+  } else if (wgrad_big(t, r_end - r_begin)) {
     if (ahead == 3)
       hipLaunchKernelGGL(k_wgrad_big<3>, dim3(grid), dim3(256), 0, st, a, slab, xcd, sig_p, sig_v);
     else
@@ -1860,7 +1922,8 @@ int launch_actor_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, c
 int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, int which,
                 const float* slab, int nch, int soft, hipStream_t st, const float* src = nullptr,
                 const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0,
-                unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
+                unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0,
+                const PerSampleArgs* sample = nullptr) {
   const NetTopo& t = topo(sys, which);
   float* nb = which == CACTO_NET_CRITIC ? nets->critic_d : nets->actor_d;
   float* m = which == CACTO_NET_CRITIC ? nets->critic_m_d : nets->actor_m_d;
@@ -1875,6 +1938,23 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, slab, nch, t, s0, nb, pk, m, v, nets->step_d, aa,
                        nets->target_d, tpk, wait_p, wait_v, sig_p, sig_v);
   };
+  if (sample) {  // the PER loop's fused form (the caller checked nch <= 64)
+    if (sig_p || nch > 64) {
+      set_error("k_adam_sample: no publishing Adam, at most 64 chunks");
+      return CACTO_EINVAL;
+    }
+    const int ns = (sample->B + 255) / 256;
+    auto gs = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(full + ns), dim3(256), 0, st, slab, nch, t, s0, nb, pk, m, v, nets->step_d, aa,
+                         nets->target_d, tpk, wait_p, wait_v, full, *sample);
+    };
+    if (nch <= 8) gs(k_adam_sample<8>);
+    else if (nch <= 16) gs(k_adam_sample<16>);
+    else if (nch <= 32) gs(k_adam_sample<32>);
+    else gs(k_adam_sample<64>);
+    CACTO_CHECK_HIP(hipGetLastError());
+    return CACTO_OK;
+  }
   if (nch <= 8) go(k_adam<8>, full);
   else if (nch <= 16) go(k_adam<16>, full);
   else if (nch <= 32) go(k_adam<32>, full);
@@ -1945,17 +2025,31 @@ int launch_wgrad_adam(const cacto_sys* sys, int mode, const AdamNet& n0, const A
 // critic step after its chain: GEMM + Adam (+ soft update) from src into nb
 int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
                      hipStream_t st, const float* src, float* nb, const unsigned long long* wait_p = nullptr,
-                     unsigned long long wait_v = 0, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
+                     unsigned long long wait_v = 0, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0,
+                     const PerRunArgs* per_run = nullptr, const PerSampleArgs* sample = nullptr) {
   const int soft = cfg->MC ? 0 : 1;
   if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 0, critic_adam_net(sys, nets, cfg, w, soft, src, nb), nullptr,
                                                  nets->step_d, st);
   const bool sob = cfg->w_S != 0.0;
   int nch = 0;
-  if (int e = launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, &nch)) return e;
+  if (int e = launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, &nch, nullptr, 0, per_run))
+    return e;
   cacto_nets dst = *nets;
   dst.critic_d = nb;
-  return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, nch, soft, st, src, wait_p, wait_v, sig_p, sig_v);
+  return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, nch, soft, st, src, wait_p, wait_v, sig_p, sig_v,
+                     sample);
 }
+
+// CACTO_PER_OVERLAP (default 1): the pipelined PER loop's priority update and next sample share the
+// critic GEMM's and Adam's launches (k_wgrad_big_per, k_adam_sample) instead of following them.
+bool per_overlap_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("CACTO_PER_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 
 int actor_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
                     hipStream_t st, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0) {
@@ -2202,6 +2296,18 @@ struct PerArgs {
   double *exp_counter, *max_priority;
 };
 
+// Whether the PER loop of this batch can take the overlapped form: the count deferred into the
+// priority update (large batches), a priority update at all (alpha != 0), 256-leaf subtrees whose
+// roots fit one workgroup, the large-batch critic GEMM and an Adam step with all chunks in flight.
+bool per_overlap_ok(const cacto_sys* sys, const cacto_update_cfg* cfg, const PerArgs* per, int B, const Workspace& w) {
+  if (!per || !per_overlap_on() || B < cacto_per_mw_min() || per->alpha == 0.0) return false;
+  if (per->cap < 2 * PER_RUN_SUB || per->cap > (int64_t)PER_RUN_SUB * PER_RUN_SUB || per->cap % PER_RUN_SUB) return false;
+  if (fused_adam(w.Bp)) return false;
+  const bool sob = cfg->w_S != 0.0;
+  const int r0 = sob ? 0 : w.Bp, r1 = 2 * w.Bp;
+  return wgrad_big(sys->critic, r1 - r0) && ceil_div(r1 - r0, wg_chunk(r1 - r0)) <= 64;
+}
+
 // The priority update of one PER step (RL.py:129-131). late_count: the sampler left its
 // exp_counter += 1 to this call (large batches), which applies it first, in the same launch. With
 // alpha == 0 the reference skips update_priorities (RL.py:130) — the count still happens.
@@ -2327,6 +2433,37 @@ int ensure_side_stream(cacto_sys* ms) {
   return CACTO_OK;
 }
 
+// The PER stream and its two events (created on first use, published only when all exist).
+int ensure_per_stream(cacto_sys* ms) {
+  if (ms->per_st) return CACTO_OK;
+  hipStream_t ps = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  const unsigned evf = hipEventDisableTiming | (std::getenv("CACTO_EVENT_SYSFENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+  hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], evf);
+  if (e != hipSuccess) {
+    for (hipEvent_t x : ev)
+      if (x) (void)hipEventDestroy(x);
+    if (ps) (void)hipStreamDestroy(ps);
+    return hip_fail(e, "cacto_update_n_per: PER stream / events");
+  }
+  ms->ev_chain = ev[0];
+  ms->ev_samp = ev[1];
+  ms->per_st = ps;
+  return CACTO_OK;
+}
+
+// CACTO_PER_STREAM (default 1): the pipelined PER loop runs the priority update of update t and the
+// sample of update t + 1 on a third stream, beside the critic's GEMM and Adam of update t (their
+// only common input is critic chain t; the next critic chain needs both). 0: all on the critic stream.
+bool per_stream_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("CACTO_PER_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                          const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
                          const Workspace& w, hipStream_t st, int* cbuf);
@@ -2336,6 +2473,8 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
   cacto_sys* ms = const_cast<cacto_sys*>(sys);
   std::lock_guard<std::mutex> lock(ms->pipe_mu);
   if (int e = ensure_side_stream(ms)) return e;
+  if (per && per_stream_on())
+    if (int e = ensure_per_stream(ms)) return e;
   const NetTopo& tc = sys->critic;
   const size_t nb_bytes = ((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256) * sizeof(float);
   const size_t nb_stride = align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
@@ -2343,12 +2482,17 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
   CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow + nb_stride, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));  // everything the caller queued before
   CACTO_CHECK_HIP(hipStreamWaitEvent(ms->side, ms->ev_critic, 0));
+  if (per && per_stream_on()) CACTO_CHECK_HIP(hipStreamWaitEvent(ms->per_st, ms->ev_critic, 0));
   // cbuf: the buffer (0 caller's, 1-2 workspace) holding the newest critic; on every exit, error or
   // not, the side stream joins the caller's stream and the newest critic lands in the caller's buffer
   int cbuf = 0;
   const int err = update_pipeline_body(sys, nets, cfg, storage_d, idx_d, per, K, B, w, st, &cbuf);
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, ms->side));
   CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
+  if (per && per_stream_on()) {
+    CACTO_CHECK_HIP(hipEventRecord(ms->ev_samp, ms->per_st));
+    CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_samp, 0));
+  }
   if (cbuf)
     CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow + (cbuf - 1) * nb_stride, nb_bytes,
                                    hipMemcpyDeviceToDevice, st));
@@ -2404,6 +2548,17 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     return e && e[0] == '1';
   }();
   const bool streamval = sig_env && ms->pipe_wsig && !devwait_actor;
+  // the PER stream (per_stream_on) with the device-side write-after-read order: the index ring has
+  // five buffers — sample t + 1 runs after critic chain t, which follows Adam(t - 1)'s wait for actor
+  // chain t - 4, the last reader of the buffer it overwrites
+  // the overlapped form (per_overlap_ok): priority update t inside the critic GEMM's launch, sample
+  // t + 1 inside its Adam's; the same five-buffer ring (sample t + 1 runs in the launch after the
+  // Adam(t - 1) that waited for actor chain t - 4)
+  const bool ovl = per && devwait && per_overlap_ok(sys, cfg, per, B, w);
+  const bool pst = per && devwait && !ovl && ms->per_st && per_stream_on();
+  hipStream_t pst_s = ms->per_st;
+  const int nring = (pst || ovl) ? 5 : devwait ? 4 : 3;
+  const int nroot = per ? (int)(per->cap / PER_RUN_SUB) : 0;
   const unsigned long long base = ms->pipe_seq;
   ms->pipe_seq = base + K;  // reserved up front: no later call's waits can be satisfied by this call's values
   for (int t = 0; t < K; ++t) {
@@ -2419,10 +2574,28 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     const int32_t* idx = idx_d + (size_t)t * B;
     const float* isw = nullptr;
     if (per) {
-      int32_t* pi = w.pidx + (size_t)(t % (devwait ? 4 : 3)) * w.Bp;
-      if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
-                                   per->uniforms + (size_t)t * B, B, pi, w.pisw, late_count ? nullptr : per->exp_counter, st))
+      int32_t* pi = w.pidx + (size_t)(t % nring) * w.Bp;
+      if (ovl) {
+        if (t == 0) {  // the first sample, recording its runs; later ones run inside the Adam launch
+          CACTO_CHECK_HIP(hipMemsetAsync(w.runs, 0x7f, (size_t)nroot * sizeof(int32_t), st));
+          CACTO_CHECK_HIP(hipMemsetAsync(w.runs + nroot, 0, (size_t)nroot * sizeof(int32_t), st));
+          if (int e = cacto_per_sample_runs_launch(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                                   per->uniforms, B, pi, w.pisw, w.runs, st))
+            return e;
+        }
+      } else if (pst) {
+        if (t == 0) {  // the first sample; later ones follow the previous priority update on per_st
+          if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                       per->uniforms, B, pi, w.pisw, late_count ? nullptr : per->exp_counter, pst_s))
+            return e;
+          CACTO_CHECK_HIP(hipEventRecord(ms->ev_samp, pst_s));
+        }
+        CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_samp, 0));
+      } else if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                          per->uniforms + (size_t)t * B, B, pi, w.pisw,
+                                          late_count ? nullptr : per->exp_counter, st)) {
         return e;
+      }
       idx = pi;
       isw = w.pisw;
     }
@@ -2430,14 +2603,40 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     cur.critic_d = buf[t % 3];
     nxt.critic_d = buf[(t + 1) % 3];
     if (int e = launch_critic_chain(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
+    if (pst) {
+      // priority update t and sample t + 1 beside the critic's GEMM and Adam: they need critic chain t
+      // (y, V; its reads of the IS weights and indices), and critic chain t + 1 waits for the sample
+      CACTO_CHECK_HIP(hipEventRecord(ms->ev_chain, st));
+      CACTO_CHECK_HIP(hipStreamWaitEvent(pst_s, ms->ev_chain, 0));
+      if (int e = per_priority_update(per, idx, y, V, B, late_count, pst_s)) return e;
+      if (t + 1 < K) {
+        int32_t* pn = w.pidx + (size_t)((t + 1) % nring) * w.Bp;
+        if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                     per->uniforms + (size_t)(t + 1) * B, B, pn, w.pisw,
+                                     late_count ? nullptr : per->exp_counter, pst_s))
+          return e;
+        CACTO_CHECK_HIP(hipEventRecord(ms->ev_samp, pst_s));
+      }
+    }
     const bool dw = devwait && t >= 3;
+    PerRunArgs pra{};
+    PerSampleArgs psa{};
+    if (ovl) {
+      pra = PerRunArgs{per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->max_idx,
+                       per->fresh, per->eps, per->alpha, per->max_priority, w.runs};
+      if (t + 1 < K)
+        psa = PerSampleArgs{per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                            per->uniforms + (size_t)(t + 1) * B, B, w.pidx + (size_t)((t + 1) % nring) * w.Bp,
+                            w.pisw, nullptr, 0, w.runs};
+    }
     if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d, dw ? sig : nullptr, base + t - 2,
-                                 devwait_actor ? sig : nullptr, base + t + 1))
+                                 devwait_actor ? sig : nullptr, base + t + 1, ovl ? &pra : nullptr,
+                                 ovl && t + 1 < K ? &psa : nullptr))
       return e;
     *cbuf = (t + 1) % 3;
     if (streamval) CACTO_CHECK_HIP(hipStreamWriteValue64(st, ms->pipe_wsig, base + t + 1, 0));
     else if (!devwait_actor) CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
-    if (per)
+    if (per && !pst && !ovl)
       if (int e = per_priority_update(per, idx, y, V, B, late_count, st)) return e;
     if (streamval)
       CACTO_CHECK_HIP(hipStreamWaitValue64(side, ms->pipe_wsig, base + t + 1, hipStreamWaitValueGte));

@@ -5,13 +5,13 @@
 #include <cstdlib>
 
 #include "internal.h"
+#include "per_device.h"
 
 namespace cacto {
 
 constexpr int PER_THREADS = 1024;
 constexpr int PER_MAX_B = 8192;
 
-__device__ __forceinline__ double tree_min(double a, double b) { return b < a ? b : a; }  // Python min(a, b)
 
 __global__ void k_per_init(double* sum_tree, double* min_tree, int64_t n2) {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n2; k += (int64_t)gridDim.x * blockDim.x) {
@@ -253,219 +253,20 @@ __global__ void __launch_bounds__(SPT == 1 ? 256 : PER_THREADS) k_per_sample(con
   }
 }
 
-// Select a[j] (j in [0, N)) from a register array without dynamic indexing (no scratch).
-// A tournament of selects on j's bits (a chain of j == q selects gets folded back into an indexed
-// load, which moves the array to scratch).
-template <int N>
-__device__ __forceinline__ double reg_pick(const double (&a)[N], int j) {
-  static_assert((N & (N - 1)) == 0, "power of two");
-  double w[N];
-#pragma unroll
-  for (int q = 0; q < N; ++q) w[q] = a[q];
-#pragma unroll
-  for (int h = N / 2, b = 0; h >= 1; h /= 2, ++b)
-#pragma unroll
-    for (int q = 0; q < h; ++q) w[q] = ((j >> b) & 1) ? w[2 * q + 1] : w[2 * q];
-  return w[0];
-}
-
-// The last R levels of find_prefixsum_idx below node n (whose descendants R levels down are the
-// leaves): the left child of every internal node and all 2^R leaves are loaded together, so the R
-// comparisons and the sampled leaf's own value (P(i) of the IS weight) cost one memory latency.
-// Same comparisons and subtractions as the reference's loop (segment_tree.py:103-114), in order.
-// One internal level D (1-based) of per_tail: its left children are lv[2^(D-1) - 1 + q].
-template <int D, int NLV>
-__device__ __forceinline__ void tail_step(const double (&lv)[NLV], int& j, double& p) {
-  double row[1 << (D - 1)];
-#pragma unroll
-  for (int q = 0; q < (1 << (D - 1)); ++q) row[q] = lv[(1 << (D - 1)) - 1 + q];
-  const double left = reg_pick(row, j);
-  if (left > p) {
-    j = 2 * j;
-  } else {
-    p -= left;
-    j = 2 * j + 1;
-  }
-}
-
-template <int R>
-__device__ __forceinline__ void per_tail(const double* __restrict__ tree, int64_t n, double& p, int64_t& node,
-                                         double& val) {
-  static_assert(R >= 1 && R <= 4, "per_tail covers up to four levels");
-  constexpr int NL = 1 << R;
-  double lf[NL];
-  double lv[R > 1 ? (1 << (R - 1)) - 1 : 1];
-#pragma unroll
-  for (int d = 1; d < R; ++d)
-#pragma unroll
-    for (int j = 0; j < (1 << (d - 1)); ++j) lv[(1 << (d - 1)) - 1 + j] = tree[(n << d) + 2 * j];
-#pragma unroll
-  for (int k = 0; k < NL; ++k) lf[k] = tree[(n << R) + k];
-  int j = 0;  // position within the current level below n
-  if constexpr (R > 1) tail_step<1>(lv, j, p);
-  if constexpr (R > 2) tail_step<2>(lv, j, p);
-  if constexpr (R > 3) tail_step<3>(lv, j, p);
-  const double left = reg_pick(lf, 2 * j);
-  if (left > p) {
-    j = 2 * j;
-  } else {
-    p -= left;
-    j = 2 * j + 1;
-  }
-  node = (n << R) + j;
-  val = reg_pick(lf, j);
-}
-
-// The multi-workgroup sampler (B >= CACTO_PER_MW_MIN, default 512): one sample per thread, 256
-// per workgroup. Each workgroup stages the top 8,192 nodes (depths 0..12, 64 KiB LDS) with every
-// thread's loads in flight at once while thread 0 gathers the batch scalars' terms in the same
-// latency; the descent walks the staged levels in LDS and finishes with per_tail (one more memory
-// latency for the remaining levels and the leaf value). For the 2^16-row buffer that is two
-// dependent global latencies per sample instead of four. exp_counter follows in k_per_count.
-constexpr int PER_MW_TOP = 8192;
-__global__ void __launch_bounds__(256) k_per_sample_mw(const double* __restrict__ sum_tree, const double* __restrict__ min_tree,
-                                                       int64_t cap, int64_t max_idx, double beta,
-                                                       const double* __restrict__ uniforms, int B, int32_t* __restrict__ idx_out,
-                                                       float* __restrict__ w_out, const double* __restrict__ shards, int n_shards) {
+// The multi-workgroup sampler (B >= CACTO_PER_MW_MIN, default 512): per_sample_body (per_device.h)
+// with an 8,192-node top, one sample per thread, 256 per workgroup. exp_counter follows in k_per_count.
+__global__ void __launch_bounds__(256) k_per_sample_mw(PerSampleArgs a) {
   __shared__ double top_s[PER_MW_TOP];
-  __shared__ double seg_s, total_s, maxw_s, scale_s;
-  const int64_t ntop = cap < PER_MW_TOP ? cap : PER_MW_TOP;
-  // wave 0: lane k loads the k-th term of prefix_reduce's sum(0, max_idx - 1) (the walk is the
-  // same for every lane; lane k stops at step k), lane 63 the roots; issued before the staging
-  // loads so both wait on one latency
-  double term = 0.0, root_sum = 0.0, root_min = 0.0;
-  bool has_term = false;
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const int64_t end = max_idx - 2;
-    int64_t node = 1, ns = 0, ne = cap - 1, at = -1;
-    for (int k = 0; k <= lane && at < 0; ++k) {
-      if (end == ne) {
-        if (k == lane) at = node;
-        break;
-      }
-      const int64_t mid = (ns + ne) / 2;
-      if (end <= mid) {
-        node = 2 * node;
-        ne = mid;
-      } else {
-        if (k == lane) at = 2 * node;
-        node = 2 * node + 1;
-        ns = mid + 1;
-      }
-    }
-    has_term = at >= 0;
-    if (has_term) term = sum_tree[at];
-    if (lane == 63) {
-      root_sum = sum_tree[1];
-      if (!shards) root_min = min_tree[1];
-    }
-  }
-  // the staging: ntop / 2 double2 pairs over 256 threads, all loads issued before the LDS writes
-  {
-    constexpr int PAIRS = PER_MW_TOP / 2 / 256;
-    const double2* src = reinterpret_cast<const double2*>(sum_tree);
-    double2 st[PAIRS];
-#pragma unroll
-    for (int r = 0; r < PAIRS; ++r) {
-      const int64_t q = threadIdx.x + r * 256;
-      st[r] = 2 * q < ntop ? src[q] : make_double2(0.0, 0.0);
-    }
-#pragma unroll
-    for (int r = 0; r < PAIRS; ++r) {
-      const int64_t q = threadIdx.x + r * 256;
-      if (2 * q < ntop) reinterpret_cast<double2*>(top_s)[q] = st[r];
-    }
-  }
-  if (threadIdx.x < 64) {
-    // the right-nested sum, deepest term first, as prefix_reduce combines them
-    const unsigned long long mask = __ballot(has_term);
-    root_sum = __shfl(root_sum, 63);
-    root_min = __shfl(root_min, 63);
-    double r = 0.0;
-    bool have = false;
-    for (int k = 63; k >= 0; --k)
-      if ((mask >> k) & 1ull) {
-        const double tk = __shfl(term, k);
-        r = have ? tk + r : tk;
-        have = true;
-      }
-    if (threadIdx.x == 0) {
-    seg_s = r / B;
-    total_s = root_sum;
-    if (shards) {  // as k_per_sample (data-parallel shards)
-      double n_all = 0.0, ratio_min = __builtin_inf();
-      for (int g = 0; g < n_shards; ++g) {
-        n_all += shards[3 * g + 2];
-        ratio_min = tree_min(ratio_min, shards[3 * g + 1] / shards[3 * g + 0]);
-      }
-      scale_s = n_all / n_shards;
-      maxw_s = pow(ratio_min * scale_s, -beta);
-    } else {
-      const double p_min = root_min / root_sum;
-      scale_s = (double)max_idx;
-      maxw_s = pow(p_min * scale_s, -beta);
-    }
-    }
-  }
-  __syncthreads();
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= B) return;
-  const double seg = seg_s;
-  double p = uniforms[i] * seg + i * seg;
-  int64_t nd = 1;
-  while (2 * nd < ntop) {
-    const double left = top_s[2 * nd];
-    if (left > p) {
-      nd = 2 * nd;
-    } else {
-      p -= left;
-      nd = 2 * nd + 1;
-    }
-  }
-  // levels below the staged top, three at a time, until at most four remain
-  int rem = 0;
-  for (int64_t s = nd; s < cap; s *= 2) ++rem;  // levels from nd down to the leaves
-  while (rem > 4) {
-    const double a = sum_tree[2 * nd], b0 = sum_tree[4 * nd], b1 = sum_tree[4 * nd + 2];
-    double c[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = sum_tree[8 * nd + 2 * q];
-    int64_t m;
-    if (a > p) {
-      m = 2 * nd;
-    } else {
-      p -= a;
-      m = 2 * nd + 1;
-    }
-    const double bl = (m & 1) ? b1 : b0;
-    if (bl > p) {
-      m = 2 * m;
-    } else {
-      p -= bl;
-      m = 2 * m + 1;
-    }
-    const double cl = reg_pick(c, (int)(m - 4 * nd));
-    if (cl > p) {
-      m = 2 * m;
-    } else {
-      p -= cl;
-      m = 2 * m + 1;
-    }
-    nd = m;
-    rem -= 3;
-  }
-  int64_t leaf;
-  double val;
-  switch (rem) {
-    case 4: per_tail<4>(sum_tree, nd, p, leaf, val); break;
-    case 3: per_tail<3>(sum_tree, nd, p, leaf, val); break;
-    case 2: per_tail<2>(sum_tree, nd, p, leaf, val); break;
-    case 1: per_tail<1>(sum_tree, nd, p, leaf, val); break;
-    default: leaf = nd; val = sum_tree[nd]; break;  // capacity 1: the root is the leaf
-  }
-  idx_out[i] = (int32_t)(leaf - cap);
-  w_out[i] = (float)(pow(val / total_s * scale_s, -beta) / maxw_s);
+  __shared__ double scal_s[4];
+  per_sample_body<PER_MW_TOP>(blockIdx.x, a, top_s, scal_s);
+}
+
+// The pipelined PER loop's first sample (the later ones run inside k_adam_sample): the 4,096-node top
+// of the fused form, with the per-subtree runs for per_update_run_body.
+__global__ void __launch_bounds__(256) k_per_sample_runs(PerSampleArgs a) {
+  __shared__ double top_s[PER_FUSED_TOP];
+  __shared__ double scal_s[4];
+  per_sample_body<PER_FUSED_TOP>(blockIdx.x, a, top_s, scal_s);
 }
 
 // The leaf writes of k_per_set over many workgroups, one leaf per thread (the two f64 pows of a
@@ -643,7 +444,7 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
   }
   __syncthreads();
   bool unsorted = false;
-  for (int i = tid; i + 1 < n; i += blockDim.x) unsorted |= id_s[i + 1] < id_s[i];
+  for (int i = tid; i + 1 < n; i += 256) unsorted |= id_s[i + 1] < id_s[i];
   const bool sorted = !__syncthreads_or(unsorted);
   if (sorted && tid < 2) {  // lower_bound of id_lo (thread 0) and id_hi (thread 1)
     const int64_t key = tid ? id_hi : id_lo;
@@ -675,7 +476,7 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
     return true;
   };
   double my_max = -__builtin_inf();
-  for (int i = a + tid; i < b; i += blockDim.x) {
+  for (int i = a + tid; i < b; i += 256) {
     if (!mine(i)) continue;
     const int32_t id = id_s[i];
     double leaf;
@@ -704,7 +505,7 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
   }
   __syncthreads();  // every occurrence has read its old count; the leaves are in LDS
   if (count && exp_counter && !vals)
-    for (int i = a + tid; i < b; i += blockDim.x) {
+    for (int i = a + tid; i < b; i += 256) {
       if (!mine(i)) continue;
       const int32_t id = id_s[i];
       if (first_occ(i, id)) exp_counter[id] += 1.0;
@@ -713,7 +514,7 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
   int lvl = 0;
   for (int lo = sub / 2; lo >= 1; lo /= 2) {
     ++lvl;
-    for (int k = lo + tid; k < 2 * lo; k += blockDim.x) {
+    for (int k = lo + tid; k < 2 * lo; k += 256) {
       ts[k] = ts[2 * k] + ts[2 * k + 1];
       tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
       const int64_t g = (leaf0 >> lvl) + (k - lo);
@@ -736,17 +537,17 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
   if (tid == 0) {
     __builtin_amdgcn_s_waitcnt(0);
     *last_s = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              (unsigned long long)(gridDim.x - 1);
+              (unsigned long long)(nroot - 1);
   }
   __syncthreads();
   if (!*last_s) return;
-  for (int64_t k = nroot + tid; k < 2 * nroot; k += blockDim.x) {
+  for (int64_t k = nroot + tid; k < 2 * nroot; k += 256) {
     ts[k] = __hip_atomic_load(sum_tree + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tm[k] = __hip_atomic_load(min_tree + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   for (int64_t lo = nroot / 2; lo >= 1; lo /= 2) {
-    for (int64_t k = lo + tid; k < 2 * lo; k += blockDim.x) {
+    for (int64_t k = lo + tid; k < 2 * lo; k += 256) {
       ts[k] = ts[2 * k] + ts[2 * k + 1];
       tm[k] = tree_min(tm[2 * k], tm[2 * k + 1]);
       sum_tree[k] = ts[k];
@@ -979,9 +780,17 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
       const char* e = std::getenv("CACTO_PER_DEEP_TOP");  // 0: the round-4 sampler (A/B)
       return !(e && e[0] == '0');
     }();
-    if (deep)
-      hipLaunchKernelGGL(k_per_sample_mw, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sum_tree_d, min_tree_d, capacity,
-                         max_idx, beta, uniforms_d, B, idx_d, is_w_d, shards_d, n_shards);
+    // CACTO_PER_TOP=4096: the fused loop's 4,096-node form standalone (its parity tests; read once)
+    static const bool top4k = [] {
+      const char* e = std::getenv("CACTO_PER_TOP");
+      return e && std::atoi(e) == 4096;
+    }();
+    const PerSampleArgs sa{sum_tree_d, min_tree_d, capacity, max_idx, beta, uniforms_d, B, idx_d, is_w_d,
+                           shards_d, n_shards, nullptr};
+    if (deep && top4k)
+      hipLaunchKernelGGL(k_per_sample_runs, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sa);
+    else if (deep)
+      hipLaunchKernelGGL(k_per_sample_mw, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sa);
     else
       hipLaunchKernelGGL((k_per_sample<1, 1>), dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sum_tree_d, min_tree_d, capacity,
                          max_idx, beta, uniforms_d, B, idx_d, is_w_d, nullptr, shards_d, n_shards, per_prio());
@@ -997,6 +806,23 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }
+
+}  // namespace
+
+// The fused PER loop's first sample (learn_kernels.hip): k_per_sample_runs, recording the per-subtree
+// runs (runs_d: 2 cap / PER_RUN_SUB ints, PER_RUN_EMPTY / 0 on entry).
+int cacto_per_sample_runs_launch(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
+                                 double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
+                                 int32_t* runs_d, hipStream_t st) {
+  using namespace cacto;
+  const PerSampleArgs sa{sum_tree_d, min_tree_d, capacity, max_idx, beta, uniforms_d, B, idx_d, is_w_d,
+                         nullptr, 0, runs_d};
+  hipLaunchKernelGGL(k_per_sample_runs, dim3((B + 255) / 256), dim3(256), 0, st, sa);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
+}
+
+namespace {
 
 // count = 1: exp_counter += 1 (the sampler's count, deferred) applied inside the priority update;
 // skip_d: an int status that, when set, leaves everything unchanged (the ReLO rule's error flag)

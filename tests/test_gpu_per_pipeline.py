@@ -12,7 +12,16 @@ its own child process:
     wait-value pair instead of an event;
   * CACTO_PER_FUSED = 0 / 1: the priority update (with the sampler's deferred exp_counter += 1) as
     the one-launch subtree kernel k_per_update_sub, or the round-3 chain k_per_count ->
-    k_per_leaves_mw -> k_per_subtrees -> k_per_top.
+    k_per_leaves_mw -> k_per_subtrees -> k_per_top;
+  * CACTO_PER_STREAM = 0 / 1: (with DEVWAIT >= 1) the priority update of update t and the sample of
+    t + 1 on a third stream beside the critic's GEMM and Adam, with a five-buffer index ring, or on
+    the critic stream;
+  * CACTO_PER_DEEP_TOP = 0 / 1: the multi-workgroup sampler of round 4 or the 8,192-node one;
+  * CACTO_PER_OVERLAP = 0 / 1: (with DEVWAIT >= 1, the default) the priority update of update t
+    inside the critic GEMM's launch (k_wgrad_big_per: 256-leaf subtrees, the runs recorded by the
+    sampler) and the sample of t + 1 inside the critic Adam's (k_adam_sample: 4,096-node top).
+The 4,096-node sampler is also checked standalone against the oracle at every descent split
+(CACTO_PER_TOP=4096, its own child).
 K = 6 and 7 (even / odd: the critic ends in the caller's buffer or a workspace copy), and the
 non-PER loop (DI, B = 1024, K = 7) against sequential updates under the same knobs. Every child
 also writes the trees after a priority update with an unsorted index list holding duplicates
@@ -124,20 +133,79 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = {}
-    for every2, fused, devwait, signal in (("0", "1", "0", "0"), ("1", "1", "0", "0"), ("1", "0", "0", "0"),
-                                           ("0", "1", "1", "0"), ("0", "1", "2", "0"), ("0", "1", "1", "1")):
+    for every2, fused, devwait, signal, pstream, deep, overlap in (
+            ("0", "1", "0", "0", "1", "1", "1"), ("1", "1", "0", "0", "1", "1", "1"), ("1", "0", "0", "0", "1", "0", "1"),
+            ("0", "1", "1", "0", "1", "1", "1"), ("0", "1", "1", "0", "1", "1", "0"), ("0", "1", "1", "0", "0", "0", "0"),
+            ("0", "0", "1", "0", "1", "1", "0"), ("0", "1", "2", "0", "1", "1", "1"), ("0", "1", "1", "1", "1", "1", "1")):
         env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait,
-                   CACTO_PIPE_SIGNAL=signal)
+                   CACTO_PIPE_SIGNAL=signal, CACTO_PER_STREAM=pstream, CACTO_PER_DEEP_TOP=deep,
+                   CACTO_PER_OVERLAP=overlap)
         r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
-        res[(every2, fused, devwait, signal)] = json.loads(line[len("RESULT "):])
+        res[(every2, fused, devwait, signal, pstream, deep, overlap)] = json.loads(line[len("RESULT "):])
     for key, r in res.items():
         assert r["K6_equal"] and r["K7_equal"] and r["di_equal"] and r["latch"] == 0, key
     for field in ("K6_hash", "K7_hash", "unsorted_hash"):
         assert len({r[field] for r in res.values()}) == 1, field
 
 
+def _sampler_child():
+    """k_per_sample_runs' 4,096-node form (CACTO_PER_TOP=4096) at every descent split, against the oracle."""
+    import torch
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import buffer as obuf
+    from cacto_amd import _lib as L
+    from cacto_amd.system import dptr, stream
+    ok = True
+    for cap in (2, 1024, 4096, 8192, 1 << 16, 1 << 17, 1 << 20):
+        rng = np.random.default_rng(cap + 1)
+        leaves = rng.uniform(0.01, 2.0, size=cap) ** 0.6
+        leaves[rng.integers(0, cap, size=max(1, cap // 7))] = 0.0
+        st, mt = np.zeros(2 * cap), np.full(2 * cap, np.inf)
+        st[cap:], mt[cap:] = leaves, np.where(leaves > 0, leaves, np.inf)
+        lo = cap // 2
+        while lo >= 1:
+            k = np.arange(lo, 2 * lo)
+            st[k] = st[2 * k] + st[2 * k + 1]
+            mt[k] = np.where(mt[2 * k + 1] < mt[2 * k], mt[2 * k + 1], mt[2 * k])
+            lo //= 2
+        o = obuf.PrioritizedReplayBuffer(cap, 1, 0.6, 0.6, 1e-2, 0.95, 0)
+        o.it_sum.value, o.it_min.value = list(st), list(mt)
+        max_idx = cap if cap <= 8192 else cap - 5
+        o.N, o.next_idx, o.full = cap, max_idx % cap, max_idx == cap
+        B = 1000
+        o.B = B
+        u = rng.uniform(size=B)
+        oidx = o.sample_proportional(list(u))
+        ow = o.sample_weights(oidx)
+        sd, md, ud = (torch.as_tensor(x, device="cuda") for x in (st, mt, u))
+        idx = torch.empty(B, dtype=torch.int32, device="cuda")
+        w = torch.empty(B, dtype=torch.float32, device="cuda")
+        L.lib().call("cacto_per_sample", dptr(sd), dptr(md), cap, max_idx, 0.6, dptr(ud), B, dptr(idx), dptr(w),
+                     None, stream())
+        ok &= bool(np.array_equal(idx.cpu().numpy(), oidx))
+        ok &= bool(np.allclose(w.cpu().numpy(), ow.astype(np.float32), rtol=1e-6))
+    print("RESULT " + json.dumps({"ok": ok}), flush=True)
+
+
+@pytest.mark.gpu
+def test_sampler_4096_top_every_depth():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, CACTO_PER_TOP="4096")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "sampler"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    assert json.loads(line[len("RESULT "):])["ok"]
+
+
 if __name__ == "__main__":
-    _child()
+    if len(sys.argv) > 1 and sys.argv[1] == "sampler":
+        _sampler_child()
+    else:
+        _child()

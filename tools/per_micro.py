@@ -3,10 +3,12 @@ timed per call with HIP events on the library's stream. Prints one line per phas
 
     python tools/per_micro.py [B] [iters]
 """
+import os
 import sys
 
-import numpy as np
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 from cacto_amd import _lib as L
 from cacto_amd.system import dptr, stream
