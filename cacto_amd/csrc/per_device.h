@@ -106,8 +106,23 @@ struct PerSampleArgs {
 // of three levels until at most five remain, then per_tail (one more memory latency for the
 // remaining levels and the leaf value). For the 2^16-row buffer: two dependent global latencies per
 // sample at TOPN = 8192 (four levels below the top) and at 4096 (five).
+#ifdef CACTO_STAMPS
+// diagnostic builds: s_memtime of thread 0 of each sampler workgroup at its phase boundaries (start,
+// staged top + scalars, LDS descent done, tail done, end), [blk][8]; read by cacto_debug_per_stamps
+__device__ unsigned long long g_per_stamps[64 * 8];
+#define PER_STAMP(blk, k)                                                                        \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && (blk) < 64) g_per_stamps[(blk) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PER_STAMP(blk, k) \
+  do {                    \
+  } while (0)
+#endif
+
 template <int TOPN>
 __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a, double* top_s, double* scal_s) {
+  PER_STAMP(blk, 0);
   const int64_t cap = a.cap, max_idx = a.max_idx;
   const double* __restrict__ sum_tree = a.sum_tree;
   const int B = a.B;
@@ -115,7 +130,20 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
   const int tid = threadIdx.x;
   const int i = blk * 256 + tid;
   const double u = i < B ? a.uniforms[i] : 0.0;  // in flight with the loads below
-  double term = 0.0, root_sum = 0.0, root_min = 0.0;
+  // the staging loads first (ntop / 2 double2 pairs over 256 threads), then, while they are in
+  // flight: wave 0 walks prefix_reduce's path (lane k loads its k-th term) and wave 1 loads the roots
+  // and forms the IS-weight normaliser (a pow) beside wave 0's sum
+  constexpr int PAIRS = TOPN / 2 / 256;
+  double2 st[PAIRS];
+  {
+    const double2* src = reinterpret_cast<const double2*>(sum_tree);
+#pragma unroll
+    for (int r = 0; r < PAIRS; ++r) {
+      const int64_t q = tid + r * 256;
+      st[r] = 2 * q < ntop ? src[q] : make_double2(0.0, 0.0);
+    }
+  }
+  double term = 0.0;
   bool has_term = false;
   if (tid < 64) {
     const int lane = tid;
@@ -137,33 +165,34 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
       }
     }
     has_term = at >= 0;
+    PER_STAMP(blk, 5);
     if (has_term) term = sum_tree[at];
-    if (lane == 63) {
-      root_sum = sum_tree[1];
-      if (!a.shards) root_min = a.min_tree[1];
+  } else if (tid == 64) {
+    const double root_sum = sum_tree[1];
+    scal_s[1] = root_sum;
+    if (a.shards) {  // data parallel: IS weights over the union of the shards (see k_per_sample)
+      double n_all = 0.0, ratio_min = __builtin_inf();
+      for (int g = 0; g < a.n_shards; ++g) {
+        n_all += a.shards[3 * g + 2];
+        ratio_min = tree_min(ratio_min, a.shards[3 * g + 1] / a.shards[3 * g + 0]);
+      }
+      scal_s[3] = n_all / a.n_shards;
+      scal_s[2] = pow(ratio_min * (n_all / a.n_shards), -a.beta);
+    } else {
+      const double p_min = a.min_tree[1] / root_sum;
+      scal_s[3] = (double)max_idx;
+      scal_s[2] = pow(p_min * (double)max_idx, -a.beta);
     }
   }
-  // the staging: ntop / 2 double2 pairs over 256 threads, all loads issued before the LDS writes
-  {
-    constexpr int PAIRS = TOPN / 2 / 256;
-    const double2* src = reinterpret_cast<const double2*>(sum_tree);
-    double2 st[PAIRS];
 #pragma unroll
-    for (int r = 0; r < PAIRS; ++r) {
-      const int64_t q = tid + r * 256;
-      st[r] = 2 * q < ntop ? src[q] : make_double2(0.0, 0.0);
-    }
-#pragma unroll
-    for (int r = 0; r < PAIRS; ++r) {
-      const int64_t q = tid + r * 256;
-      if (2 * q < ntop) reinterpret_cast<double2*>(top_s)[q] = st[r];
-    }
+  for (int r = 0; r < PAIRS; ++r) {
+    const int64_t q = tid + r * 256;
+    if (2 * q < ntop) reinterpret_cast<double2*>(top_s)[q] = st[r];
   }
+  PER_STAMP(blk, 6);
   if (tid < 64) {
     // the right-nested sum, deepest term first, as prefix_reduce combines them
     const unsigned long long mask = __ballot(has_term);
-    root_sum = __shfl(root_sum, 63);
-    root_min = __shfl(root_min, 63);
     double r = 0.0;
     bool have = false;
     for (int k = 63; k >= 0; --k)
@@ -175,25 +204,11 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
         r = have ? tk + r : tk;
         have = true;
       }
-    if (tid == 0) {
-      scal_s[0] = r / B;  // segment
-      scal_s[1] = root_sum;
-      if (a.shards) {  // data parallel: IS weights over the union of the shards (see k_per_sample)
-        double n_all = 0.0, ratio_min = __builtin_inf();
-        for (int g = 0; g < a.n_shards; ++g) {
-          n_all += a.shards[3 * g + 2];
-          ratio_min = tree_min(ratio_min, a.shards[3 * g + 1] / a.shards[3 * g + 0]);
-        }
-        scal_s[3] = n_all / a.n_shards;
-        scal_s[2] = pow(ratio_min * scal_s[3], -a.beta);
-      } else {
-        const double p_min = root_min / root_sum;
-        scal_s[3] = (double)max_idx;
-        scal_s[2] = pow(p_min * scal_s[3], -a.beta);
-      }
-    }
+    if (tid == 0) scal_s[0] = r / B;  // segment
+    PER_STAMP(blk, 7);
   }
   __syncthreads();
+  PER_STAMP(blk, 1);
   if (i >= B) return;
   const double seg = scal_s[0];
   double p = u * seg + i * seg;
@@ -207,6 +222,7 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
       nd = 2 * nd + 1;
     }
   }
+  PER_STAMP(blk, 2);
   // levels below the staged top, three at a time, until at most five remain
   int rem = 0;
   for (int64_t s = nd; s < cap; s *= 2) ++rem;  // levels from nd down to the leaves
@@ -249,9 +265,11 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
     case 1: per_tail<1>(sum_tree, nd, p, leaf, val); break;
     default: leaf = nd; val = sum_tree[nd]; break;  // capacity 1: the root is the leaf
   }
+  PER_STAMP(blk, 3);
   const int32_t id = (int32_t)(leaf - cap);
   a.idx_out[i] = id;
   a.w_out[i] = (float)(pow(val / scal_s[1] * scal_s[3], -a.beta) / scal_s[2]);
+  PER_STAMP(blk, 4);
   if (a.runs) {
     const int64_t nroot = cap / PER_RUN_SUB, s = id / PER_RUN_SUB;
     __hip_atomic_fetch_min(a.runs + s, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -809,6 +809,14 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
 
 }  // namespace
 
+#ifdef CACTO_STAMPS
+extern "C" int cacto_debug_per_stamps(unsigned long long* out_h) {  // [64][8], this TU's samplers
+  CACTO_CHECK_HIP(hipDeviceSynchronize());
+  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(cacto::g_per_stamps), sizeof(unsigned long long) * 64 * 8));
+  return CACTO_OK;
+}
+#endif
+
 // The fused PER loop's first sample (learn_kernels.hip): k_per_sample_runs, recording the per-subtree
 // runs (runs_d: 2 cap / PER_RUN_SUB ints, PER_RUN_EMPTY / 0 on entry).
 int cacto_per_sample_runs_launch(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
