@@ -143,30 +143,30 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
       st[r] = 2 * q < ntop ? src[q] : make_double2(0.0, 0.0);
     }
   }
+  // lane k's term in closed form (cap = 2^L; [0, cap - 1] halves at every level, so the path to
+  // `end` is end's bits from the top): the walk stops at depth d* = L - (trailing ones of end, at
+  // most L) with the node itself as the last term; above it, a step right at depth k (bit L - 1 - k
+  // of end set) adds that node's left child
   double term = 0.0;
   bool has_term = false;
+  int dstar = -1;  // deepest term's depth (no term when end < 0)
+  const int64_t end = max_idx - 2;
+  if (end >= 0) {
+    const int L = 63 - __builtin_clzll((unsigned long long)cap);
+    const int ones = __builtin_ctzll(~(unsigned long long)end);
+    dstar = L - (ones < L ? ones : L);
+  }
   if (tid < 64) {
-    const int lane = tid;
-    const int64_t end = max_idx - 2;
-    int64_t node = 1, ns = 0, ne = cap - 1, at = -1;
-    for (int k = 0; k <= lane && at < 0; ++k) {
-      if (end == ne) {
-        if (k == lane) at = node;
-        break;
-      }
-      const int64_t mid = (ns + ne) / 2;
-      if (end <= mid) {
-        node = 2 * node;
-        ne = mid;
-      } else {
-        if (k == lane) at = 2 * node;
-        node = 2 * node + 1;
-        ns = mid + 1;
-      }
+    const int k = tid;
+    if (end >= 0) {
+      const int L = 63 - __builtin_clzll((unsigned long long)cap);
+      int64_t at = -1;
+      if (k == dstar) at = ((int64_t)1 << k) | (end >> (L - k));
+      else if (k < dstar && ((end >> (L - 1 - k)) & 1)) at = (((int64_t)1 << k) | (end >> (L - k))) * 2;
+      has_term = at >= 0;
+      PER_STAMP(blk, 5);
+      if (has_term) term = sum_tree[at];
     }
-    has_term = at >= 0;
-    PER_STAMP(blk, 5);
-    if (has_term) term = sum_tree[at];
   } else if (tid == 64) {
     const double root_sum = sum_tree[1];
     scal_s[1] = root_sum;
@@ -195,7 +195,7 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
     const unsigned long long mask = __ballot(has_term);
     double r = 0.0;
     bool have = false;
-    for (int k = 63; k >= 0; --k)
+    for (int k = dstar; k >= 0; --k)
       if ((mask >> k) & 1ull) {  // k is uniform: read the lane's term into scalar registers
         const long long tb = __double_as_longlong(term);
         const int lo = __builtin_amdgcn_readlane((int)(tb & 0xffffffffll), k);
@@ -213,7 +213,24 @@ __device__ __forceinline__ void per_sample_body(int blk, const PerSampleArgs& a,
   const double seg = scal_s[0];
   double p = u * seg + i * seg;
   int64_t nd = 1;
-  while (2 * nd < ntop) {
+  while (4 * nd < ntop) {  // two staged levels per LDS latency: the left child and both left grandchildren
+    const double a0 = top_s[2 * nd], b0 = top_s[4 * nd], b1 = top_s[4 * nd + 2];
+    int64_t m;
+    if (a0 > p) {
+      m = 2 * nd;
+    } else {
+      p -= a0;
+      m = 2 * nd + 1;
+    }
+    const double bl = (m & 1) ? b1 : b0;
+    if (bl > p) {
+      nd = 2 * m;
+    } else {
+      p -= bl;
+      nd = 2 * m + 1;
+    }
+  }
+  if (2 * nd < ntop) {
     const double left = top_s[2 * nd];
     if (left > p) {
       nd = 2 * nd;
