@@ -55,6 +55,13 @@ struct ChainScalars {
   // its critic pass at s', until *wait_p >= wait_v (the critic's Adam of the same update has run)
   const unsigned long long* wait_p;
   unsigned long long wait_v;
+  // 1 (CACTO_PIPE_DEVWAIT=3): that wait with a relaxed load and no fence — the Adam wrote the critic
+  // through to memory at agent scope and published after its stores completed, and no L2 holds a
+  // line of the buffer from before (kernel starts invalidate; nothing reads it in between)
+  int wait_relaxed;
+  // 1 (the PER loops): that wait at the chain's start, before it gathers the sampled rows (the
+  // sample of the update precedes the critic's Adam on the other stream)
+  int wait_at_start;
   // 1: the 16-sample tiles dealt so that the tiles of one 256-row GEMM chunk run on the XCD that
   // k_wgrad_big runs that chunk on (chain_tile_of)
   int xcd_tiles;
@@ -562,8 +569,12 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   CSTAMP(3);
   if (L.wave == 0) fill_input_tile(p, stn, XS, L);
   if (cs.wait_p) {  // pipeline: the critic this pass reads is written by the other stream's Adam
-    if (L.tid == 0) pipe_wait<true>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
-    __threadfence();  // acquire at agent scope: no stale L1 / L2 line of that critic buffer
+    if (cs.wait_relaxed) {
+      if (L.tid == 0) pipe_wait<false>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
+    } else {
+      if (L.tid == 0) pipe_wait<true>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
+      __threadfence();  // acquire at agent scope: no stale L1 / L2 line of that critic buffer
+    }
   }
   __syncthreads();
   // critic (already updated) at s': V and dV/dx0 (NeuralNetwork.py:190-195)
@@ -646,7 +657,13 @@ __global__ void __launch_bounds__(CACTO_THREADS) __attribute__((amdgpu_waves_per
                  const double* __restrict__ storage, const int32_t* __restrict__ idx, int B, GradBufs gb,
                  int32_t* __restrict__ step) {
   __shared__ ActorLds S;
-  actor_chain<NJ>(S, chain_tile_of(blockIdx.x, gridDim.x, cs.xcd_tiles), sdp, Ac, C, cs, storage, idx, B, gb, step);
+  ChainScalars c = cs;
+  if (cs.wait_p && cs.wait_at_start) {
+    if (threadIdx.x == 0) pipe_wait<false>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
+    __syncthreads();
+    c.wait_p = nullptr;
+  }
+  actor_chain<NJ>(S, chain_tile_of(blockIdx.x, gridDim.x, cs.xcd_tiles), sdp, Ac, C, c, storage, idx, B, gb, step);
 }
 
 // The critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the
@@ -1082,16 +1099,25 @@ __device__ __forceinline__ void write_packed_w(float4* pk4, const NetTopo& t, in
      (o & 3)] = val;
 }
 
-__device__ __forceinline__ void write_packed(float4* pk4, const NetTopo& t, int p, float val) {
+// thru: the store written through to memory at agent scope (a relaxed atomic store), for a reader
+// on another stream that orders itself by a device-side flag instead of a kernel boundary
+__device__ __forceinline__ void store_f(float* p, float v, bool thru) {
+  if (thru) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+__device__ __forceinline__ void write_packed(float4* pk4, const NetTopo& t, int p, float val, bool thru = false) {
   float* pk = reinterpret_cast<float*>(pk4);
   int l = t.L - 1;
   while (t.woff[l] > p) --l;
   if (p >= t.boff[l]) return;
   const int local = p - t.woff[l];
   const int i = local / t.out[l], o = local - (local / t.out[l]) * t.out[l];
-  pk[((size_t)(t.pkoff[l] + (o >> 4) * t.KT[l] + (i >> 4)) * 64 + ((i & 15) >> 2) * 16 + (o & 15)) * 4 + (i & 3)] = val;
-  pk[((size_t)(t.blocks + t.pkoff[l] + (i >> 4) * t.OT[l] + (o >> 4)) * 64 + ((o & 15) >> 2) * 16 + (i & 15)) * 4 +
-     (o & 3)] = val;
+  store_f(pk + ((size_t)(t.pkoff[l] + (o >> 4) * t.KT[l] + (i >> 4)) * 64 + ((i & 15) >> 2) * 16 + (o & 15)) * 4 + (i & 3),
+          val, thru);
+  store_f(pk + ((size_t)(t.blocks + t.pkoff[l] + (i >> 4) * t.OT[l] + (o >> 4)) * 64 + ((o & 15) >> 2) * 16 + (i & 15)) * 4 +
+              (o & 3),
+          val, thru);
 }
 
 struct AdamScalars {
@@ -1142,12 +1168,29 @@ __device__ __forceinline__ void adam_publish(unsigned long long* sig_p, unsigned
 }
 
 // One parameter per thread, workgroup blk (NCH > 0).
+// The same publication for write-through stores (CACTO_PIPE_DEVWAIT=3): every thread's stores have
+// completed (waitcnt) before its workgroup counts itself; no fence, no L2 write-back.
+__device__ __forceinline__ void adam_publish_thru(unsigned long long* sig_p, unsigned long long sig_v) {
+  if (!sig_p) return;
+  __shared__ int last;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(sig_p + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned long long)(gridDim.x - 1);
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __hip_atomic_store(sig_p + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sig_p + 2, sig_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int NCH>
 __device__ __forceinline__ void adam_nch_body(const int blk, const float* __restrict__ slab, int nch, const NetTopo& t,
                                               const float* src, float* netbuf, float4* packed, float* __restrict__ m,
                                               float* __restrict__ v, const int32_t* __restrict__ step, const AdamArgs& a,
                                               float* target, float4* target_packed, const unsigned long long* wait_p,
-                                              unsigned long long wait_v) {
+                                              unsigned long long wait_v, bool thru = false) {
   const int p0 = blk * 256 + threadIdx.x;
   float q[NCH], mm = 0.f, vv = 0.f, th0 = 0.f, tg0 = 0.f;
   const int pc = min(p0, t.params - 1);
@@ -1169,8 +1212,8 @@ __device__ __forceinline__ void adam_nch_body(const int blk, const float* __rest
     const float th = fsub(th0, fdiv(fmul(mm, s.alpha), fadd(__fsqrt_rn(vv), s.eps)));
     m[p0] = mm;
     v[p0] = vv;
-    netbuf[p0] = th;
-    write_packed(packed, t, p0, th);
+    store_f(netbuf + p0, th, thru);
+    write_packed(packed, t, p0, th, thru);
     if (a.soft) {
       const float tg = fadd(fmul(th, s.tau), fmul(tg0, s.omt));
       target[p0] = tg;
@@ -1205,11 +1248,12 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
                                               const int32_t* __restrict__ step, AdamArgs a, float* target,
                                               float4* target_packed, const unsigned long long* wait_p,
                                               unsigned long long wait_v, unsigned long long* sig_p,
-                                              unsigned long long sig_v) {
+                                              unsigned long long sig_v, int thru) {
   if constexpr (NCH > 0) {
     adam_nch_body<NCH>(blockIdx.x, slab, nch, t, src, netbuf, packed, m, v, step, a, target, target_packed, wait_p,
-                       wait_v);
-    adam_publish(sig_p, sig_v);
+                       wait_v, thru != 0);
+    if (thru) adam_publish_thru(sig_p, sig_v);
+    else adam_publish(sig_p, sig_v);
     return;
   }
   const int it = step[a.which];  // = Keras iterations + 1
@@ -1244,15 +1288,16 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
     const float th = fsub(src[p], fdiv(fmul(mm, alpha), fadd(__fsqrt_rn(vv), eps)));
     m[p] = mm;
     v[p] = vv;
-    netbuf[p] = th;
-    write_packed(packed, t, p, th);
+    store_f(netbuf + p, th, thru != 0);
+    write_packed(packed, t, p, th, thru != 0);
     if (a.soft) {
       const float tg = fadd(fmul(th, tau), fmul(target[p], omt));
       target[p] = tg;
       write_packed(target_packed, t, p, tg);
     }
   }
-  adam_publish(sig_p, sig_v);
+  if (thru) adam_publish_thru(sig_p, sig_v);
+  else adam_publish(sig_p, sig_v);
 }
 
 __global__ void __launch_bounds__(256) k_soft(NetTopo t, const float* __restrict__ src, float* target,
@@ -1840,6 +1885,8 @@ ChainScalars chain_scalars(const cacto_update_cfg* cfg, int B) {
   cs.want_vt = cfg->want_target_V;
   cs.wait_p = nullptr;
   cs.wait_v = 0;
+  cs.wait_relaxed = 0;
+  cs.wait_at_start = 0;
   // CACTO_CHAIN_XCD=0 keeps the tiles in block order (A/B; read once)
   static const bool xcd_env = [] {
     const char* e = std::getenv("CACTO_CHAIN_XCD");
@@ -1901,12 +1948,15 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
 
 int launch_actor_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                        const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
-                       const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0) {
+                       const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0,
+                       int wait_relaxed = 0, int wait_at_start = 0) {
   NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
   NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
   ChainScalars cs = chain_scalars(cfg, B);
   cs.wait_p = wait_p;
   cs.wait_v = wait_v;
+  cs.wait_relaxed = wait_relaxed;
+  cs.wait_at_start = wait_at_start;
   return dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st);
 }
 
@@ -1923,7 +1973,7 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
                 const float* slab, int nch, int soft, hipStream_t st, const float* src = nullptr,
                 const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0,
                 unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0,
-                const PerSampleArgs* sample = nullptr) {
+                const PerSampleArgs* sample = nullptr, int thru = 0) {
   const NetTopo& t = topo(sys, which);
   float* nb = which == CACTO_NET_CRITIC ? nets->critic_d : nets->actor_d;
   float* m = which == CACTO_NET_CRITIC ? nets->critic_m_d : nets->actor_m_d;
@@ -1936,7 +1986,7 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
   const int full = (t.params + 255) / 256;
   auto go = [&](auto kern, int grid) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, slab, nch, t, s0, nb, pk, m, v, nets->step_d, aa,
-                       nets->target_d, tpk, wait_p, wait_v, sig_p, sig_v);
+                       nets->target_d, tpk, wait_p, wait_v, sig_p, sig_v, thru);
   };
   if (sample) {  // the PER loop's fused form (the caller checked nch <= 64)
     if (sig_p || nch > 64) {
@@ -2026,7 +2076,7 @@ int launch_wgrad_adam(const cacto_sys* sys, int mode, const AdamNet& n0, const A
 int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const Workspace& w,
                      hipStream_t st, const float* src, float* nb, const unsigned long long* wait_p = nullptr,
                      unsigned long long wait_v = 0, unsigned long long* sig_p = nullptr, unsigned long long sig_v = 0,
-                     const PerRunArgs* per_run = nullptr, const PerSampleArgs* sample = nullptr) {
+                     const PerRunArgs* per_run = nullptr, const PerSampleArgs* sample = nullptr, int thru = 0) {
   const int soft = cfg->MC ? 0 : 1;
   if (fused_adam(w.Bp)) return launch_wgrad_adam(sys, 0, critic_adam_net(sys, nets, cfg, w, soft, src, nb), nullptr,
                                                  nets->step_d, st);
@@ -2037,7 +2087,7 @@ int critic_step_tail(const cacto_sys* sys, const cacto_nets* nets, const cacto_u
   cacto_nets dst = *nets;
   dst.critic_d = nb;
   return launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, w.slab, nch, soft, st, src, wait_p, wait_v, sig_p, sig_v,
-                     sample);
+                     sample, thru);
 }
 
 // CACTO_PER_OVERLAP (default 1): the pipelined PER loop's priority update and next sample share the
@@ -2522,24 +2572,28 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   // actor chains on the device, and the critic's Adam(t) polls it (pipe_wait) before overwriting the
   // buffer actor chain(t-3) read; the PER index ring has four buffers, so the sampler of update t
   // overwrites the one actor chain(t-4) read, which Adam(t-1)'s wait covers. Read once; A/B.
-  // default 1 (measured r05, 1 MI355X, updates/s: DI B = 4096 12.3 k -> 12.7 k, car_park PER
-  // B = 4096 9.88 k -> 9.98 k, manipulator B = 8192 7.70 k -> 7.68 k); CACTO_PIPE_DEVWAIT=0 restores
-  // the queue markers
+  // 1 measured r05 (1 MI355X, updates/s): DI B = 4096 12.3 k -> 12.7 k, car_park PER B = 4096 9.88 k ->
+  // 9.98 k, manipulator B = 8192 7.70 k -> 7.68 k; the default is 3 (below); CACTO_PIPE_DEVWAIT=0
+  // restores the queue markers
   static const int devwait_env = [] {
     const char* e = std::getenv("CACTO_PIPE_DEVWAIT");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 3;
   }();
   const bool devwait = devwait_env >= 1;
   // ... and the side stream's wait on the critic's Adam too (k_adam's last workgroup publishes, the
   // actor chain polls just before its critic pass at s' — its actor forward, dynamics and d r / d a
   // run first), where that cannot starve the critic stream of CUs: 16-sample actor tiles (the q4
   // chains take no wait), at most one actor workgroup per CU (a CU holding one actor workgroup still
-  // fits a critic chain, GEMM or Adam workgroup beside it, so the critic stream always progresses),
-  // and no PER (the actor chain gathers the sampled rows at its start).
+  // fits a critic chain, GEMM or Adam workgroup beside it, so the critic stream always progresses);
+  // with 2, no PER (the actor chain gathers the sampled rows at its start).
   // (CACTO_PIPE_DEVWAIT=2; measured r05: DI B = 4096 10.8 k -> 7.5 k updates/s — the acquire side's
   // agent-scope L2 invalidations and the Adam's releases cost more than the queue marker they replace)
-  const bool devwait_actor = devwait_env >= 2 && !per && chain_tile(w.Bp) == CACTO_TILE &&
+  // CACTO_PIPE_DEVWAIT=3 (default): that wait without fences — the critic's Adam writes the weights
+  // through to memory at agent scope and publishes after its stores completed, the chain polls
+  // relaxed; with PER too, the chain polling at its start (before it gathers the sampled rows)
+  const bool devwait_actor = devwait_env >= 2 && (!per || devwait_env >= 3) && chain_tile(w.Bp) == CACTO_TILE &&
                              w.Bp / CACTO_TILE <= cu_count();
+  const int thru = devwait_actor && devwait_env >= 3 ? 1 : 0;
   unsigned long long* const sig = ms->pipe_sig;
   // CACTO_PIPE_SIGNAL=1: the side stream's wait on the critic's Adam as a stream write / wait-value
   // pair on a signal-memory word instead of an event record / wait (A/B; read once)
@@ -2631,7 +2685,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     }
     if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d, dw ? sig : nullptr, base + t - 2,
                                  devwait_actor ? sig : nullptr, base + t + 1, ovl ? &pra : nullptr,
-                                 ovl && t + 1 < K ? &psa : nullptr))
+                                 ovl && t + 1 < K ? &psa : nullptr, thru))
       return e;
     *cbuf = (t + 1) % 3;
     if (streamval) CACTO_CHECK_HIP(hipStreamWriteValue64(st, ms->pipe_wsig, base + t + 1, 0));
@@ -2643,7 +2697,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     else if (!devwait_actor)
       CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side, devwait_actor ? sig + 2 : nullptr,
-                                   base + t + 1))
+                                   base + t + 1, thru, per ? 1 : 0))
       return e;
     if (int e = actor_step_tail(sys, nets, cfg, w, side, devwait ? sig : nullptr, base + t + 1)) return e;
     if (devwait) {

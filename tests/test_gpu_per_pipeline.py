@@ -7,7 +7,8 @@ its own child process:
   * CACTO_PIPE_DEVWAIT = 1: that ordering on the device (the actor's GEMM publishes finished
     chains, the critic's Adam polls) instead of queue markers, with a four-buffer PER index ring;
     = 2: also the actor chain's wait on the critic's Adam (the critic's Adam publishes, the chain
-    polls before its critic pass; not with PER);
+    polls before its critic pass; not with PER); = 3: that wait without fences (the Adam writes the
+    critic through to memory at agent scope, the chain polls relaxed);
   * CACTO_PIPE_SIGNAL = 1: the side stream's wait on the critic's Adam as a stream write-value /
     wait-value pair instead of an event;
   * CACTO_PER_FUSED = 0 / 1: the priority update (with the sampler's deferred exp_counter += 1) as
@@ -136,7 +137,8 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
     for every2, fused, devwait, signal, pstream, deep, overlap in (
             ("0", "1", "0", "0", "1", "1", "1"), ("1", "1", "0", "0", "1", "1", "1"), ("1", "0", "0", "0", "1", "0", "1"),
             ("0", "1", "1", "0", "1", "1", "1"), ("0", "1", "1", "0", "1", "1", "0"), ("0", "1", "1", "0", "0", "0", "0"),
-            ("0", "0", "1", "0", "1", "1", "0"), ("0", "1", "2", "0", "1", "1", "1"), ("0", "1", "1", "1", "1", "1", "1")):
+            ("0", "0", "1", "0", "1", "1", "0"), ("0", "1", "2", "0", "1", "1", "1"), ("0", "1", "3", "0", "1", "1", "1"),
+            ("0", "1", "1", "1", "1", "1", "1")):
         env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait,
                    CACTO_PIPE_SIGNAL=signal, CACTO_PER_STREAM=pstream, CACTO_PER_DEEP_TOP=deep,
                    CACTO_PER_OVERLAP=overlap)
