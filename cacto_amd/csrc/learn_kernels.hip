@@ -62,6 +62,10 @@ struct ChainScalars {
   // 1 (the PER loops): that wait at the chain's start, before it gathers the sampled rows (the
   // sample of the update precedes the critic's Adam on the other stream)
   int wait_at_start;
+  // the 16-sample actor chain issued as launches of at most `split` tiles (0: one launch), blk0 the
+  // first tile block of this launch: with the device-side wait above, no launch holds more workgroups
+  // than the chip has CUs, so a CU always fits the critic stream's chain beside the waiting tiles
+  int split, blk0;
   // 1: the 16-sample tiles dealt so that the tiles of one 256-row GEMM chunk run on the XCD that
   // k_wgrad_big runs that chunk on (chain_tile_of)
   int xcd_tiles;
@@ -663,7 +667,8 @@ __global__ void __launch_bounds__(CACTO_THREADS) __attribute__((amdgpu_waves_per
     __syncthreads();
     c.wait_p = nullptr;
   }
-  actor_chain<NJ>(S, chain_tile_of(blockIdx.x, gridDim.x, cs.xcd_tiles), sdp, Ac, C, c, storage, idx, B, gb, step);
+  actor_chain<NJ>(S, chain_tile_of(blockIdx.x + cs.blk0, gridDim.x, cs.xcd_tiles), sdp, Ac, C, c, storage, idx, B, gb,
+                  step);
 }
 
 // The critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the
@@ -1170,14 +1175,15 @@ __device__ __forceinline__ void adam_publish(unsigned long long* sig_p, unsigned
 // One parameter per thread, workgroup blk (NCH > 0).
 // The same publication for write-through stores (CACTO_PIPE_DEVWAIT=3): every thread's stores have
 // completed (waitcnt) before its workgroup counts itself; no fence, no L2 write-back.
-__device__ __forceinline__ void adam_publish_thru(unsigned long long* sig_p, unsigned long long sig_v) {
+// nblk: the Adam step's workgroups (the launch's, or the leading part of k_adam_sample's).
+__device__ __forceinline__ void adam_publish_thru(unsigned long long* sig_p, unsigned long long sig_v, int nblk) {
   if (!sig_p) return;
   __shared__ int last;
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0)
     last = __hip_atomic_fetch_add(sig_p + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-           (unsigned long long)(gridDim.x - 1);
+           (unsigned long long)(nblk - 1);
   __syncthreads();
   if (last && threadIdx.x == 0) {
     __hip_atomic_store(sig_p + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1232,13 +1238,15 @@ __global__ void __launch_bounds__(256) k_adam_sample(const float* __restrict__ s
                                                      float* __restrict__ v, const int32_t* __restrict__ step, AdamArgs a,
                                                      float* target, float4* target_packed,
                                                      const unsigned long long* wait_p, unsigned long long wait_v,
-                                                     int nadam, PerSampleArgs sa) {
+                                                     int nadam, PerSampleArgs sa, unsigned long long* sig_p,
+                                                     unsigned long long sig_v, int thru) {
   __shared__ double top_s[PER_FUSED_TOP];
   __shared__ double scal_s[4];
-  if ((int)blockIdx.x < nadam)
+  if ((int)blockIdx.x < nadam) {
     adam_nch_body<NCH>(blockIdx.x, slab, nch, t, src, netbuf, packed, m, v, step, a, target, target_packed, wait_p,
-                       wait_v);
-  else
+                       wait_v, thru != 0);
+    adam_publish_thru(sig_p, sig_v, nadam);  // (sig_p only with write-through stores; the host checks)
+  } else
     per_sample_body<PER_FUSED_TOP>(blockIdx.x - nadam, sa, top_s, scal_s);
 }
 
@@ -1252,7 +1260,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
   if constexpr (NCH > 0) {
     adam_nch_body<NCH>(blockIdx.x, slab, nch, t, src, netbuf, packed, m, v, step, a, target, target_packed, wait_p,
                        wait_v, thru != 0);
-    if (thru) adam_publish_thru(sig_p, sig_v);
+    if (thru) adam_publish_thru(sig_p, sig_v, gridDim.x);
     else adam_publish(sig_p, sig_v);
     return;
   }
@@ -1296,7 +1304,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
       write_packed(target_packed, t, p, tg);
     }
   }
-  if (thru) adam_publish_thru(sig_p, sig_v);
+  if (thru) adam_publish_thru(sig_p, sig_v, gridDim.x);
   else adam_publish(sig_p, sig_v);
 }
 
@@ -1652,8 +1660,13 @@ struct LaunchActorChain {
       hipLaunchKernelGGL(k_actor_grad_q4<NJ>, dim3(Bp / Q4_TILE), dim3(Q4_THREADS), 0, st, sys->dev, Ac, C, cs,
                          storage, idx, B, gb, step);
     else
-      hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage,
-                         idx, B, gb, step);
+      for (int b0 = 0; b0 < Bp / 16; b0 += cs.split > 0 ? cs.split : Bp / 16) {
+        ChainScalars c = cs;
+        c.blk0 = b0;
+        const int n = cs.split > 0 ? std::min(cs.split, Bp / 16 - b0) : Bp / 16;
+        hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(n), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, c, storage, idx, B,
+                           gb, step);
+      }
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
   }
@@ -1887,6 +1900,8 @@ ChainScalars chain_scalars(const cacto_update_cfg* cfg, int B) {
   cs.wait_v = 0;
   cs.wait_relaxed = 0;
   cs.wait_at_start = 0;
+  cs.split = 0;
+  cs.blk0 = 0;
   // CACTO_CHAIN_XCD=0 keeps the tiles in block order (A/B; read once)
   static const bool xcd_env = [] {
     const char* e = std::getenv("CACTO_CHAIN_XCD");
@@ -1949,7 +1964,7 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
 int launch_actor_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                        const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
                        const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0,
-                       int wait_relaxed = 0, int wait_at_start = 0) {
+                       int wait_relaxed = 0, int wait_at_start = 0, int split = 0) {
   NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
   NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
   ChainScalars cs = chain_scalars(cfg, B);
@@ -1957,6 +1972,7 @@ int launch_actor_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto
   cs.wait_v = wait_v;
   cs.wait_relaxed = wait_relaxed;
   cs.wait_at_start = wait_at_start;
+  cs.split = split;
   return dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st);
 }
 
@@ -1989,14 +2005,14 @@ int launch_adam(const cacto_sys* sys, const cacto_nets* nets, const cacto_update
                        nets->target_d, tpk, wait_p, wait_v, sig_p, sig_v, thru);
   };
   if (sample) {  // the PER loop's fused form (the caller checked nch <= 64)
-    if (sig_p || nch > 64) {
-      set_error("k_adam_sample: no publishing Adam, at most 64 chunks");
+    if ((sig_p && !thru) || nch > 64) {
+      set_error("k_adam_sample: a publishing Adam writes through; at most 64 chunks");
       return CACTO_EINVAL;
     }
     const int ns = (sample->B + 255) / 256;
     auto gs = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(full + ns), dim3(256), 0, st, slab, nch, t, s0, nb, pk, m, v, nets->step_d, aa,
-                         nets->target_d, tpk, wait_p, wait_v, full, *sample);
+                         nets->target_d, tpk, wait_p, wait_v, full, *sample, sig_p, sig_v, thru);
     };
     if (nch <= 8) gs(k_adam_sample<8>);
     else if (nch <= 16) gs(k_adam_sample<16>);
@@ -2591,9 +2607,13 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   // CACTO_PIPE_DEVWAIT=3 (default): that wait without fences — the critic's Adam writes the weights
   // through to memory at agent scope and publishes after its stores completed, the chain polls
   // relaxed; with PER too, the chain polling at its start (before it gathers the sampled rows)
+  // (=3 also splits a chain of more tiles than CUs into launches of at most 256 / the CU count rounded
+  // down to 128 tiles — the XCD dealing's period — each waiting on the previous one)
+  const int split_n = cu_count() / 128 * 128;
   const bool devwait_actor = devwait_env >= 2 && (!per || devwait_env >= 3) && chain_tile(w.Bp) == CACTO_TILE &&
-                             w.Bp / CACTO_TILE <= cu_count();
+                             (w.Bp / CACTO_TILE <= cu_count() || (devwait_env >= 3 && split_n > 0));
   const int thru = devwait_actor && devwait_env >= 3 ? 1 : 0;
+  const int asplit = thru && w.Bp / CACTO_TILE > cu_count() ? split_n : 0;
   unsigned long long* const sig = ms->pipe_sig;
   // CACTO_PIPE_SIGNAL=1: the side stream's wait on the critic's Adam as a stream write / wait-value
   // pair on a signal-memory word instead of an event record / wait (A/B; read once)
@@ -2697,7 +2717,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     else if (!devwait_actor)
       CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side, devwait_actor ? sig + 2 : nullptr,
-                                   base + t + 1, thru, per ? 1 : 0))
+                                   base + t + 1, thru, per ? 1 : 0, asplit))
       return e;
     if (int e = actor_step_tail(sys, nets, cfg, w, side, devwait ? sig : nullptr, base + t + 1)) return e;
     if (devwait) {

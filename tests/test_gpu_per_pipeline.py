@@ -24,7 +24,8 @@ its own child process:
 The 4,096-node sampler is also checked standalone against the oracle at every descent split
 (CACTO_PER_TOP=4096, its own child).
 K = 6 and 7 (even / odd: the critic ends in the caller's buffer or a workspace copy), and the
-non-PER loop (DI, B = 1024, K = 7) against sequential updates under the same knobs. Every child
+non-PER loop (DI, B = 1024, K = 7, and B = 8192, K = 5: more actor tiles than CUs) against
+sequential updates under the same knobs. Every child
 also writes the trees after a priority update with an unsorted index list holding duplicates
 (B = 1024, the fused kernel's filter path), and all children must agree on every byte.
 replay_buffer.py:139-218, RL.py:120-143."""
@@ -107,11 +108,27 @@ def _child():
         runs.append([t.cpu().numpy() for t in (rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf,
                                                rl.actor_m, rl.critic_v, rl.steps)])
     out["di_equal"] = all(np.array_equal(x, z) for x, z in zip(*runs))
+    # B = 8192: 512 actor tiles, more than the CUs — with CACTO_PIPE_DEVWAIT=3 the actor chain is
+    # issued as launches of at most 256 tiles (each under the device-side wait)
+    didx8 = torch.as_tensor(rng.integers(0, N, size=(5, 8192)).astype(np.int32), device="cuda")
+    runs = []
+    for pipelined in (False, True):
+        rl8 = RL_AC(denv, NN(denv, dconf, w_S=1e-2, seed=4), dconf)
+        rl8.setup_model()
+        if pipelined:
+            rl8.update_rows_n(storage, didx8)
+        else:
+            for k in range(5):
+                rl8.update_rows(storage, didx8[k])
+        torch.cuda.synchronize()
+        runs.append([t.cpu().numpy() for t in (rl8.actor_model.buf, rl8.critic_model.buf, rl8.target_critic.buf,
+                                               rl8.actor_m, rl8.critic_v, rl8.steps)])
+    out["di8192_equal"] = all(np.array_equal(x, z) for x, z in zip(*runs))
     # no device-side wait of the pipeline ever timed out (cacto_pipeline_status word 1)
     import ctypes
     from cacto_amd import _lib as L
     latch = 0
-    for sysobj in (env.sys, denv.sys, rl.sys):
+    for sysobj in (env.sys, denv.sys, rl.sys, rl8.sys):
         st = (ctypes.c_ulonglong * 4)()
         L.lib().call("cacto_pipeline_status", sysobj.handle, st)
         latch |= int(st[1])
@@ -148,7 +165,7 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
         res[(every2, fused, devwait, signal, pstream, deep, overlap)] = json.loads(line[len("RESULT "):])
     for key, r in res.items():
-        assert r["K6_equal"] and r["K7_equal"] and r["di_equal"] and r["latch"] == 0, key
+        assert r["K6_equal"] and r["K7_equal"] and r["di_equal"] and r["di8192_equal"] and r["latch"] == 0, key
     for field in ("K6_hash", "K7_hash", "unsorted_hash"):
         assert len({r[field] for r in res.values()}) == 1, field
 
