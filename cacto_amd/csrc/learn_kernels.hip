@@ -2607,9 +2607,15 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   // CACTO_PIPE_DEVWAIT=3 (default): that wait without fences — the critic's Adam writes the weights
   // through to memory at agent scope and publishes after its stores completed, the chain polls
   // relaxed; with PER too, the chain polling at its start (before it gathers the sampled rows)
-  // (=3 also splits a chain of more tiles than CUs into launches of at most 256 / the CU count rounded
-  // down to 128 tiles — the XCD dealing's period — each waiting on the previous one)
-  const int split_n = cu_count() / 128 * 128;
+  // CACTO_ACTOR_SPLIT=1 (with =3): a chain of more tiles than CUs issued as launches of at most the CU
+  // count rounded down to 128 tiles (the XCD dealing's period), so it can wait on the device too.
+  // Measured (updates/s): manipulator B = 8192 8.35 k -> 7.31 k — the halves no longer overlap the
+  // critic stream as one launch does — so it is off by default (read once; A/B).
+  static const bool split_env = [] {
+    const char* e = std::getenv("CACTO_ACTOR_SPLIT");
+    return e && e[0] == '1';
+  }();
+  const int split_n = split_env ? cu_count() / 128 * 128 : 0;
   const bool devwait_actor = devwait_env >= 2 && (!per || devwait_env >= 3) && chain_tile(w.Bp) == CACTO_TILE &&
                              (w.Bp / CACTO_TILE <= cu_count() || (devwait_env >= 3 && split_n > 0));
   const int thru = devwait_actor && devwait_env >= 3 ? 1 : 0;

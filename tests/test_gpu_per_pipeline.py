@@ -18,6 +18,8 @@ its own child process:
     t + 1 on a third stream beside the critic's GEMM and Adam, with a five-buffer index ring, or on
     the critic stream;
   * CACTO_PER_DEEP_TOP = 0 / 1: the multi-workgroup sampler of round 4 or the 8,192-node one;
+  * CACTO_ACTOR_SPLIT = 1: (with DEVWAIT = 3) an actor chain of more tiles than CUs in launches
+    of at most 256 tiles, each waiting on the device;
   * CACTO_PER_OVERLAP = 0 / 1: (with DEVWAIT >= 1, the default) the priority update of update t
     inside the critic GEMM's launch (k_wgrad_big_per: 256-leaf subtrees, the runs recorded by the
     sampler) and the sample of t + 1 inside the critic Adam's (k_adam_sample: 4,096-node top).
@@ -108,8 +110,8 @@ def _child():
         runs.append([t.cpu().numpy() for t in (rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf,
                                                rl.actor_m, rl.critic_v, rl.steps)])
     out["di_equal"] = all(np.array_equal(x, z) for x, z in zip(*runs))
-    # B = 8192: 512 actor tiles, more than the CUs — with CACTO_PIPE_DEVWAIT=3 the actor chain is
-    # issued as launches of at most 256 tiles (each under the device-side wait)
+    # B = 8192: 512 actor tiles, more than the CUs (with CACTO_ACTOR_SPLIT=1 the actor chain is issued
+    # as launches of at most 256 tiles, each under the device-side wait)
     didx8 = torch.as_tensor(rng.integers(0, N, size=(5, 8192)).astype(np.int32), device="cuda")
     runs = []
     for pipelined in (False, True):
@@ -151,19 +153,21 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = {}
-    for every2, fused, devwait, signal, pstream, deep, overlap in (
-            ("0", "1", "0", "0", "1", "1", "1"), ("1", "1", "0", "0", "1", "1", "1"), ("1", "0", "0", "0", "1", "0", "1"),
-            ("0", "1", "1", "0", "1", "1", "1"), ("0", "1", "1", "0", "1", "1", "0"), ("0", "1", "1", "0", "0", "0", "0"),
-            ("0", "0", "1", "0", "1", "1", "0"), ("0", "1", "2", "0", "1", "1", "1"), ("0", "1", "3", "0", "1", "1", "1"),
-            ("0", "1", "1", "1", "1", "1", "1")):
+    for every2, fused, devwait, signal, pstream, deep, overlap, split in (
+            ("0", "1", "0", "0", "1", "1", "1", "0"), ("1", "1", "0", "0", "1", "1", "1", "0"),
+            ("1", "0", "0", "0", "1", "0", "1", "0"), ("0", "1", "1", "0", "1", "1", "1", "0"),
+            ("0", "1", "1", "0", "1", "1", "0", "0"), ("0", "1", "1", "0", "0", "0", "0", "0"),
+            ("0", "0", "1", "0", "1", "1", "0", "0"), ("0", "1", "2", "0", "1", "1", "1", "0"),
+            ("0", "1", "3", "0", "1", "1", "1", "0"), ("0", "1", "3", "0", "1", "1", "1", "1"),
+            ("0", "1", "1", "1", "1", "1", "1", "0")):
         env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait,
                    CACTO_PIPE_SIGNAL=signal, CACTO_PER_STREAM=pstream, CACTO_PER_DEEP_TOP=deep,
-                   CACTO_PER_OVERLAP=overlap)
+                   CACTO_PER_OVERLAP=overlap, CACTO_ACTOR_SPLIT=split)
         r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
-        res[(every2, fused, devwait, signal, pstream, deep, overlap)] = json.loads(line[len("RESULT "):])
+        res[(every2, fused, devwait, signal, pstream, deep, overlap, split)] = json.loads(line[len("RESULT "):])
     for key, r in res.items():
         assert r["K6_equal"] and r["K7_equal"] and r["di_equal"] and r["di8192_equal"] and r["latch"] == 0, key
     for field in ("K6_hash", "K7_hash", "unsorted_hash"):
