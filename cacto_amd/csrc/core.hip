@@ -124,6 +124,7 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   if (sys->per_st) (void)hipStreamSynchronize(sys->per_st);
   if (sys->ev_chain) (void)hipEventDestroy(sys->ev_chain);
   if (sys->ev_samp) (void)hipEventDestroy(sys->ev_samp);
+  if (sys->latch_host) (void)hipHostFree(sys->latch_host);
   if (sys->per_st) (void)hipStreamDestroy(sys->per_st);
   if (sys->pipe_sig) (void)hipFree(sys->pipe_sig);
   if (sys->pipe_wsig) (void)hipFree(sys->pipe_wsig);

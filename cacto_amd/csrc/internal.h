@@ -19,6 +19,9 @@ struct cacto_sys {
   // and its two events: the critic chain finished / the next sample is drawn
   hipStream_t per_st = nullptr;
   hipEvent_t ev_chain = nullptr, ev_samp = nullptr;
+  // pinned host copy of pipe_sig[1] (the device waits' timeout latch), refreshed asynchronously at
+  // the end of every pipelined call and checked at the start of the next one
+  unsigned long long* latch_host = nullptr;
   // device-side ordering of the two-stream pipeline (CACTO_PIPE_DEVWAIT): pipe_sig[0] counts the actor
   // iterations whose chain has finished, [2] the critic Adam steps finished (both monotonic over the
   // handle's life), [1] latches a wait that timed out, [3] is k_adam's last-workgroup counter;

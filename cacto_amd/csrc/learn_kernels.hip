@@ -2541,6 +2541,20 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
   if (int e = ensure_side_stream(ms)) return e;
   if (per && per_stream_on())
     if (int e = ensure_per_stream(ms)) return e;
+  if (!ms->latch_host) {
+    CACTO_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&ms->latch_host), sizeof(unsigned long long),
+                                  hipHostMallocDefault));
+    *ms->latch_host = 0;
+  }
+  // a device-side wait of an earlier call timed out (its copy of the latch has landed by now, or
+  // the next call sees it): the device-side order cannot be trusted, so fail loudly — that happens
+  // when kernels are serialized (AMD_SERIALIZE_KERNEL, counter collection), where the waiting
+  // kernel holds the queue its producer needs; CACTO_PIPE_DEVWAIT=0 uses queue markers instead
+  if (*reinterpret_cast<volatile unsigned long long*>(ms->latch_host)) {
+    set_error("cacto_update_n: a device-side pipeline wait timed out (kernels serialized?); results of that call "
+              "are not trustworthy — run with CACTO_PIPE_DEVWAIT=0");
+    return CACTO_EINVAL;
+  }
   const NetTopo& tc = sys->critic;
   const size_t nb_bytes = ((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256) * sizeof(float);
   const size_t nb_stride = align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
@@ -2555,6 +2569,8 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
   const int err = update_pipeline_body(sys, nets, cfg, storage_d, idx_d, per, K, B, w, st, &cbuf);
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, ms->side));
   CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
+  CACTO_CHECK_HIP(hipMemcpyAsync(ms->latch_host, ms->pipe_sig + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 st));
   if (per && per_stream_on()) {
     CACTO_CHECK_HIP(hipEventRecord(ms->ev_samp, ms->per_st));
     CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_samp, 0));
@@ -2593,7 +2609,13 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   // restores the queue markers
   static const int devwait_env = [] {
     const char* e = std::getenv("CACTO_PIPE_DEVWAIT");
-    return e ? std::atoi(e) : 3;
+    if (e) return std::atoi(e);
+    // serialized kernels (each waits for the previous one to finish) would leave a polling kernel
+    // holding the queue its producer needs: queue markers then
+    const char* s1 = std::getenv("AMD_SERIALIZE_KERNEL");
+    const char* s2 = std::getenv("HIP_LAUNCH_BLOCKING");
+    if ((s1 && std::atoi(s1) != 0) || (s2 && std::atoi(s2) != 0)) return 0;
+    return 3;
   }();
   const bool devwait = devwait_env >= 1;
   // ... and the side stream's wait on the critic's Adam too (k_adam's last workgroup publishes, the
@@ -2628,6 +2650,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     return e && e[0] == '1';
   }();
   const bool streamval = sig_env && ms->pipe_wsig && !devwait_actor;
+
   // the PER stream (per_stream_on) with the device-side write-after-read order: the index ring has
   // five buffers — sample t + 1 runs after critic chain t, which follows Adam(t - 1)'s wait for actor
   // chain t - 4, the last reader of the buffer it overwrites

@@ -14,6 +14,9 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/trace -o run -- python3
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/b128 -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 1000 --batches 128 --extra-systems "" $SMALL > $D/b128.json 2> $D/b128.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/b4096 -o run -- python3 bench.py --steps 10 --warmup 2 --update-steps 1000 --batches 4096 --extra-systems "" $SMALL > $D/b4096.json 2> $D/b4096.err
 PMCARGS="--steps 3 --warmup 1 --extra-systems= --update-steps 20 $SMALL"
+# counter collection serializes the kernels: the two-stream pipeline's device-side waits would then
+# hold the queue their producer needs, so the PMC passes order the streams with queue markers
+export CACTO_PIPE_DEVWAIT=0
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_rollout -d $D/fetch -o run -- python3 bench.py $PMCARGS --batches 128 > $D/fetch.json 2> $D/fetch.err
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_rollout -d $D/write -o run -- python3 bench.py $PMCARGS --batches 128 > $D/write.json 2> $D/write.err
 python3 tools/prof_summary.py stats $D/trace/run_results.db > $D/kernel_stats.csv
