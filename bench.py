@@ -318,14 +318,16 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     seq = {k: out[k] for k in ("S", "A", "status")}
     n_d = inputs[1]
 
-    def step():
+    def step(mid=None):
         # one rollout batch = the sequential pass (k_rollout: actor + dynamics, S/A) and the parallel
-        # reward / EE pass over the recorded steps (k_rollout_rewards), launched apart so each
-        # kernel gets its own HIP-event time; both run on torch's current stream. (Rewards on the
-        # rollout's idle waves beside the dynamics measured slower: one f64 reward per lane is a
-        # 7.6 k-cycle chain on DI against wave 0's 2 k-cycle dynamics phase — DESIGN.md §3.)
+        # reward / EE pass over the recorded steps (k_rollout_rewards), launched apart (a HIP event
+        # between them on the sampled steps gives each kernel its own time); both run on torch's
+        # current stream. (Rewards on the rollout's idle waves beside the dynamics measured slower: one
+        # f64 reward per lane is a 7.6 k-cycle chain on DI against wave 0's 2 k-cycle dynamics phase —
+        # DESIGN.md §3.)
         rl.rollout_batch(None, None, T, inputs=inputs, out=seq)
-        ev[1].record()
+        if mid is not None:
+            mid.record()
         rl.rollout_rewards(out, n_d, T)
 
     # robustness check beside the contract's K-step region (the driver runs K = 20, ~16 ms): a long
@@ -350,46 +352,50 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
         long_region = dict(batches=long_k, seconds=lev[0].elapsed_time(lev[5]) * 1e-3, segment_rates=rates,
                            median=sum_over_ranks(float(np.median(rates)), world),
                            spread=float((max(rates) - min(rates)) / np.median(rates)))
-    ev = [None, torch.cuda.Event(enable_timing=True)]
     for _ in range(W):
         step()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    # HIP events in the timed region: the 5 segment boundaries, and around the rollout kernel and the
+    # rewards kernel of the last step of each segment (every step when K < 5), where the kernel
+    # times (roofline.kernel_ms) are taken. An event is a queue marker with a cost of its own (≈5 µs
+    # on this stack, §6), so the K steps are not bracketed one by one.
+    nseg = 5 if K >= 5 else 0
+    cuts = [j * K // 5 for j in range(6)] if nseg else []
+    sampled = sorted({cuts[j + 1] - 1 for j in range(5)}) if nseg else list(range(K))
+    smp = {k: [torch.cuda.Event(enable_timing=True) for _ in range(3)] for k in sampled}
+    seg_ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if nseg else []
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e in evs:
-        e[0].record()
-        ev[1] = e[1]
-        step()
-        e[2].record()
+    for k in range(K):
+        if nseg and k in cuts[:5]:
+            seg_ev[cuts.index(k)].record()
+        e = smp.get(k)
+        if e is not None:
+            e[0].record()
+        step(e[1] if e is not None else None)
+        if e is not None:
+            e[2].record()
+    if nseg:
+        seg_ev[5].record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
-    kern_ms = sum(e[0].elapsed_time(e[2]) for e in evs) / K
-    seq_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / K
+    evs = [smp[k] for k in sampled]
+    kern_ms = sum(e[0].elapsed_time(e[2]) for e in evs) / len(evs)
+    seq_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
     # the timed region in 5 consecutive segments (HIP events at their boundaries): per-segment rate
     # and the median of the 5, beside the whole-region value
-    seg = segments([(e[0], e[2]) for e in evs], steps_per_call)
+    seg = None
+    if nseg:
+        rates = [steps_per_call * (cuts[j + 1] - cuts[j]) / (seg_ev[j].elapsed_time(seg_ev[j + 1]) * 1e-3)
+                 for j in range(5)]
+        seg = dict(n=5, items_per_segment=K // 5, rates=rates, median=float(np.median(rates)),
+                   spread=float((max(rates) - min(rates)) / np.median(rates)))
     return dict(out=out, S0=S0, nsteps=nsteps, T=T, wall=wall, kernel_ms=kern_ms, seq_kernel_ms=seq_ms,
                 seq_kernel_ms_median=float(np.median([e[0].elapsed_time(e[1]) for e in evs])),
-                rewards_kernel_ms=kern_ms - seq_ms, steps_per_call=steps_per_call,
+                kernel_ms_samples=len(evs), rewards_kernel_ms=kern_ms - seq_ms, steps_per_call=steps_per_call,
                 total_steps=sum_over_ranks(steps_per_call * K, world), segments=seg, long_region=long_region)
-
-
-def segments(pairs, units_per_item, n=5):
-    """Split K timed items (each a (start, end) HIP-event pair, back to back on one stream) into n
-    consecutive segments: units/s of each segment (start of its first item -> end of its last)."""
-    K = len(pairs)
-    if K < n:
-        return None
-    rates = []
-    for j in range(n):
-        lo, hi = j * K // n, (j + 1) * K // n
-        ms = pairs[lo][0].elapsed_time(pairs[hi - 1][1])
-        rates.append(units_per_item * (hi - lo) / (ms * 1e-3))
-    return dict(n=n, items_per_segment=K // n, rates=rates, median=float(np.median(rates)),
-                spread=float((max(rates) - min(rates)) / np.median(rates)))
 
 
 def rollout_diagnostics(rl, conf, roll, K=5):
@@ -901,7 +907,8 @@ def main():
                          "bound": "mfma", "achieved": achieved / 1e12,
                          "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                         "kernel_ms": roll["seq_kernel_ms"], "flop_per_env_step": fa_flops(ns, na),
+                         "kernel_ms": roll["seq_kernel_ms"], "kernel_ms_samples": roll["kernel_ms_samples"],
+                         "flop_per_env_step": fa_flops(ns, na),
                          "rollout_batch_ms": roll["kernel_ms"], "rewards_kernel_ms": roll["rewards_kernel_ms"],
                          "env_steps_per_launch": roll["steps_per_call"],
                          # bytes the batch (k_rollout + k_rollout_rewards) must move: per env step
