@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from conftest import load_weights
+from oracle import buffer as obuf
 from oracle import dynamics as odyn
 from oracle import env as oenv
 from oracle import nn as onn
@@ -283,3 +284,56 @@ def test_vectorised_di_rollout_matches_per_sample_port():
     for e in range(len(S0)):
         ref = oroll.policy_rollout(oe, actor, S0[e], int(n[e]))[0][-1]
         np.testing.assert_allclose(S[e], ref, rtol=1e-12, atol=1e-12)
+
+
+def test_prefix_terms_closed_form_matches_reduce_walk():
+    """The multi-workgroup sampler (cacto_amd/csrc/per_device.h) forms prefix_reduce's terms of
+    sum(0, end) in closed form: the walk stops at depth d* = L - min(trailing ones of end, L) with
+    that node itself as the last term, and above it a right step at depth k (bit L-1-k of end set)
+    adds the node's left child. Same nodes, same order, as the recursion of SegmentTree._reduce
+    (segment_tree.py:76-98) — checked here for every end of every capacity up to 2^10 and sampled
+    ends up to 2^20."""
+    def walk(cap, end):  # the recursion's path (reduce(0, end) with end inclusive)
+        terms, node, ns, ne = [], 1, 0, cap - 1
+        while True:
+            if end == ne:
+                terms.append(node)
+                return terms
+            mid = (ns + ne) // 2
+            if end <= mid:
+                node, ne = 2 * node, mid
+            else:
+                terms.append(2 * node)
+                node, ns = 2 * node + 1, mid + 1
+
+    def closed(cap, end):
+        L = cap.bit_length() - 1
+        ones = 0
+        while ones < L and (end >> ones) & 1:
+            ones += 1
+        dstar = L - ones
+        out = []
+        for k in range(dstar + 1):
+            if k == dstar:
+                out.append((1 << k) | (end >> (L - k)))
+            elif (end >> (L - 1 - k)) & 1:
+                out.append(((1 << k) | (end >> (L - k))) * 2)
+        return out
+
+    rng = np.random.default_rng(0)
+    for L in range(0, 21):
+        cap = 1 << L
+        ends = range(cap) if cap <= 1024 else rng.integers(0, cap, size=2000)
+        for end in ends:
+            assert closed(cap, int(end)) == walk(cap, int(end)), (cap, end)
+    # and the sums agree with SegmentTree.sum on a random tree (the right-nested combination)
+    t = obuf.SumSegmentTree(1 << 12)
+    vals = rng.uniform(0, 1, size=1 << 12)
+    for i, v in enumerate(vals):
+        t[i] = float(v)
+    for end in rng.integers(1, 1 << 12, size=200):
+        terms = closed(1 << 12, int(end) - 1)
+        r = t.value[terms[-1]]
+        for node in reversed(terms[:-1]):
+            r = t.value[node] + r
+        assert r == t.sum(0, int(end))
