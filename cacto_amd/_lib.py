@@ -56,6 +56,7 @@ _SIGS = {
     "cacto_abi_version": (C.c_int, []),
     "cacto_sys_create": (C.c_int, [C.POINTER(SysParams), vp, C.POINTER(vp)]),
     "cacto_sys_destroy": (C.c_int, [vp]),
+    "cacto_sys_set_critic_type": (C.c_int, [vp, C.c_int]),
     "cacto_env_step_batch": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
     "cacto_env_ee": (C.c_int, [vp, vp, vp, C.c_int, vp]),
     "cacto_env_step": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),

@@ -41,8 +41,10 @@ struct Q4CriticFwd {
   Q4Frags<4, N8, NW> f2;
   Q4Frags<8, N8, NW> f3;
   Q4Split<N8, NW> f4;
+  int act;  // NetTopo::act (elu layers of the sine-elu critic)
   template <bool BIAS>
   __device__ __forceinline__ void load(const NetView& N, int wi, int lane) {
+    act = N.t.act;
     f0.template load<BIAS>(N.fwd(0), N.biasp(0), 4, 64, wi, lane);
     f1.template load<BIAS>(N.fwd(1), N.biasp(1), 4, 64, wi, lane);
     f2.template load<BIAS>(N.fwd(2), N.biasp(2), 8, 128, wi, lane);
@@ -91,7 +93,8 @@ __device__ void q4_critic_forward_f(const Q4CriticFwd<NW>& F, const float* X0, f
   auto epi = [&](int l, float* out) {
     return [&, l, out](int ot, float z) {
       float h, c;
-      fast_sincos(z, &h, &c);
+      if ((F.act >> l) & 1) elu_pair(z, &h, &c);
+      else fast_sincos(z, &h, &c);
       const int e = q4e(ot, lane);
       if (Cs) Cs[ZOFF[l] * 64 + e] = c;
       out[e] = h;
@@ -346,7 +349,8 @@ __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, 
         const int e = q4e(ot, lane);
         const float sz = Hs[ZOFF[l] * 64 + e], cz = Cs[ZOFF[l] * 64 + e];
         const float gu = l < 3 ? G[goff[l + 1] * 64 + e] : w5;  // layer 3: out tile `wave`
-        float zb = fmul(-fmul(acc, gu), sz);                     // CosGrad: -grad * sin(x)
+        float zb = ((C.t.act >> l) & 1) ? fmul(fmul(acc, gu), act_d2(true, sz))  // elu: grad * exp(z) below 0
+                                        : fmul(-fmul(acc, gu), sz);             // CosGrad: -grad * sin(x)
         if (l == 3) zb = fadd(zb, fmul(fmul(vb, w5), cz));
         ZB[ZOFF[l] * 64 + e] = zb;
         const float gn = fmul(acc, cz);  // MulGrad into the upstream grad

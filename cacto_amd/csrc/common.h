@@ -51,6 +51,19 @@ __device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b)
 __device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
 __device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
 
+// The sine-elu critic's elu layers (critic_type 'sine-elu', NeuralNetwork.py:80-93): tf.nn.elu
+// (features < 0 ? exp(features) - 1 : features) and the factor EluGrad applies to the upstream
+// gradient (activations < 0 ? activations + 1 : 1) — the (h, c) pair a sine layer gives as
+// (sin z, cos z).
+__device__ __forceinline__ void elu_pair(float z, float* h, float* c) {
+  const float y = z < 0.f ? __fsub_rn(expf(z), 1.f) : z;
+  *h = y;
+  *c = y < 0.f ? __fadd_rn(y, 1.f) : 1.f;
+}
+// The second derivative of a hidden activation from its stored value h: sine -h (CosGrad's
+// -sin), elu h < 0 ? h + 1 (= exp z) : 0.
+__device__ __forceinline__ float act_d2(bool elu, float h) { return elu ? (h < 0.f ? __fadd_rn(h, 1.f) : 0.f) : -h; }
+
 // sin and cos of x: Cody-Waite reduction by pi/2 (3-part constant, FMA) and minimax polynomials
 // on [-pi/4, pi/4] (max error ~1 ulp for |x| <= 8192, far beyond SIREN pre-activations);
 // larger |x| falls back to the library's Payne-Hanek path.

@@ -110,6 +110,13 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
   }
 }
 
+extern "C" int cacto_sys_set_critic_type(cacto_sys* sys, int critic_type) {
+  CACTO_REQUIRE(sys && (critic_type == 0 || critic_type == 1),
+                "cacto_sys_set_critic_type: 0 (sine) or 1 (sine-elu); the elu / relu critics are not built");
+  sys->critic.act = critic_type == 1 ? 0xA : 0;  // hidden layers 1 and 3 elu
+  return CACTO_OK;
+}
+
 extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   if (!sys) return CACTO_OK;
   (void)hipFree(sys->dev);

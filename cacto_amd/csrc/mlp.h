@@ -33,6 +33,7 @@ struct NetTopo {
   int pkoff[MAX_LAYERS];  // in blocks
   int blocks;             // pk blocks (pkT region has the same count, starts at `blocks`)
   int params;
+  int act;                // critic: bit l set = hidden layer l is elu (critic_type 'sine-elu'), else sine
 };
 
 inline NetTopo make_topo(int net, int ns, int na) {

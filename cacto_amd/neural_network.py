@@ -14,6 +14,7 @@ from . import h5
 from .system import DEVICE, dptr, stream
 
 ACTOR, CRITIC = L.CACTO_NET_ACTOR, L.CACTO_NET_CRITIC
+SINE_ELU = ("sine", "elu", "sine", "elu")  # critic_type 'sine-elu' hidden layers (NeuralNetwork.py:80-93)
 
 
 def layer_shapes(kind, ns, na):
@@ -112,15 +113,16 @@ class Net:
         self.set_weights([z["arr_%d" % i] for i in range(len(self.shapes))])
 
 
-def init_weights(kind, ns, na, rng):
+def init_weights(kind, ns, na, rng, critic_acts=("sine",) * 4):
     """Keras initialisers: Glorot-uniform kernels / zero biases for Dense; tf_siren
     SinusodialRepresentationDense (w0 = 1, c = 6): kernel U(+-sqrt(6/fan_in)), bias he_uniform
-    U(+-sqrt(6/units))."""
+    U(+-sqrt(6/units)). `critic_acts`: the critic's hidden layers ('sine' SIREN layers, 'elu' Dense
+    layers: NeuralNetwork.py:80-93)."""
     ws = []
     shapes = layer_shapes(kind, ns, na)
     for li in range(0, len(shapes), 2):
         fi, fo = shapes[li]
-        siren = kind == CRITIC and li < 8
+        siren = kind == CRITIC and li < 8 and critic_acts[li // 2] == "sine"
         lim = np.sqrt(6.0 / fi) if siren else np.sqrt(6.0 / (fi + fo))
         ws.append(rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32))
         b = rng.uniform(-np.sqrt(6.0 / fo), np.sqrt(6.0 / fo), size=fo) if siren else np.zeros(fo)
@@ -144,14 +146,24 @@ class NN:
         return net
 
     def create_critic_sine(self):
+        self.sys.set_critic_type("sine")
         net = Net(self.sys, CRITIC)
         net.set_weights(init_weights(CRITIC, self.sys.ns, self.sys.na, self.rng))
         return net
 
-    def create_critic_elu(self):
-        raise NotImplementedError("critic_type 'elu' is outside the hot path (every conf uses 'sine')")
+    def create_critic_sine_elu(self):
+        """NeuralNetwork.py:80-93: sine (64), elu (64), sine (128), elu (128) hidden layers + Dense(1).
+        The activation is a property of the system handle (cacto_sys_set_critic_type), so every
+        critic of this system — the target too — takes it."""
+        self.sys.set_critic_type("sine-elu")
+        net = Net(self.sys, CRITIC)
+        net.set_weights(init_weights(CRITIC, self.sys.ns, self.sys.na, self.rng, critic_acts=SINE_ELU))
+        return net
 
-    create_critic_sine_elu = create_critic_elu
+    def create_critic_elu(self):
+        raise NotImplementedError("critic_type 'elu' (16, 32, 256, 256 wide) is not built; every shipped conf "
+                                  "uses 'sine' ('sine-elu' is built)")
+
     create_critic_relu = create_critic_elu
 
     # ---- NeuralNetwork.py:130-138 ----

@@ -115,7 +115,12 @@ class RL_AC:
         """`weights`: optional dict {'actor', 'critic', 'target'} of Keras-order arrays (e.g. the
         .h5-derived fixtures) instead of fresh initialisers."""
         self.actor_model = self.NN.create_actor()
-        self.critic_model = self.NN.create_critic_sine()
+        # RL.py:65-76 (critic_type: 'sine' in every shipped config; 'sine-elu' built; 'elu' / 'relu'
+        # raise NotImplementedError)
+        ctype = getattr(self.conf, "critic_type", "sine")
+        create = {"sine": self.NN.create_critic_sine, "sine-elu": self.NN.create_critic_sine_elu,
+                  "elu": self.NN.create_critic_elu}.get(ctype, self.NN.create_critic_relu)
+        self.critic_model = create()
         self.target_critic = Net(self.sys, CRITIC, role="target")
         if weights is not None:
             self.actor_model.set_weights(weights["actor"])

@@ -140,6 +140,11 @@ class System:
     def param_count(self, net):
         return int(L.lib().raw("cacto_mlp_param_count")(self.handle, net))
 
+    def set_critic_type(self, critic_type):
+        """RL.py:65-76 critic_type of this system's critics: 'sine' or 'sine-elu'."""
+        L.lib().call("cacto_sys_set_critic_type", self.handle, {"sine": 0, "sine-elu": 1}[critic_type])
+        self.critic_type = critic_type
+
     def netbuf_floats(self, net):
         return int(L.lib().raw("cacto_mlp_netbuf_floats")(self.handle, net))
 

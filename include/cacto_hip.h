@@ -119,6 +119,11 @@ int cacto_abi_version(void);
 /* joint_table_h: n_joints x CACTO_JOINT_COLS float64 (host), see cacto_amd/robots.py */
 int cacto_sys_create(const cacto_sys_params* params_h, const double* joint_table_h, cacto_sys** out);
 int cacto_sys_destroy(cacto_sys* sys);
+/* The critic's hidden activations (RL.py:65-76 critic_type): 0 = 'sine' (4 SIREN layers, the
+ * default, every shipped config), 1 = 'sine-elu' (NeuralNetwork.py:80-93: sine, elu, sine, elu
+ * layers of the same widths). Set before creating or updating critic networks of this handle; the
+ * 'elu' and 'relu' critics (16, 32, 256, 256 wide) are not built (CACTO_EINVAL). */
+int cacto_sys_set_critic_type(cacto_sys* sys, int critic_type);
 
 /* ---------------------------------------------------------------- environment ------------ */
 

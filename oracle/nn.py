@@ -7,6 +7,7 @@ Restated:
   * normalize_tensor                      utils.py:17-24
   * actor  Dense-LeakyReLU(0.3)x2-Dense   NeuralNetwork.py:51-63 (regularisers never enter a loss)
   * critic 4x sin(xW+b) (tf_siren w0=1) + Dense(1)                       NeuralNetwork.py:95-108
+    and the sine-elu critic (sine, elu, sine, elu hidden layers of the same widths)  :80-93
   * custom_logarithm                      NeuralNetwork.py:140-148
   * compute_critic_grad (Sobolev)         NeuralNetwork.py:150-178
   * compute_actor_grad                    NeuralNetwork.py:180-233
@@ -75,13 +76,30 @@ def actor_forward32(params, S, norm):
         return h2 @ W3 + b3
 
 
-def critic_forward(params, S, norm, keep=False):
+SINE = ("sine",) * 4            # critic_type 'sine' (every shipped config)
+SINE_ELU = ("sine", "elu", "sine", "elu")   # critic_type 'sine-elu' (NeuralNetwork.py:80-93)
+
+
+def act(z, kind):
+    """Hidden activation: tf_siren sin(z) (w0 = 1) or Keras 'elu' (z if z > 0 else exp(z) - 1)."""
+    return np.sin(z) if kind == "sine" else np.where(z > 0, z, np.expm1(np.minimum(z, 0.0)))
+
+
+def act_d1(z, kind):
+    return np.cos(z) if kind == "sine" else np.where(z > 0, 1.0, np.exp(np.minimum(z, 0.0)))
+
+
+def act_d2(z, kind):
+    return -np.sin(z) if kind == "sine" else np.where(z > 0, 0.0, np.exp(np.minimum(z, 0.0)))
+
+
+def critic_forward(params, S, norm, keep=False, acts=SINE):
     P = [np.asarray(p, dtype=np.float64) for p in params]
     h = normalize(S, norm)
     hs, zs = [h], []
     for l in range(4):
         z = h @ P[2 * l] + P[2 * l + 1]
-        h = np.sin(z)
+        h = act(z, acts[l])
         zs.append(z)
         hs.append(h)
     V = h @ P[8] + P[9]
@@ -90,16 +108,16 @@ def critic_forward(params, S, norm, keep=False):
     return V
 
 
-def critic_input_grad(params, S, norm, keep=None):
-    """dV/ds (raw state) through the sine MLP (cos terms) and the normalisation."""
+def critic_input_grad(params, S, norm, keep=None, acts=SINE):
+    """dV/ds (raw state) through the MLP (activation derivatives) and the normalisation."""
     P = [np.asarray(p, dtype=np.float64) for p in params]
     if keep is None:
-        _, keep = critic_forward(params, S, norm, keep=True)
+        _, keep = critic_forward(params, S, norm, keep=True, acts=acts)
     hs, zs = keep
     g = np.broadcast_to(P[8][:, 0], (S.shape[0], P[8].shape[0]))
     ds = []
     for l in range(3, -1, -1):
-        d = g * np.cos(zs[l])
+        d = g * act_d1(zs[l], acts[l])
         ds.append(d)
         g = d @ P[2 * l].T
     ds = ds[::-1]          # ds[l] = dV/dz_{l+1}
@@ -115,7 +133,7 @@ def clog_grad(x):
     return np.where(ax >= CLOG_EPS, 1.0 / (np.maximum(ax, CLOG_EPS) + 1.0), 0.0)
 
 
-def compute_critic_grad(critic, target, S, S_next, R, dVdx, d, w, w_S, norm, MC=False):
+def compute_critic_grad(critic, target, S, S_next, R, dVdx, d, w, w_S, norm, MC=False, acts=SINE):
     """NeuralNetwork.py:150-178. Returns (grads, y, V, V_tgt(s), loss)."""
     S = np.asarray(S, dtype=np.float64)
     B = S.shape[0]
@@ -125,9 +143,9 @@ def compute_critic_grad(critic, target, S, S_next, R, dVdx, d, w, w_S, norm, MC=
     if MC:
         y = R
     else:
-        y = R + (1 - d) * critic_forward(target, S_next, norm)
+        y = R + (1 - d) * critic_forward(target, S_next, norm, acts=acts)
     P = [np.asarray(p, dtype=np.float64) for p in critic]
-    V, keep = critic_forward(critic, S, norm, keep=True)
+    V, keep = critic_forward(critic, S, norm, keep=True, acts=acts)
     hs, zs = keep
     grads = [np.zeros_like(p) for p in P]
     zbar = [np.zeros_like(z) for z in zs]
@@ -139,7 +157,7 @@ def compute_critic_grad(critic, target, S, S_next, R, dVdx, d, w, w_S, norm, MC=
     grads[9] += Vbar.sum(axis=0)
     hbar = Vbar @ P[8].T
     if w_S != 0:
-        dVds, ds = critic_input_grad(critic, S, norm, keep)
+        dVds, ds = critic_input_grad(critic, S, norm, keep, acts=acts)
         ns = S.shape[1]
         yt, yp = clog(np.asarray(dVdx, dtype=np.float64)[:, :-1]), clog(dVds[:, :-1])
         loss += np.mean(w[:, 0] * np.mean((yp - yt) ** 2, axis=1))
@@ -147,41 +165,41 @@ def compute_critic_grad(critic, target, S, S_next, R, dVdx, d, w, w_S, norm, MC=
         g0bar = np.zeros_like(dVds)
         g0bar[:, :-1] = gyp * clog_grad(dVds[:, :-1])
         gbar = g0bar * norm_grad_scale(norm)                   # adjoint of g_0 = dV/dx0
-        # backward of the first backward pass. With G[4] = W5[:, 0], D[l] = G[l+1]*cos(z_l),
+        # backward of the first backward pass. With G[4] = W5[:, 0], D[l] = G[l+1]*act'(z_l),
         # G[l] = D[l] W_l^T (G[0] = dV/dx0), walk l = 0..3 carrying gbar = adjoint of G[l].
         for l in range(4):
             W = P[2 * l]
             grads[2 * l] += gbar.T @ ds[l]                     # G[l] = D[l] W_l^T
             dbar = gbar @ W                                    # adjoint of D[l]
-            g_up = _g_of_layer(P, zs, l)                       # G[l+1]
-            zbar[l] += dbar * g_up * (-np.sin(zs[l]))
-            gbar = dbar * np.cos(zs[l])                        # adjoint of G[l+1]
+            g_up = _g_of_layer(P, zs, l, acts)                 # G[l+1]
+            zbar[l] += dbar * g_up * act_d2(zs[l], acts[l])
+            gbar = dbar * act_d1(zs[l], acts[l])               # adjoint of G[l+1]
         grads[8][:, 0] += gbar.sum(axis=0)                     # G[4] = W5[:, 0]
     # backward through the forward graph
-    zbar[3] += hbar * np.cos(zs[3])
+    zbar[3] += hbar * act_d1(zs[3], acts[3])
     for l in range(3, -1, -1):
         grads[2 * l] += hs[l].T @ zbar[l]
         grads[2 * l + 1] += zbar[l].sum(axis=0)
         if l > 0:
-            zbar[l - 1] += (zbar[l] @ P[2 * l].T) * np.cos(zs[l - 1])
-    return grads, y, V, critic_forward(target, S, norm), loss
+            zbar[l - 1] += (zbar[l] @ P[2 * l].T) * act_d1(zs[l - 1], acts[l - 1])
+    return grads, y, V, critic_forward(target, S, norm, acts=acts), loss
 
 
-def _g_of_layer(P, zs, l):
-    """g_l = dV/dh_{l+1} (h_{l+1} = sin z_l) for layer index l in 0..3."""
+def _g_of_layer(P, zs, l, acts=SINE):
+    """g_l = dV/dh_{l+1} (h_{l+1} = act(z_l)) for layer index l in 0..3."""
     B = zs[0].shape[0]
     g = np.broadcast_to(P[8][:, 0], (B, P[8].shape[0]))
     for k in range(3, l, -1):
-        g = (g * np.cos(zs[k])) @ P[2 * k].T
+        g = (g * act_d1(zs[k], acts[k])) @ P[2 * k].T
     return g
 
 
-def critic_loss(critic, target, S, S_next, R, dVdx, d, w, w_S, norm):
+def critic_loss(critic, target, S, S_next, R, dVdx, d, w, w_S, norm, acts=SINE):
     """Scalar loss (for finite-difference checks)."""
-    return compute_critic_grad(critic, target, S, S_next, R, dVdx, d, w, w_S, norm)[4]
+    return compute_critic_grad(critic, target, S, S_next, R, dVdx, d, w, w_S, norm, acts=acts)[4]
 
 
-def actor_dq_da(env, actor, critic, S, term, norm):
+def actor_dq_da(env, actor, critic, S, term, norm, acts=SINE):
     """dQ/da of NeuralNetwork.py:185-215 (float64; env.simulate_batch/derivative_batch cast to f32
     as the reference does)."""
     conf = env.conf
@@ -189,7 +207,7 @@ def actor_dq_da(env, actor, critic, S, term, norm):
     A = actor_forward(actor, S32, norm).astype(np.float32)
     S_next = env.simulate_batch(S32, A)
     Fu = env.derivative_batch(S32, A).astype(np.float64)
-    dVds_next, _ = critic_input_grad(critic, S_next.astype(np.float64), norm)
+    dVds_next, _ = critic_input_grad(critic, S_next.astype(np.float64), norm, acts=acts)
     term = np.asarray(term, dtype=np.float64).reshape(-1, 1)
     W = term @ np.reshape(conf.cost_weights_terminal, (1, -1)) + \
         (1 - term) @ np.reshape(conf.cost_weights_running, (1, -1))
@@ -198,11 +216,11 @@ def actor_dq_da(env, actor, critic, S, term, norm):
     return dQ_da, A, S_next, Fu, dVds_next, dr_da
 
 
-def compute_actor_grad(env, actor, critic, S, term, norm, batch_size=None):
+def compute_actor_grad(env, actor, critic, S, term, norm, batch_size=None, acts=SINE):
     """NeuralNetwork.py:180-233: grads of mean_b(-dQ/da_b . pi(s_b)) w.r.t. actor params."""
     S = np.asarray(S, dtype=np.float64)
     B = S.shape[0] if batch_size is None else batch_size
-    dQ_da = actor_dq_da(env, actor, critic, S, term, norm)[0]
+    dQ_da = actor_dq_da(env, actor, critic, S, term, norm, acts=acts)[0]
     P = [np.asarray(p, dtype=np.float64) for p in actor]
     a, (x0, z1, h1, z2, h2) = actor_forward(actor, S, norm, keep=True)
     abar = -dQ_da / B

@@ -29,8 +29,9 @@ def actor_shapes(ns, na):
     return [(ns, 256), (256,), (256, 256), (256,), (256, na), (na,)]
 
 
+@pytest.mark.parametrize("acts", [onn.SINE, onn.SINE_ELU])
 @pytest.mark.parametrize("w_S", [0.0, 1e-2])
-def test_critic_grad_fd(w_S):
+def test_critic_grad_fd(w_S, acts):
     rng = np.random.default_rng(0)
     ns, B = 5, 6
     norm = np.array([15., 15., 6., 6., 10.])
@@ -40,8 +41,8 @@ def test_critic_grad_fd(w_S):
     Sn = rng.uniform(-10, 10, size=(B, ns))
     R = rng.normal(size=(B, 1)); d = (rng.uniform(size=(B, 1)) < .4) * 1.0
     dVdx = rng.normal(size=(B, ns)); w = rng.uniform(.5, 2, size=(B, 1))
-    grads = onn.compute_critic_grad(crit, tgt, S, Sn, R, dVdx, d, w, w_S, norm)[0]
-    f = lambda P: onn.critic_loss(P, tgt, S, Sn, R, dVdx, d, w, w_S, norm)
+    grads = onn.compute_critic_grad(crit, tgt, S, Sn, R, dVdx, d, w, w_S, norm, acts=acts)[0]
+    f = lambda P: onn.critic_loss(P, tgt, S, Sn, R, dVdx, d, w, w_S, norm, acts=acts)
     eps = 1e-6
     for li, (p, g) in enumerate(zip(crit, grads)):
         flat = p.reshape(-1)
@@ -54,18 +55,19 @@ def test_critic_grad_fd(w_S):
             assert abs(fd - g.reshape(-1)[k]) <= 1e-6 * max(1.0, abs(fd)), (li, k, fd, g.reshape(-1)[k])
 
 
-def test_critic_input_grad_fd():
+@pytest.mark.parametrize("acts", [onn.SINE, onn.SINE_ELU])
+def test_critic_input_grad_fd(acts):
     rng = np.random.default_rng(1)
     ns = 7
     norm = np.array([15., 15., 15., 10., 10., 10., 5.])
     crit = _rand_params(rng, critic_shapes(ns))
     S = rng.uniform(-3, 3, size=(4, ns))
-    g, _ = onn.critic_input_grad(crit, S, norm)
+    g, _ = onn.critic_input_grad(crit, S, norm, acts=acts)
     eps = 1e-6
     for j in range(ns):
         Sp, Sm = S.copy(), S.copy()
         Sp[:, j] += eps; Sm[:, j] -= eps
-        fd = (onn.critic_forward(crit, Sp, norm) - onn.critic_forward(crit, Sm, norm))[:, 0] / (2 * eps)
+        fd = (onn.critic_forward(crit, Sp, norm, acts=acts) - onn.critic_forward(crit, Sm, norm, acts=acts))[:, 0] / (2 * eps)
         np.testing.assert_allclose(g[:, j], fd, rtol=1e-6, atol=1e-8)
 
 
