@@ -15,6 +15,8 @@
  *   cacto_rollout_rewards  Env.step reward / get_end_effector_position over recorded trajectories
  *   cacto_ddp_backward     TO.backward_pass TO.py:119-202 (dV/dx Sobolev labels)
  *   cacto_mlp_pack         (layout transform for the kernels; no reference counterpart)
+ *   cacto_sys_set_critic_type  RL_AC.setup_model's critic_type choice RL.py:65-76 ('sine' /
+ *                          'sine-elu', NeuralNetwork.py:80-108)
  *   cacto_actor_forward    NN.eval(actor, s)  NeuralNetwork.py:130-138 (+ utils.py:17-24)
  *   cacto_critic_forward   NN.eval(critic, s)
  *   cacto_critic_input_grad tape.gradient(V, s)  NeuralNetwork.py:162-165, :190-195
