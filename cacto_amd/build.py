@@ -42,22 +42,37 @@ def _compile(src):
     return obj
 
 
-def build_variant(name, defines):
-    """A diagnostic build (e.g. in-kernel timestamps) into cacto_amd/<name>.so."""
+def build_variant(name, defines, force=True, verbose=False):
+    """Another build of the library with extra defines into cacto_amd/<name>.so: diagnostic builds
+    (in-kernel timestamps) and the sine-elu critic build (VARIANTS)."""
     out = os.path.join(HERE, name + ".so")
-    objs = []
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= _deps_mtime():
+        return out
     os.makedirs(OBJ, exist_ok=True)
-    for src in SOURCES:
+
+    def one(src):
         obj = os.path.join(OBJ, name + "_" + src.replace(".hip", ".o"))
         cmd = [hipcc()] + FLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(r.stderr[-4000:])
-        objs.append(obj)
-    r = subprocess.run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-o", out] + objs, capture_output=True, text=True)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(one, SOURCES))
+    r = subprocess.run([hipcc(), "--offload-arch=" + ARCH, "-shared", "-o", out + ".tmp"] + objs, capture_output=True,
+                       text=True)
     if r.returncode != 0:
         raise RuntimeError(r.stderr[-4000:])
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print("built", out)
     return out
+
+
+# library variants built beside libcacto_hip.so: critic_type 'sine-elu' (NeuralNetwork.py:80-93) has
+# its elu layers compiled in only here, so the default (sine) build's chain kernels carry no branch
+VARIANTS = {"libcacto_hip_sine_elu": ["CACTO_CRITIC_ELU"]}
 
 
 def build(force=False, verbose=True):
@@ -65,6 +80,7 @@ def build(force=False, verbose=True):
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
         if verbose:
             print("libcacto_hip.so up to date")
+        build_variants(verbose=verbose)
         return LIB
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
         objs = list(ex.map(_compile, SOURCES))
@@ -75,7 +91,13 @@ def build(force=False, verbose=True):
     os.replace(LIB + ".tmp", LIB)
     if verbose:
         print("built", LIB)
+    build_variants(verbose=verbose)
     return LIB
+
+
+def build_variants(force=False, verbose=True):
+    for name, defines in VARIANTS.items():
+        build_variant(name, defines, force=force, verbose=verbose)
 
 
 if __name__ == "__main__":

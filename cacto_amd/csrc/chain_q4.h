@@ -93,8 +93,11 @@ __device__ void q4_critic_forward_f(const Q4CriticFwd<NW>& F, const float* X0, f
   auto epi = [&](int l, float* out) {
     return [&, l, out](int ot, float z) {
       float h, c;
+#ifdef CACTO_CRITIC_ELU
       if ((F.act >> l) & 1) elu_pair(z, &h, &c);
-      else fast_sincos(z, &h, &c);
+      else
+#endif
+        fast_sincos(z, &h, &c);
       const int e = q4e(ot, lane);
       if (Cs) Cs[ZOFF[l] * 64 + e] = c;
       out[e] = h;
@@ -349,8 +352,12 @@ __device__ __forceinline__ void q4_critic_chain(Q4CriticLds& S, const int tile, 
         const int e = q4e(ot, lane);
         const float sz = Hs[ZOFF[l] * 64 + e], cz = Cs[ZOFF[l] * 64 + e];
         const float gu = l < 3 ? G[goff[l + 1] * 64 + e] : w5;  // layer 3: out tile `wave`
+#ifdef CACTO_CRITIC_ELU
         float zb = ((C.t.act >> l) & 1) ? fmul(fmul(acc, gu), act_d2(true, sz))  // elu: grad * exp(z) below 0
                                         : fmul(-fmul(acc, gu), sz);             // CosGrad: -grad * sin(x)
+#else
+        float zb = fmul(-fmul(acc, gu), sz);
+#endif
         if (l == 3) zb = fadd(zb, fmul(fmul(vb, w5), cz));
         ZB[ZOFF[l] * 64 + e] = zb;
         const float gn = fmul(acc, cz);  // MulGrad into the upstream grad

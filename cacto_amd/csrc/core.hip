@@ -113,6 +113,13 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
 extern "C" int cacto_sys_set_critic_type(cacto_sys* sys, int critic_type) {
   CACTO_REQUIRE(sys && (critic_type == 0 || critic_type == 1),
                 "cacto_sys_set_critic_type: 0 (sine) or 1 (sine-elu); the elu / relu critics are not built");
+#ifndef CACTO_CRITIC_ELU
+  // the elu layers are compiled into the kernels only in the CACTO_CRITIC_ELU build
+  // (cacto_amd/libcacto_hip_sine_elu.so): a runtime branch in the chain kernels' epilogues cost the
+  // sine critic 4-7 % of its B = 4096 update rate
+  CACTO_REQUIRE(critic_type == 0, "cacto_sys_set_critic_type: critic_type 'sine-elu' needs the CACTO_CRITIC_ELU build "
+                                  "(CACTO_HIP_LIB=cacto_amd/libcacto_hip_sine_elu.so)");
+#endif
   sys->critic.act = critic_type == 1 ? 0xA : 0;  // hidden layers 1 and 3 elu
   return CACTO_OK;
 }

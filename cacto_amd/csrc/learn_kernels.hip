@@ -252,7 +252,11 @@ __device__ __forceinline__ void critic_chain(CriticLds& S, const int tile, const
         const float sv[4] = {sz.x, sz.y, sz.z, sz.w}, cv[4] = {cz.x, cz.y, cz.z, cz.w};
         const float gg[4] = {gu.x, gu.y, gu.z, gu.w};
         float zb[4], gn[4];
+#ifdef CACTO_CRITIC_ELU
         const bool elu = (C.t.act >> l) & 1;
+#else
+        constexpr bool elu = false;
+#endif
         for (int r = 0; r < 4; ++r) {
           // CosGrad: -grad * sin(x) (an elu layer: grad * exp(z) below zero)
           zb[r] = elu ? fmul(fmul(acc[r], gg[r]), act_d2(true, sv[r])) : fmul(-fmul(acc[r], gg[r]), sv[r]);

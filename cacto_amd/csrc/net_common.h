@@ -211,10 +211,13 @@ __device__ void critic_forward_tile_f(const CriticFwdFrags& F, const NetView& N,
     return [&, l, out](int ot, floatx4 acc) {
       float h[4], c[4];
       const float z[4] = {acc[0], acc[1], acc[2], acc[3]};  // x W + b
+#ifdef CACTO_CRITIC_ELU
       if ((N.t.act >> l) & 1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) elu_pair(z[r], &h[r], &c[r]);
-      } else {
+      } else
+#endif
+      {
         fast_sincos4(z, h, c);
       }
       const float4 h4 = make_float4(h[0], h[1], h[2], h[3]);

@@ -219,76 +219,6 @@ def test_actor_grad(system, tag, B):
         assert rel_l2(a.cpu().numpy(), b) < 2e-4, (i, rel_l2(a.cpu().numpy(), b))
 
 
-def _sine_elu_nets(system, seed=0):
-    """critic_type 'sine-elu' (NeuralNetwork.py:80-93) on a fresh conf (its own system handle:
-    the critic activation is a property of the handle)."""
-    from cacto_amd.environment import make_env
-    from cacto_amd.neural_network import NN
-    from cacto_amd.rl import RL_AC
-    conf = load_conf(system, fresh=True)
-    conf.critic_type = "sine-elu"
-    genv = make_env(conf)
-    nn = NN(genv, conf, w_S=1e-2, seed=seed)
-    rl = RL_AC(genv, nn, conf)
-    rl.setup_model()
-    assert genv.sys.critic_type == "sine-elu"
-    return conf, genv, oenv.make_env(conf), nn, rl
-
-
-@pytest.mark.parametrize("B", [128, 1024])  # the 4-sample (B <= 512) and the 16-sample chain tiles
-def test_sine_elu_critic(B):
-    """The sine-elu critic (sine, elu, sine, elu hidden layers): forward, dV/ds, the Sobolev critic
-    gradient and the actor gradient through it against the oracle (acts=SINE_ELU; the oracle's
-    elu double backprop is pinned by finite differences, test_oracle_math.py)."""
-    conf, genv, oe, nn, rl = _sine_elu_nets("double_integrator")
-    ns = conf.nb_state
-    norm = conf.state_norm_arr.astype(np.float64)
-    rng = np.random.default_rng(21)
-    S = _states(conf, 200, rng).astype(np.float32)
-    cw = rl.critic_model.get_weights()
-    V, g = nn.critic_input_grad(rl.critic_model, S)
-    ref_V = onn.critic_forward(cw, S.astype(np.float64), norm, acts=onn.SINE_ELU)
-    ref_g, _ = onn.critic_input_grad(cw, S.astype(np.float64), norm, acts=onn.SINE_ELU)
-    assert np.abs(V.cpu().numpy() - ref_V).max() <= 1e-5 * max(1.0, np.abs(ref_V).max())
-    assert rel_l2(g.cpu().numpy(), ref_g) < 2e-5
-    Ve = nn.eval(rl.critic_model, S).cpu().numpy()
-    assert np.abs(Ve - ref_V).max() <= 1e-5 * max(1.0, np.abs(ref_V).max())
-    rows = _replay_rows(conf, B, rng)
-    rows_f32 = rows.astype(np.float32).astype(np.float64)
-    idx = torch.arange(B, dtype=torch.int32, device="cuda")
-    gc, y, Vr, Vt = rl.critic_grad_rows(torch.as_tensor(rows, device="cuda"), idx)
-    ref = onn.compute_critic_grad(cw, rl.target_critic.get_weights(), rows_f32[:, :ns],
-                                  rows_f32[:, ns + 1:2 * ns + 1], rows_f32[:, ns:ns + 1],
-                                  rows_f32[:, 2 * ns + 1:3 * ns + 1], rows_f32[:, 3 * ns + 1:3 * ns + 2],
-                                  np.ones((B, 1)), 1e-2, norm, acts=onn.SINE_ELU)
-    for i, (a, b) in enumerate(zip(gc, ref[0])):
-        assert rel_l2(a.cpu().numpy(), b) < 2e-4, (i, rel_l2(a.cpu().numpy(), b))
-    ga = rl.actor_grad_rows(torch.as_tensor(rows, device="cuda"), idx)
-    refa = onn.compute_actor_grad(oe, rl.actor_model.get_weights(), cw, rows[:, :ns].astype(np.float32),
-                                  rows[:, 3 * ns + 2:3 * ns + 3], norm, acts=onn.SINE_ELU)
-    for i, (a, b) in enumerate(zip(ga, refa)):
-        assert rel_l2(a.cpu().numpy(), b) < 2e-4, (i, rel_l2(a.cpu().numpy(), b))
-
-
-def test_sine_elu_pipelined_updates_equal_sequential():
-    """The pipelined update loop (B = 1024: two streams) with the sine-elu critic equals the
-    sequential updates bit for bit."""
-    runs = []
-    for pipelined in (False, True):
-        conf, genv, oe, nn, rl = _sine_elu_nets("double_integrator", seed=3)
-        rng = np.random.default_rng(22)
-        storage = torch.as_tensor(_replay_rows(conf, 4000, rng), device="cuda")
-        idx = torch.as_tensor(rng.integers(0, 4000, size=(4, 1024)).astype(np.int32), device="cuda")
-        if pipelined:
-            rl.update_rows_n(storage, idx)
-        else:
-            for k in range(4):
-                rl.update_rows(storage, idx[k])
-        torch.cuda.synchronize()
-        runs.append([t.cpu().numpy() for t in (rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf)])
-    assert all(np.array_equal(a, b) for a, b in zip(*runs))
-
-
 def test_update_matches_oracle_sequence():
     """Several fused cacto_update steps == the oracle's critic step -> actor step (new critic) ->
     target update sequence with Keras-Adam (RL.py:101-118)."""
