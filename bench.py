@@ -339,19 +339,17 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     long_region = None
     if long_k >= 5:
         lev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-        cuts = [j * long_k // 5 for j in range(6)]
+        cuts_l = [j * long_k // 5 for j in range(6)]
         barrier(world)
         lev[0].record()
         for j in range(5):
-            for _ in range(cuts[j + 1] - cuts[j]):
+            for _ in range(cuts_l[j + 1] - cuts_l[j]):
                 rl.rollout_batch(None, None, T, inputs=inputs, out=seq)
                 rl.rollout_rewards(out, n_d, T)
             lev[j + 1].record()
-        torch.cuda.synchronize()
-        rates = [steps_per_call * (cuts[j + 1] - cuts[j]) / (lev[j].elapsed_time(lev[j + 1]) * 1e-3) for j in range(5)]
-        long_region = dict(batches=long_k, seconds=lev[0].elapsed_time(lev[5]) * 1e-3, segment_rates=rates,
-                           median=sum_over_ranks(float(np.median(rates)), world),
-                           spread=float((max(rates) - min(rates)) / np.median(rates)))
+    # the W warmup steps follow the long region on the queue with no host synchronisation between
+    # them (its rates are read after the timed region), so the GPU does not idle before the timed
+    # region's own barrier
     for _ in range(W):
         step()
     # HIP events in the timed region: the 5 segment boundaries, and around the rollout kernel and the
@@ -381,6 +379,12 @@ def rollout_phase(rl, conf, env, R, K, W, world, rank):
     t1 = time.perf_counter()
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
+    if long_k >= 5:
+        rates = [steps_per_call * (cuts_l[j + 1] - cuts_l[j]) / (lev[j].elapsed_time(lev[j + 1]) * 1e-3)
+                 for j in range(5)]
+        long_region = dict(batches=long_k, seconds=lev[0].elapsed_time(lev[5]) * 1e-3, segment_rates=rates,
+                           median=sum_over_ranks(float(np.median(rates)), world),
+                           spread=float((max(rates) - min(rates)) / np.median(rates)))
     evs = [smp[k] for k in sampled]
     kern_ms = sum(e[0].elapsed_time(e[2]) for e in evs) / len(evs)
     seq_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
