@@ -515,12 +515,20 @@ def episode_to_buffer_phase(rl, conf, roll, env, K, dVdx=None):
                 algorithmic_bytes_per_row=row_bytes, achieved_GBps=rows * row_bytes / (ms * 1e-3) / 1e9)
 
 
+# untimed updates before each update phase's timed region, queued right before its barrier: the host
+# work between phases (buffer fills, index draws) idles the GPU, and a few warm-up updates left the
+# timed region's first segment below the settled rate (the rollout's timed region showed the same,
+# DESIGN.md §6)
+UPDATE_WARMUP = 200
+
+
 def update_phase(rl, buf, B, K, W, world, seed):
     """K learn_and_update iterations (RL.py:101-118 each) on pre-drawn minibatch indices, as the
     package's learn_and_update runs them: one RL_AC.update_rows_n call (the critic step of update
     t+1 overlaps the actor step of update t; bit-identical to K sequential updates). With --graph
     (one rank) the K updates replay as one HIP graph of the sequential loop instead. With N > 1
     ranks each update is the data-parallel one (RCCL all-reduce of both gradients)."""
+    W = max(W, UPDATE_WARMUP)
     gen = np.random.Generator(np.random.PCG64(seed))
     idx = torch.as_tensor(gen.integers(0, buf.max_idx(), size=(K + W, B)).astype(np.int32), device="cuda")
     if world == 1 and not USE_GRAPH:
@@ -583,6 +591,7 @@ def per_update_phase(rl, buf, B, K, W, world, seed):
     """learn_and_update with PER (RL.py:122-137): sample (stratified, IS weights) -> update ->
     priority update, with the per-step uniforms pre-drawn on the device, through the loop the
     product runs at this rank count (per_loop)."""
+    W = max(W, UPDATE_WARMUP)
     gen = np.random.Generator(np.random.PCG64(seed))
     U = torch.as_tensor(gen.random((K + W, B)), device="cuda")
     loop = per_loop(rl, world)
