@@ -77,6 +77,7 @@ _SIGS = {
     "cacto_update": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, C.c_int, vp, vp, vp,
                                vp, sz, vp]),
     "cacto_pipeline_status": (C.c_int, [vp, vp]),
+    "cacto_pipeline_check": (C.c_int, [vp, vp]),
     "cacto_update_n": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, C.c_int, C.c_int, vp, sz, vp]),
     "cacto_update_n_per": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, i64, i64, C.c_double, vp,
                                      vp, C.c_double, C.c_double, C.c_double, vp, C.c_int, C.c_int, vp, sz, vp]),

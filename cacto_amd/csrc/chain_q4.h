@@ -484,6 +484,7 @@ __device__ __forceinline__ void q4_actor_chain(Q4ActorLds& S, const int tile, co
     // the system copy (branch-free: clamped index, duplicates write the same value), issued right
     // after the rows so the first barrier's wait covers it and not the fragments
     constexpr int SDW = sizeof(SysDevice) / sizeof(double);
+    static_assert(SDW <= 8 * 64 && sizeof(SysDevice) % sizeof(double) == 0, "one double of SysDevice per thread");
     const int k = min(tid, SDW - 1);
     const double sv = reinterpret_cast<const double*>(sdp)[k];
     F1.load<true>(Ac.fwd(0), Ac.biasp(0), 16, 256, wave, lane);

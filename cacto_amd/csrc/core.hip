@@ -75,6 +75,32 @@ extern "C" int cacto_sys_create(const cacto_sys_params* params_h, const double* 
     }
     if (joint_table_h && p.dyn_kind == CACTO_DYN_CHAIN)
       std::memcpy(host.joints, joint_table_h, sizeof(double) * p.n_joints * CACTO_JOINT_COLS);
+    if (p.dyn_kind == CACTO_DYN_CHAIN && p.n_joints == 3 && p.gravity[0] == 0.0 && p.gravity[1] == 0.0) {
+      // planar 3R chain (the manipulator): closed-form M / h constants for the rollout (env.h planar3_step)
+      bool planar = true;
+      for (int i = 0; i < 3; ++i) {
+        const double* r = joint_table_h + i * CACTO_JOINT_COLS;
+        planar = planar && (int)r[1] == 0 && r[2] == 0.0 && r[3] == 0.0 && r[4] == 1.0;
+        for (int k = 0; k < 9; ++k) planar = planar && r[5 + k] == ((k % 4 == 0) ? 1.0 : 0.0);
+      }
+      if (planar) {
+        const double* J = joint_table_h;
+        auto col = [&](int i, int c) { return J[i * CACTO_JOINT_COLS + c]; };
+        double* pl = host.pl;
+        pl[0] = 1.0;
+        pl[1] = col(1, 14), pl[2] = col(1, 15);
+        pl[3] = col(2, 14), pl[4] = col(2, 15);
+        for (int k = 0; k < 3; ++k) {
+          pl[5 + 2 * k] = col(k, 18);
+          pl[6 + 2 * k] = col(k, 19);
+          pl[11 + k] = col(k, 17);
+        }
+        pl[14] = col(0, 26) + col(1, 26) + col(2, 26);
+        pl[15] = col(1, 26) + col(2, 26);
+        pl[16] = col(2, 26);
+        pl[17] = col(0, 17) * (col(0, 18) * col(0, 18) + col(0, 19) * col(0, 19));
+      }
+    }
     for (int r = 0; r < CACTO_MAX_STATE; ++r)  // IEEE double division: the same bits as on the device
       host.inv_norm[r] = r < p.nb_state && p.state_norm[r] != 0.0 ? 1.0 / p.state_norm[r] : 0.0;
     cacto_sys* s = new cacto_sys();
@@ -135,13 +161,8 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   for (hipEvent_t e : sys->ev_actor)
     if (e) (void)hipEventDestroy(e);
   if (sys->side) (void)hipStreamDestroy(sys->side);
-  if (sys->per_st) (void)hipStreamSynchronize(sys->per_st);
-  if (sys->ev_chain) (void)hipEventDestroy(sys->ev_chain);
-  if (sys->ev_samp) (void)hipEventDestroy(sys->ev_samp);
   if (sys->latch_host) (void)hipHostFree(sys->latch_host);
-  if (sys->per_st) (void)hipStreamDestroy(sys->per_st);
   if (sys->pipe_sig) (void)hipFree(sys->pipe_sig);
-  if (sys->pipe_wsig) (void)hipFree(sys->pipe_wsig);
   delete sys;
   return CACTO_OK;
 }

@@ -20,7 +20,117 @@ struct SysDevice {
   double cd_L[CACTO_MAX_JOINTS * CACTO_MAX_JOINTS];
   double cd_h[CACTO_MAX_JOINTS];
   double cd_Fu[CACTO_MAX_STATE * CACTO_MAX_ACTION];
+  // 3-joint planar chains (every joint revolute about z, identity placement rotations, no in-plane
+  // gravity: the manipulator): the link constants of the closed-form M(q) and h(q, v) the rollout
+  // kernels step with (planar3_step below), filled by cacto_sys_create; pl[0] = 1 when they apply
+  double pl[20];
 };
+
+// ------------------------------------------------------------------ planar 3R closed form
+// For a chain of revolute-z joints whose links move in the xy plane (Manipulator,
+// environment.py:654-734, conf_manipulator.py's planar_manipulator_3dof.urdf), M(q) and the bias
+// forces h(q, v) = C(q, v) v (gravity along z does no work) follow from the link COM positions:
+//   M_ij = sum_{k >= max(i,j)} m_k r_ik . r_jk + Izz_k,   h_i = sum_{k >= i} m_k r_ik x a_k,
+// with r_ik the vector from joint i to the COM of link k and a_k that COM's acceleration at
+// qdd = 0 (every link-fixed vector rotating at w_j = v_0 + ... + v_j contributes -w_j^2 times
+// itself). Everything is expressed in link 0's frame, so only q1, q2 enter. Equal to CRBA / RNEA
+// to rounding (the rollout tests hold it to 1e-12 of the oracle's Featherstone restatement).
+// Layout of SysDevice::pl (host: cacto_sys_create): [0] on, [1,2] joint-1 origin in link 0,
+// [3,4] joint-2 origin in link 1, [5..10] COM of links 0..2 in their frames, [11..13] masses,
+// [14] Izz_0 + Izz_1 + Izz_2, [15] Izz_1 + Izz_2, [16] Izz_2, [17] m_0 |c_0|^2.
+struct Planar3 {
+  double P0x, P0y, p2x, p2y, c0x, c0y, c1x, c1y, c2x, c2y, m0, m1, m2, I012, I12, I2, m0cc;
+  __device__ __forceinline__ explicit Planar3(const double* pl)
+      : P0x(pl[1]), P0y(pl[2]), p2x(pl[3]), p2y(pl[4]), c0x(pl[5]), c0y(pl[6]), c1x(pl[7]), c1y(pl[8]),
+        c2x(pl[9]), c2y(pl[10]), m0(pl[11]), m1(pl[12]), m2(pl[13]), I012(pl[14]), I12(pl[15]), I2(pl[16]),
+        m0cc(pl[17]) {}
+};
+
+// sin and cos of a joint angle: one Cody-Waite reduction by pi/2 (three-part constant, exact
+// products in the FMAs) and the FreeBSD k_sin / k_cos minimax kernels on |r| <= pi/4 (within an
+// ulp or so), the quadrant by selects — a third of the f64 instructions of the library sincos,
+// whose Payne-Hanek branch also cost the one-slot-per-wave rollout its registers. The reduction
+// stays accurate while x * 2/pi rounds to the nearest integer, |x| < 2^52 (a joint angle beyond
+// that has no meaningful phase); NaN / inf give NaN. Deterministic: every kernel that calls it for
+// the same x gets the same bits.
+__device__ __forceinline__ void joint_sincos(double x, double* sp, double* cp) {
+  const double n = rint(x * 0.63661977236758134308);
+  double r = fma(-n, 1.5707963267948966, x);
+  r = fma(-n, 6.123233995736766e-17, r);
+  r = fma(-n, -1.4973849048591698e-33, r);
+  const double z = r * r, w = z * z;
+  // k_sin
+  const double rs = fma(z, fma(z, 2.75573137070700676789e-06, -1.98412698298579493134e-04), 8.33333333332248946124e-03) +
+                    z * w * fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+  const double sr = fma(z * r, fma(z, rs, -1.66666666666666324348e-01), r);
+  // k_cos
+  const double rc = z * fma(z, fma(z, 2.48015872894767294178e-05, -1.38888888888741095749e-03), 4.16666666666666019037e-02) +
+                    w * w * fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09), -2.75573143513906633035e-07);
+  const double hz = 0.5 * z, wc = 1.0 - hz;
+  const double cr = wc + (((1.0 - wc) - hz) + z * rc);
+  const int q = (int)(n - 4.0 * floor(n * 0.25));  // n mod 4, exact for |n| < 2^53
+  const double ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+  *sp = (q & 2) ? -ss : ss;
+  *cp = ((q + 1) & 2) ? -cc : cc;
+}
+
+// Explicit Euler step of the planar 3R chain: qdd = M^-1 (a - h) by the adjugate (one division),
+// q' = q + v dt, v' = v + qdd dt, t' = t + dt, given (s1, c1, s2, c2) = sin / cos of q1, q2
+// (joint_sincos). Every rollout kernel that runs such a chain steps it with this function, so the
+// schedule never changes a result.
+__device__ __forceinline__ void planar3_step_sc(const Planar3& k, double dt, const double* s, const double* a,
+                                                double s1, double c1, double s2, double c2, double* out) {
+  const double c12 = fma(c1, c2, -(s1 * s2)), s12 = fma(s1, c2, c1 * s2);
+  // link-fixed vectors in link 0's frame: joint 1 -> joint 2 (P1), joint i -> COM i (Ci)
+  const double P1x = fma(k.p2x, c1, -(k.p2y * s1)), P1y = fma(k.p2x, s1, k.p2y * c1);
+  const double C1x = fma(k.c1x, c1, -(k.c1y * s1)), C1y = fma(k.c1x, s1, k.c1y * c1);
+  const double C2x = fma(k.c2x, c12, -(k.c2y * s12)), C2y = fma(k.c2x, s12, k.c2y * c12);
+  const double r01x = k.P0x + C1x, r01y = k.P0y + C1y;  // joint 0 -> COM 1
+  const double r12x = P1x + C2x, r12y = P1y + C2y;      // joint 1 -> COM 2
+  const double r02x = k.P0x + r12x, r02y = k.P0y + r12y;  // joint 0 -> COM 2
+  auto dot2 = [](double ax, double ay, double bx, double by) { return fma(ax, bx, ay * by); };
+  auto crs2 = [](double ax, double ay, double bx, double by) { return fma(ax, by, -(ay * bx)); };
+  const double M00 = fma(k.m2, dot2(r02x, r02y, r02x, r02y), fma(k.m1, dot2(r01x, r01y, r01x, r01y), k.m0cc)) + k.I012;
+  const double M01 = fma(k.m2, dot2(r02x, r02y, r12x, r12y), k.m1 * dot2(r01x, r01y, C1x, C1y)) + k.I12;
+  const double M02 = fma(k.m2, dot2(r02x, r02y, C2x, C2y), k.I2);
+  const double M11 = fma(k.m2, dot2(r12x, r12y, r12x, r12y), k.m1 * dot2(C1x, C1y, C1x, C1y)) + k.I12;
+  const double M12 = fma(k.m2, dot2(r12x, r12y, C2x, C2y), k.I2);
+  const double M22 = fma(k.m2, dot2(C2x, C2y, C2x, C2y), k.I2);
+  // COM accelerations at qdd = 0 (negated): w_j^2 times the link-fixed vectors on the way
+  const double w0 = s[3], w1 = w0 + s[4], w2 = w1 + s[5];
+  const double q0 = w0 * w0, q1 = w1 * w1, q2 = w2 * w2;
+  const double n0x = q0 * k.c0x, n0y = q0 * k.c0y;
+  const double b0x = q0 * k.P0x, b0y = q0 * k.P0y;
+  const double n1x = fma(q1, C1x, b0x), n1y = fma(q1, C1y, b0y);
+  const double n2x = fma(q2, C2x, fma(q1, P1x, b0x)), n2y = fma(q2, C2y, fma(q1, P1y, b0y));
+  const double h2 = -(k.m2 * crs2(C2x, C2y, n2x, n2y));
+  const double h1 = -fma(k.m1, crs2(C1x, C1y, n1x, n1y), k.m2 * crs2(r12x, r12y, n2x, n2y));
+  const double h0 = -fma(k.m0, crs2(k.c0x, k.c0y, n0x, n0y),
+                         fma(k.m1, crs2(r01x, r01y, n1x, n1y), k.m2 * crs2(r02x, r02y, n2x, n2y)));
+  // qdd = adj(M) (a - h) / det M
+  const double e0 = a[0] - h0, e1 = a[1] - h1, e2 = a[2] - h2;
+  const double A00 = fma(M11, M22, -(M12 * M12)), A01 = fma(M02, M12, -(M01 * M22)),
+               A02 = fma(M01, M12, -(M02 * M11)), A11 = fma(M00, M22, -(M02 * M02)),
+               A12 = fma(M01, M02, -(M00 * M12)), A22 = fma(M00, M11, -(M01 * M01));
+  const double r = 1.0 / fma(M00, A00, fma(M01, A01, M02 * A02));
+  const double d0 = fma(A00, e0, fma(A01, e1, A02 * e2)) * r;
+  const double d1 = fma(A01, e0, fma(A11, e1, A12 * e2)) * r;
+  const double d2 = fma(A02, e0, fma(A12, e1, A22 * e2)) * r;
+  out[0] = fma(s[3], dt, s[0]);
+  out[1] = fma(s[4], dt, s[1]);
+  out[2] = fma(s[5], dt, s[2]);
+  out[3] = fma(d0, dt, s[3]);
+  out[4] = fma(d1, dt, s[4]);
+  out[5] = fma(d2, dt, s[5]);
+  out[6] = s[6] + dt;
+}
+__device__ __forceinline__ void planar3_step(const Planar3& k, double dt, const double* s, const double* a,
+                                             double* out) {
+  double s1, c1, s2, c2;
+  joint_sincos(s[1], &s1, &c1);
+  joint_sincos(s[2], &s2, &c2);
+  planar3_step_sc(k, dt, s, a, s1, c1, s2, c2, out);
+}
 
 // ------------------------------------------------------------------ small 3-vector algebra
 struct V3 {

@@ -15,20 +15,19 @@ struct cacto_sys {
   hipStream_t side = nullptr;  // cacto_update_n's actor-step stream and its events
   hipEvent_t ev_critic = nullptr, ev_actor[3] = {nullptr, nullptr, nullptr};
   std::mutex pipe_mu;  // one two-stream pipeline at a time per handle (they share side / events)
-  // the PER pipeline's third stream (priority update + next sample beside the critic's GEMM and Adam)
-  // and its two events: the critic chain finished / the next sample is drawn
-  hipStream_t per_st = nullptr;
-  hipEvent_t ev_chain = nullptr, ev_samp = nullptr;
   // pinned host copy of pipe_sig[1] (the device waits' timeout latch), refreshed asynchronously at
-  // the end of every pipelined call and checked at the start of the next one
+  // the end of every pipelined call with device-side waits; read (and cleared) by
+  // cacto_pipeline_check after a stream synchronisation, refused on at the start of the next call
   unsigned long long* latch_host = nullptr;
-  // device-side ordering of the two-stream pipeline (CACTO_PIPE_DEVWAIT): pipe_sig[0] counts the actor
-  // iterations whose chain has finished, [2] the critic Adam steps finished (both monotonic over the
-  // handle's life), [1] latches a wait that timed out, [3] is k_adam's last-workgroup counter;
-  // pipe_seq is the host's count of pipeline iterations issued before this call
+  // device-side ordering of the two-stream pipeline: pipe_sig[0] counts the actor iterations whose
+  // chain has finished, [2] the critic Adam steps finished (both monotonic over the handle's life),
+  // [1] latches a wait that timed out, [3] is k_adam's last-workgroup counter, [4..7] the one-time
+  // concurrency probe's words; pipe_seq is the host's count of pipeline iterations issued before
+  // this call; pipe_probe: -1 not run yet, 0 the streams' kernels did not run concurrently (queue
+  // markers), 1 they did (device-side waits)
   unsigned long long* pipe_sig = nullptr;
-  unsigned long long* pipe_wsig = nullptr;  // CACTO_PIPE_SIGNAL: hipStreamWaitValue64 word (signal memory)
   unsigned long long pipe_seq = 0;
+  int pipe_probe = -1;
   // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (layer << 16 | net << 15 | item, -1 = none), for
   // the critic alone, the actor alone and both (built at creation, cacto_build_wgrad_adam_items)
   int32_t* wa_items[3] = {nullptr, nullptr, nullptr};

@@ -11,6 +11,7 @@
 //   -> k_wgrad: one wave per (layer, 16x16 output tile | bias tile, row chunk) -> slab[chunk][P]
 //   -> k_adam : sum chunks in fixed order (deterministic), Adam, packed copies, soft update.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <vector>
 
@@ -51,21 +52,16 @@ struct ChainScalars {
   int MC;
   int B_global;
   int want_vt;
-  // the two-stream pipeline's device-side ordering (CACTO_PIPE_DEVWAIT): the actor chain waits, before
-  // its critic pass at s', until *wait_p >= wait_v (the critic's Adam of the same update has run)
+  // the two-stream pipeline's device-side ordering (DESIGN §3 "memory-ordering contract"): the actor
+  // chain waits, before its critic pass at s', until *wait_p >= wait_v (the critic's Adam of the same
+  // update has run) — a relaxed poll, no fence: the Adam wrote the critic through to memory at agent
+  // scope and published after its stores completed, and no L2 holds a line of the buffer from before
+  // (kernel starts invalidate; nothing reads it in between)
   const unsigned long long* wait_p;
   unsigned long long wait_v;
-  // 1 (CACTO_PIPE_DEVWAIT=3): that wait with a relaxed load and no fence — the Adam wrote the critic
-  // through to memory at agent scope and published after its stores completed, and no L2 holds a
-  // line of the buffer from before (kernel starts invalidate; nothing reads it in between)
-  int wait_relaxed;
   // 1 (the PER loops): that wait at the chain's start, before it gathers the sampled rows (the
   // sample of the update precedes the critic's Adam on the other stream)
   int wait_at_start;
-  // the 16-sample actor chain issued as launches of at most `split` tiles (0: one launch), blk0 the
-  // first tile block of this launch: with the device-side wait above, no launch holds more workgroups
-  // than the chip has CUs, so a CU always fits the critic stream's chain beside the waiting tiles
-  int split, blk0;
   // 1: the 16-sample tiles dealt so that the tiles of one 256-row GEMM chunk run on the XCD that
   // k_wgrad_big runs that chunk on (chain_tile_of)
   int xcd_tiles;
@@ -83,20 +79,42 @@ __device__ __forceinline__ int chain_tile_of(int b, int ntiles, int xcd_tiles) {
 
 // The device-side waits of the pipeline: until *wait_p >= wait_v (normally already true: one load).
 // Bounded: after ~2^22 polls (seconds) the wait gives up and latches the timeout word, so an
-// ordering bug cannot hang the GPU. The signal words live in cacto_sys::pipe_sig: [0] actor chains
-// finished, [1] timeout latch, [2] critic Adam steps finished, [3] k_adam's last-workgroup counter.
-// ACQ = false: a write-after-read order (the critic's Adam may overwrite what an actor chain read
-// once that chain has finished) — no data flows, so relaxed polls suffice and no L2 maintenance is
-// paid. ACQ = true: the actor chain reads what the critic's Adam wrote (acquire; the caller fences).
-template <bool ACQ>
+// ordering bug cannot hang the GPU; the host then fails the call (cacto_pipeline_check). The signal
+// words live in cacto_sys::pipe_sig: [0] actor chains finished, [1] timeout latch, [2] critic Adam
+// steps finished, [3] k_adam's last-workgroup counter, [4..7] the concurrency probe's words. Relaxed
+// polls: the write-after-read order (the critic's Adam may overwrite what an actor chain read once
+// that chain has finished) carries no data; for the read-after-write order (the actor chain reads
+// what the critic's Adam wrote) the Adam's stores went through to memory before it published (see
+// ChainScalars and DESIGN §3's memory-ordering contract).
 __device__ __forceinline__ void pipe_wait(const unsigned long long* wait_p, unsigned long long wait_v,
                                           unsigned long long* latch) {
   if (!wait_p) return;
   for (int k = 0; k < (1 << 22); ++k) {
-    if (__hip_atomic_load(wait_p, ACQ ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= wait_v) return;
+    if (__hip_atomic_load(wait_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= wait_v) return;
     __builtin_amdgcn_s_sleep(2);
   }
   __hip_atomic_store(latch, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One-time probe per handle (cacto_update_n[_per]'s first two-stream call): can a kernel on the side
+// stream and one on the caller's stream run at the same time? Role 0 (side) raises flag w[4] and
+// polls for w[5]; role 1 (caller's stream) polls for w[4], then raises w[5]. Each records in w[6 +
+// role] whether its poll succeeded (bounded: ~2^14 polls). When the device serializes kernels
+// (AMD_SERIALIZE_KERNEL, HIP_LAUNCH_BLOCKING, counter collection) the first of the two to run cannot
+// see the other's flag, so a device-side wait would spin until its bound: the pipeline then orders
+// the streams with queue markers.
+__global__ void k_pipe_probe(unsigned long long* w, int role) {
+  if (threadIdx.x != 0) return;
+  unsigned long long* mine = w + 4 + role;
+  const unsigned long long* other = w + 5 - role;
+  if (role == 0) __hip_atomic_store(mine, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long ok = 0;
+  for (int k = 0; k < (1 << 14) && !ok; ++k) {
+    ok = __hip_atomic_load(other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!ok) __builtin_amdgcn_s_sleep(2);
+  }
+  if (role == 1) __hip_atomic_store(mine, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 6 + role, ok ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void store_panel(float* base, int ld, int row, int t, int g, float4 v) {
@@ -578,14 +596,8 @@ __device__ __forceinline__ void actor_chain(ActorLds& S, const int tile, const S
   __syncthreads();
   CSTAMP(3);
   if (L.wave == 0) fill_input_tile(p, stn, XS, L);
-  if (cs.wait_p) {  // pipeline: the critic this pass reads is written by the other stream's Adam
-    if (cs.wait_relaxed) {
-      if (L.tid == 0) pipe_wait<false>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
-    } else {
-      if (L.tid == 0) pipe_wait<true>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
-      __threadfence();  // acquire at agent scope: no stale L1 / L2 line of that critic buffer
-    }
-  }
+  // pipeline: the critic this pass reads is written by the other stream's Adam
+  if (cs.wait_p && L.tid == 0) pipe_wait(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
   __syncthreads();
   // critic (already updated) at s': V and dV/dx0 (NeuralNetwork.py:190-195)
   float4* HC = H;            // 16 tiles
@@ -669,12 +681,11 @@ __global__ void __launch_bounds__(CACTO_THREADS) __attribute__((amdgpu_waves_per
   __shared__ ActorLds S;
   ChainScalars c = cs;
   if (cs.wait_p && cs.wait_at_start) {
-    if (threadIdx.x == 0) pipe_wait<false>(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
+    if (threadIdx.x == 0) pipe_wait(cs.wait_p, cs.wait_v, const_cast<unsigned long long*>(cs.wait_p) - 1);
     __syncthreads();
     c.wait_p = nullptr;
   }
-  actor_chain<NJ>(S, chain_tile_of(blockIdx.x + cs.blk0, gridDim.x, cs.xcd_tiles), sdp, Ac, C, c, storage, idx, B, gb,
-                  step);
+  actor_chain<NJ>(S, chain_tile_of(blockIdx.x, gridDim.x, cs.xcd_tiles), sdp, Ac, C, c, storage, idx, B, gb, step);
 }
 
 // The critic chain of update t (workgroups [0, nct)) and the actor chain of update t - 1 (the
@@ -1162,25 +1173,10 @@ __device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int
 // the partials are still summed in chunk order (bit-identical). NCH = 0: any chunk count.
 //
 // wait_p / wait_v: the pipeline's wait before overwriting a critic buffer an actor chain of the other
-// stream read (k_wgrad's sig_p publishes those chains). sig_p / sig_v: after its stores the last
-// workgroup to finish publishes sig_p[2] = sig_v (this Adam step done) for the actor chain's wait.
-__device__ __forceinline__ void adam_publish(unsigned long long* sig_p, unsigned long long sig_v) {
-  if (!sig_p) return;
-  __shared__ int last;
-  __threadfence();  // release this workgroup's stores at agent scope
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(sig_p + 3, 1ull) == (unsigned long long)(gridDim.x - 1);
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    sig_p[3] = 0ull;
-    __threadfence();
-    __hip_atomic_store(sig_p + 2, sig_v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// One parameter per thread, workgroup blk (NCH > 0).
-// The same publication for write-through stores (CACTO_PIPE_DEVWAIT=3): every thread's stores have
-// completed (waitcnt) before its workgroup counts itself; no fence, no L2 write-back.
+// stream read (k_wgrad's sig_p publishes those chains). sig_p / sig_v: after its stores (written
+// through to memory, `thru`) the last workgroup to finish publishes sig_p[2] = sig_v (this Adam step
+// done) for the actor chain's wait: every thread's stores have completed (waitcnt) before its
+// workgroup counts itself; no fence, no L2 write-back.
 // nblk: the Adam step's workgroups (the launch's, or the leading part of k_adam_sample's).
 __device__ __forceinline__ void adam_publish_thru(unsigned long long* sig_p, unsigned long long sig_v, int nblk) {
   if (!sig_p) return;
@@ -1213,7 +1209,7 @@ __device__ __forceinline__ void adam_nch_body(const int blk, const float* __rest
   th0 = src[pc];
   if (a.soft) tg0 = target[pc];
   const AdamScalars s = adam_scalars(a, step);
-  pipe_wait<false>(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);  // the loads above are in flight
+  pipe_wait(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);  // the loads above are in flight
   if (p0 < t.params) {
     float g = q[0];
 #pragma unroll
@@ -1251,7 +1247,7 @@ __global__ void __launch_bounds__(256) k_adam_sample(const float* __restrict__ s
   if ((int)blockIdx.x < nadam) {
     adam_nch_body<NCH>(blockIdx.x, slab, nch, t, src, netbuf, packed, m, v, step, a, target, target_packed, wait_p,
                        wait_v, thru != 0);
-    adam_publish_thru(sig_p, sig_v, nadam);  // (sig_p only with write-through stores; the host checks)
+    adam_publish_thru(sig_p, sig_v, nadam);  // (sig_p only with write-through stores)
   } else
     per_sample_body<PER_FUSED_TOP>(blockIdx.x - nadam, sa, top_s, scal_s);
 }
@@ -1266,8 +1262,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
   if constexpr (NCH > 0) {
     adam_nch_body<NCH>(blockIdx.x, slab, nch, t, src, netbuf, packed, m, v, step, a, target, target_packed, wait_p,
                        wait_v, thru != 0);
-    if (thru) adam_publish_thru(sig_p, sig_v, gridDim.x);
-    else adam_publish(sig_p, sig_v);
+    adam_publish_thru(sig_p, sig_v, gridDim.x);  // (sig_p only with write-through stores)
     return;
   }
   const int it = step[a.which];  // = Keras iterations + 1
@@ -1283,7 +1278,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
   const float alpha = fdiv(fmul((float)lr, __fsqrt_rn(fsub(1.f, b2p))), fsub(1.f, b1p));
   const float c1 = (float)(1.0 - a.beta1), c2 = (float)(1.0 - a.beta2), eps = (float)a.eps;
   const float tau = (float)a.tau, omt = (float)(1.0 - a.tau);
-  pipe_wait<false>(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);
+  pipe_wait(wait_p, wait_v, const_cast<unsigned long long*>(wait_p) + 1);
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < t.params; p += gridDim.x * blockDim.x) {
     // chunk partials summed in chunk order; loads issued 8 at a time so they overlap
     float g = slab[p];
@@ -1310,8 +1305,7 @@ __global__ void __launch_bounds__(256) k_adam(const float* __restrict__ slab, in
       write_packed(target_packed, t, p, tg);
     }
   }
-  if (thru) adam_publish_thru(sig_p, sig_v, gridDim.x);
-  else adam_publish(sig_p, sig_v);
+  adam_publish_thru(sig_p, sig_v, gridDim.x);
 }
 
 __global__ void __launch_bounds__(256) k_soft(NetTopo t, const float* __restrict__ src, float* target,
@@ -1666,13 +1660,8 @@ struct LaunchActorChain {
       hipLaunchKernelGGL(k_actor_grad_q4<NJ>, dim3(Bp / Q4_TILE), dim3(Q4_THREADS), 0, st, sys->dev, Ac, C, cs,
                          storage, idx, B, gb, step);
     else
-      for (int b0 = 0; b0 < Bp / 16; b0 += cs.split > 0 ? cs.split : Bp / 16) {
-        ChainScalars c = cs;
-        c.blk0 = b0;
-        const int n = cs.split > 0 ? std::min(cs.split, Bp / 16 - b0) : Bp / 16;
-        hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(n), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, c, storage, idx, B,
-                           gb, step);
-      }
+      hipLaunchKernelGGL(k_actor_grad<NJ>, dim3(Bp / 16), dim3(CACTO_THREADS), 0, st, sys->dev, Ac, C, cs, storage, idx,
+                         B, gb, step);
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
   }
@@ -1904,10 +1893,7 @@ ChainScalars chain_scalars(const cacto_update_cfg* cfg, int B) {
   cs.want_vt = cfg->want_target_V;
   cs.wait_p = nullptr;
   cs.wait_v = 0;
-  cs.wait_relaxed = 0;
   cs.wait_at_start = 0;
-  cs.split = 0;
-  cs.blk0 = 0;
   // CACTO_CHAIN_XCD=0 keeps the tiles in block order (A/B; read once)
   static const bool xcd_env = [] {
     const char* e = std::getenv("CACTO_CHAIN_XCD");
@@ -1970,15 +1956,13 @@ int launch_critic_chain_and_wgrad(const cacto_sys* sys, const cacto_nets* nets, 
 int launch_actor_chain(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                        const double* storage, const int32_t* idx, int B, const Workspace& w, hipStream_t st,
                        const unsigned long long* wait_p = nullptr, unsigned long long wait_v = 0,
-                       int wait_relaxed = 0, int wait_at_start = 0, int split = 0) {
+                       int wait_at_start = 0) {
   NetView Ac = cacto_make_view(sys, CACTO_NET_ACTOR, nets->actor_d);
   NetView C = cacto_make_view(sys, CACTO_NET_CRITIC, nets->critic_d);
   ChainScalars cs = chain_scalars(cfg, B);
   cs.wait_p = wait_p;
   cs.wait_v = wait_v;
-  cs.wait_relaxed = wait_relaxed;
   cs.wait_at_start = wait_at_start;
-  cs.split = split;
   return dispatch_nj<LaunchActorChain>(sys->host.p, sys, Ac, C, cs, storage, idx, B, w.act, nets->step_d, st);
 }
 
@@ -2453,48 +2437,20 @@ int ensure_side_stream(cacto_sys* ms) {
   if (ms->side) return CACTO_OK;
   hipStream_t side = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  // CACTO_SIDE_PRIO=hi|lo: the side (actor) stream at the device's greatest / least priority
-  // (read once; benchmarks). Default: normal priority.
-  int prio = 0, least = 0, greatest = 0;
-  if (const char* pe = std::getenv("CACTO_SIDE_PRIO")) {
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-      prio = pe[0] == 'h' ? greatest : pe[0] == 'l' ? least : 0;
-  }
-  hipError_t e = hipStreamCreateWithPriority(&side, hipStreamNonBlocking, prio);
-  // device-scope events (CACTO_EVENT_SYSFENCE=1 restores the system-scope fence): every
-  // producer and consumer of these dependencies is a kernel on this device
-  const unsigned evf = hipEventDisableTiming | (std::getenv("CACTO_EVENT_SYSFENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+  hipError_t e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+  // device-scope events: every producer and consumer of these dependencies is a kernel on this device
+  const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
   for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], evf);
-  if (e != hipSuccess) {
-    for (hipEvent_t x : ev)
-      if (x) (void)hipEventDestroy(x);
-    if (side) (void)hipStreamDestroy(side);
-    return hip_fail(e, "cacto_update_n: side stream / events");
-  }
   unsigned long long* sig = nullptr;
-  if (e == hipSuccess) e = hipMalloc(&sig, 4 * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemset(sig, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&sig, 8 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(sig, 0, 8 * sizeof(unsigned long long));
   if (e != hipSuccess) {
     if (sig) (void)hipFree(sig);
     for (hipEvent_t x : ev)
       if (x) (void)hipEventDestroy(x);
     if (side) (void)hipStreamDestroy(side);
-    return hip_fail(e, "cacto_update_n: pipeline signal");
+    return hip_fail(e, "cacto_update_n: side stream / events / pipeline signal");
   }
-  // the side stream's wait word for CACTO_PIPE_SIGNAL (stream memory operations need signal memory);
-  // optional: without it the events are used
-  unsigned long long* wsig = nullptr;
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&wsig), sizeof(unsigned long long), hipMallocSignalMemory) ==
-      hipSuccess) {
-    if (hipMemset(wsig, 0, sizeof(unsigned long long)) != hipSuccess) {
-      (void)hipFree(wsig);
-      wsig = nullptr;
-    }
-  } else {
-    wsig = nullptr;
-    (void)hipGetLastError();
-  }
-  ms->pipe_wsig = wsig;
   ms->pipe_sig = sig;
   ms->pipe_seq = 0;
   ms->ev_critic = ev[0];
@@ -2505,62 +2461,76 @@ int ensure_side_stream(cacto_sys* ms) {
   return CACTO_OK;
 }
 
-// The PER stream and its two events (created on first use, published only when all exist).
-int ensure_per_stream(cacto_sys* ms) {
-  if (ms->per_st) return CACTO_OK;
-  hipStream_t ps = nullptr;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  const unsigned evf = hipEventDisableTiming | (std::getenv("CACTO_EVENT_SYSFENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
-  hipError_t e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
-  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ev[k], evf);
-  if (e != hipSuccess) {
-    for (hipEvent_t x : ev)
-      if (x) (void)hipEventDestroy(x);
-    if (ps) (void)hipStreamDestroy(ps);
-    return hip_fail(e, "cacto_update_n_per: PER stream / events");
-  }
-  ms->ev_chain = ev[0];
-  ms->ev_samp = ev[1];
-  ms->per_st = ps;
-  return CACTO_OK;
-}
-
-// CACTO_PER_STREAM (default 1): the pipelined PER loop runs the priority update of update t and the
-// sample of update t + 1 on a third stream, beside the critic's GEMM and Adam of update t (their
-// only common input is critic chain t; the next critic chain needs both). 0: all on the critic stream.
-bool per_stream_on() {
-  static const bool v = [] {
-    const char* e = std::getenv("CACTO_PER_STREAM");
-    return !(e && e[0] == '0');
+// How the two streams of this call are ordered: true = device-side waits (the default), false = queue
+// markers (event record / wait). CACTO_PIPE_DEVWAIT=0 / 1 forces markers / device waits (read once;
+// A/B and the timeout test). Otherwise markers when kernels are serialized by the environment
+// (AMD_SERIALIZE_KERNEL, HIP_LAUNCH_BLOCKING) or when the handle's one-time concurrency probe failed
+// (k_pipe_probe; e.g. counter collection). Always markers while `st` is being captured into a graph:
+// the waits compare device counters with absolute targets baked into the launches, and a replayed
+// graph would find its targets already reached.
+int pipe_devwait(cacto_sys* ms, hipStream_t st, bool* out) {
+  static const int env = [] {
+    const char* e = std::getenv("CACTO_PIPE_DEVWAIT");
+    if (e) return std::atoi(e) != 0 ? 1 : 0;
+    const char* s1 = std::getenv("AMD_SERIALIZE_KERNEL");
+    const char* s2 = std::getenv("HIP_LAUNCH_BLOCKING");
+    if ((s1 && std::atoi(s1) != 0) || (s2 && std::atoi(s2) != 0)) return 0;
+    return -1;  // probe
   }();
-  return v;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  CACTO_CHECK_HIP(hipStreamIsCapturing(st, &cap));
+  if (cap != hipStreamCaptureStatusNone) {
+    *out = false;
+    return CACTO_OK;
+  }
+  if (env >= 0) {
+    *out = env == 1;
+    return CACTO_OK;
+  }
+  if (ms->pipe_probe < 0) {
+    // both probe kernels start after everything already queued on `st`; the side one first
+    unsigned long long* w = ms->pipe_sig;
+    CACTO_CHECK_HIP(hipMemsetAsync(w + 4, 0, 4 * sizeof(unsigned long long), st));
+    CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+    CACTO_CHECK_HIP(hipStreamWaitEvent(ms->side, ms->ev_critic, 0));
+    hipLaunchKernelGGL(k_pipe_probe, dim3(1), dim3(64), 0, ms->side, w, 0);
+    CACTO_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_pipe_probe, dim3(1), dim3(64), 0, st, w, 1);
+    CACTO_CHECK_HIP(hipGetLastError());
+    CACTO_CHECK_HIP(hipStreamSynchronize(ms->side));
+    CACTO_CHECK_HIP(hipStreamSynchronize(st));
+    unsigned long long ok[2] = {0, 0};
+    CACTO_CHECK_HIP(hipMemcpy(ok, w + 6, sizeof(ok), hipMemcpyDeviceToHost));
+    ms->pipe_probe = ok[0] && ok[1] ? 1 : 0;
+  }
+  *out = ms->pipe_probe == 1;
+  return CACTO_OK;
 }
 
 int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                          const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
-                         const Workspace& w, hipStream_t st, int* cbuf);
+                         const Workspace& w, hipStream_t st, int* cbuf, bool devwait);
 
 int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg, const double* storage_d,
                     const int32_t* idx_d, const PerArgs* per, int K, int B, const Workspace& w, hipStream_t st) {
   cacto_sys* ms = const_cast<cacto_sys*>(sys);
   std::lock_guard<std::mutex> lock(ms->pipe_mu);
   if (int e = ensure_side_stream(ms)) return e;
-  if (per && per_stream_on())
-    if (int e = ensure_per_stream(ms)) return e;
   if (!ms->latch_host) {
     CACTO_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&ms->latch_host), sizeof(unsigned long long),
                                   hipHostMallocDefault));
     *ms->latch_host = 0;
   }
-  // a device-side wait of an earlier call timed out (its copy of the latch has landed by now, or
-  // the next call sees it): the device-side order cannot be trusted, so fail loudly — that happens
-  // when kernels are serialized (AMD_SERIALIZE_KERNEL, counter collection), where the waiting
-  // kernel holds the queue its producer needs; CACTO_PIPE_DEVWAIT=0 uses queue markers instead
+  // a device-side wait of an earlier call timed out and nobody has collected it with
+  // cacto_pipeline_check (the Python layer does at the end of every learn_and_update and before
+  // every checkpoint save): refuse to build on results whose order cannot be trusted
   if (*reinterpret_cast<volatile unsigned long long*>(ms->latch_host)) {
-    set_error("cacto_update_n: a device-side pipeline wait timed out (kernels serialized?); results of that call "
-              "are not trustworthy — run with CACTO_PIPE_DEVWAIT=0");
+    set_error("cacto_update_n: a device-side pipeline wait of an earlier call timed out (kernels serialized?); its "
+              "results are not trustworthy — collect it with cacto_pipeline_check, or run with CACTO_PIPE_DEVWAIT=0");
     return CACTO_EINVAL;
   }
+  bool devwait = false;
+  if (int e = pipe_devwait(ms, st, &devwait)) return e;
   const NetTopo& tc = sys->critic;
   const size_t nb_bytes = ((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256) * sizeof(float);
   const size_t nb_stride = align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
@@ -2568,19 +2538,16 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
   CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow + nb_stride, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));  // everything the caller queued before
   CACTO_CHECK_HIP(hipStreamWaitEvent(ms->side, ms->ev_critic, 0));
-  if (per && per_stream_on()) CACTO_CHECK_HIP(hipStreamWaitEvent(ms->per_st, ms->ev_critic, 0));
   // cbuf: the buffer (0 caller's, 1-2 workspace) holding the newest critic; on every exit, error or
   // not, the side stream joins the caller's stream and the newest critic lands in the caller's buffer
   int cbuf = 0;
-  const int err = update_pipeline_body(sys, nets, cfg, storage_d, idx_d, per, K, B, w, st, &cbuf);
+  const int err = update_pipeline_body(sys, nets, cfg, storage_d, idx_d, per, K, B, w, st, &cbuf, devwait);
   CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, ms->side));
   CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
-  CACTO_CHECK_HIP(hipMemcpyAsync(ms->latch_host, ms->pipe_sig + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                 st));
-  if (per && per_stream_on()) {
-    CACTO_CHECK_HIP(hipEventRecord(ms->ev_samp, ms->per_st));
-    CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_samp, 0));
-  }
+  // the timeout latch's host copy, read by cacto_pipeline_check after a synchronisation of `st`
+  if (devwait)
+    CACTO_CHECK_HIP(hipMemcpyAsync(ms->latch_host, ms->pipe_sig + 1, sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, st));
   if (cbuf)
     CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow + (cbuf - 1) * nb_stride, nb_bytes,
                                    hipMemcpyDeviceToDevice, st));
@@ -2589,7 +2556,7 @@ int update_pipeline(const cacto_sys* sys, const cacto_nets* nets, const cacto_up
 
 int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                          const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
-                         const Workspace& w, hipStream_t st, int* cbuf) {
+                         const Workspace& w, hipStream_t st, int* cbuf, bool devwait) {
   cacto_sys* ms = const_cast<cacto_sys*>(sys);
   hipStream_t side = ms->side;
   const size_t nb_stride = align64((size_t)flat_span(sys->critic) + (size_t)2 * sys->critic.blocks * 256);
@@ -2597,79 +2564,40 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
   float* const y = w.scal;
   float* const V = w.scal + w.Bp;
   const bool late_count = per && B >= cacto_per_mw_min();  // exp_counter += 1 just before the priority update
-  // every other iteration with PER (car_park B = 4096: 9.04 k -> 9.36 k updates/s), every iteration
-  // without (manipulator B = 8192 lost 8 % to the tighter wait); CACTO_PIPE_EVERY2=0 / 1 forces it
-  // (read once; benchmarks)
-  static const int every2_env = [] {
-    const char* e = std::getenv("CACTO_PIPE_EVERY2");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
-  const bool every2 = every2_env >= 0 ? every2_env == 1 : per != nullptr;
-  // CACTO_PIPE_DEVWAIT >= 1: the critic stream's ordering against the side stream without queue
-  // markers — the actor's GEMM (the launch after each actor chain) publishes the count of finished
-  // actor chains on the device, and the critic's Adam(t) polls it (pipe_wait) before overwriting the
-  // buffer actor chain(t-3) read; the PER index ring has four buffers, so the sampler of update t
-  // overwrites the one actor chain(t-4) read, which Adam(t-1)'s wait covers. Read once; A/B.
-  // 1 measured r05 (1 MI355X, updates/s): DI B = 4096 12.3 k -> 12.7 k, car_park PER B = 4096 9.88 k ->
-  // 9.98 k, manipulator B = 8192 7.70 k -> 7.68 k; the default is 3 (below); CACTO_PIPE_DEVWAIT=0
-  // restores the queue markers
-  static const int devwait_env = [] {
-    const char* e = std::getenv("CACTO_PIPE_DEVWAIT");
-    if (e) return std::atoi(e);
-    // serialized kernels (each waits for the previous one to finish) would leave a polling kernel
-    // holding the queue its producer needs: queue markers then
-    const char* s1 = std::getenv("AMD_SERIALIZE_KERNEL");
-    const char* s2 = std::getenv("HIP_LAUNCH_BLOCKING");
-    if ((s1 && std::atoi(s1) != 0) || (s2 && std::atoi(s2) != 0)) return 0;
-    return 3;
-  }();
-  const bool devwait = devwait_env >= 1;
-  // ... and the side stream's wait on the critic's Adam too (k_adam's last workgroup publishes, the
-  // actor chain polls just before its critic pass at s' — its actor forward, dynamics and d r / d a
-  // run first), where that cannot starve the critic stream of CUs: 16-sample actor tiles (the q4
-  // chains take no wait), at most one actor workgroup per CU (a CU holding one actor workgroup still
-  // fits a critic chain, GEMM or Adam workgroup beside it, so the critic stream always progresses);
-  // with 2, no PER (the actor chain gathers the sampled rows at its start).
-  // (CACTO_PIPE_DEVWAIT=2; measured r05: DI B = 4096 10.8 k -> 7.5 k updates/s — the acquire side's
-  // agent-scope L2 invalidations and the Adam's releases cost more than the queue marker they replace)
-  // CACTO_PIPE_DEVWAIT=3 (default): that wait without fences — the critic's Adam writes the weights
-  // through to memory at agent scope and publishes after its stores completed, the chain polls
-  // relaxed; with PER too, the chain polling at its start (before it gathers the sampled rows)
-  // CACTO_ACTOR_SPLIT=1 (with =3): a chain of more tiles than CUs issued as launches of at most the CU
-  // count rounded down to 128 tiles (the XCD dealing's period), so it can wait on the device too.
-  // Measured (updates/s): manipulator B = 8192 8.35 k -> 7.31 k — the halves no longer overlap the
-  // critic stream as one launch does — so it is off by default (read once; A/B).
-  static const bool split_env = [] {
-    const char* e = std::getenv("CACTO_ACTOR_SPLIT");
-    return e && e[0] == '1';
-  }();
-  const int split_n = split_env ? cu_count() / 128 * 128 : 0;
-  const bool devwait_actor = devwait_env >= 2 && (!per || devwait_env >= 3) && chain_tile(w.Bp) == CACTO_TILE &&
-                             (w.Bp / CACTO_TILE <= cu_count() || (devwait_env >= 3 && split_n > 0));
-  const int thru = devwait_actor && devwait_env >= 3 ? 1 : 0;
-  const int asplit = thru && w.Bp / CACTO_TILE > cu_count() ? split_n : 0;
+  // queue markers (devwait off): every other iteration with PER (car_park B = 4096: 9.04 k -> 9.36 k
+  // updates/s), every iteration without (manipulator B = 8192 lost 8 % to the tighter wait)
+  const bool every2 = per != nullptr;
+  // devwait: the critic stream's ordering against the side stream without queue markers — the
+  // actor's GEMM (the launch after each actor chain) publishes the count of finished actor chains on
+  // the device, and the critic's Adam(t) polls it (pipe_wait) before overwriting the buffer actor
+  // chain(t-3) read; the PER index ring has four buffers, so the sampler of update t overwrites the
+  // one actor chain(t-4) read, which Adam(t-1)'s wait covers. Measured r05 (1 MI355X, updates/s): DI
+  // B = 4096 12.3 k -> 12.7 k, car_park PER B = 4096 9.88 k -> 9.98 k, manipulator B = 8192 unchanged.
+  // ... and the side stream's wait on the critic's Adam too (devwait_actor): the critic's Adam writes
+  // the weights through to memory at agent scope and publishes after its stores completed, the actor
+  // chain polls relaxed just before its critic pass at s' (with PER at its start, before it gathers
+  // the sampled rows) — where that cannot starve the critic stream of CUs: 16-sample actor tiles (the
+  // q4 chains take no wait), at most one actor workgroup per CU (a CU holding one actor workgroup
+  // still fits a critic chain, GEMM or Adam workgroup beside it, so the critic stream always
+  // progresses). DI B = 4096 13.2-13.3 k -> 14.2-14.4 k updates/s (r05).
+  const bool devwait_actor = devwait && chain_tile(w.Bp) == CACTO_TILE && w.Bp / CACTO_TILE <= cu_count();
+  const int thru = devwait_actor ? 1 : 0;
   unsigned long long* const sig = ms->pipe_sig;
-  // CACTO_PIPE_SIGNAL=1: the side stream's wait on the critic's Adam as a stream write / wait-value
-  // pair on a signal-memory word instead of an event record / wait (A/B; read once)
-  static const bool sig_env = [] {
-    const char* e = std::getenv("CACTO_PIPE_SIGNAL");
-    return e && e[0] == '1';
-  }();
-  const bool streamval = sig_env && ms->pipe_wsig && !devwait_actor;
-
-  // the PER stream (per_stream_on) with the device-side write-after-read order: the index ring has
-  // five buffers — sample t + 1 runs after critic chain t, which follows Adam(t - 1)'s wait for actor
-  // chain t - 4, the last reader of the buffer it overwrites
-  // the overlapped form (per_overlap_ok): priority update t inside the critic GEMM's launch, sample
-  // t + 1 inside its Adam's; the same five-buffer ring (sample t + 1 runs in the launch after the
-  // Adam(t - 1) that waited for actor chain t - 4)
+  // the overlapped PER form (per_overlap_ok): priority update t inside the critic GEMM's launch,
+  // sample t + 1 inside its Adam's; the index ring has five buffers (sample t + 1 runs in the launch
+  // after the Adam(t - 1) that waited for actor chain t - 4). Otherwise the sample and the priority
+  // update run on the critic stream between its launches.
   const bool ovl = per && devwait && per_overlap_ok(sys, cfg, per, B, w);
-  const bool pst = per && devwait && !ovl && ms->per_st && per_stream_on();
-  hipStream_t pst_s = ms->per_st;
-  const int nring = (pst || ovl) ? 5 : devwait ? 4 : 3;
+  const int nring = ovl ? 5 : devwait ? 4 : 3;
   const int nroot = per ? (int)(per->cap / PER_RUN_SUB) : 0;
   const unsigned long long base = ms->pipe_seq;
   ms->pipe_seq = base + K;  // reserved up front: no later call's waits can be satisfied by this call's values
+  // test hook (tests/test_gpu_per_pipeline.py): CACTO_PIPE_FAULT_INJECT=1 gives the first device-side
+  // wait of the process an unreachable target, so it times out and latches (once per process)
+  static std::atomic<int> inject{[] {
+    const char* e = std::getenv("CACTO_PIPE_FAULT_INJECT");
+    return e && e[0] == '1' ? 1 : 0;
+  }()};
   for (int t = 0; t < K; ++t) {
     // actor chain(t-3) read the critic buffer Adam(t) writes and (PER) the index buffer of update t.
     // every2: the side stream records only at even iterations and the critic waits at even t for
@@ -2692,14 +2620,6 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
                                                    per->uniforms, B, pi, w.pisw, w.runs, st))
             return e;
         }
-      } else if (pst) {
-        if (t == 0) {  // the first sample; later ones follow the previous priority update on per_st
-          if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
-                                       per->uniforms, B, pi, w.pisw, late_count ? nullptr : per->exp_counter, pst_s))
-            return e;
-          CACTO_CHECK_HIP(hipEventRecord(ms->ev_samp, pst_s));
-        }
-        CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_samp, 0));
       } else if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
                                           per->uniforms + (size_t)t * B, B, pi, w.pisw,
                                           late_count ? nullptr : per->exp_counter, st)) {
@@ -2712,22 +2632,8 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     cur.critic_d = buf[t % 3];
     nxt.critic_d = buf[(t + 1) % 3];
     if (int e = launch_critic_chain(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
-    if (pst) {
-      // priority update t and sample t + 1 beside the critic's GEMM and Adam: they need critic chain t
-      // (y, V; its reads of the IS weights and indices), and critic chain t + 1 waits for the sample
-      CACTO_CHECK_HIP(hipEventRecord(ms->ev_chain, st));
-      CACTO_CHECK_HIP(hipStreamWaitEvent(pst_s, ms->ev_chain, 0));
-      if (int e = per_priority_update(per, idx, y, V, B, late_count, pst_s)) return e;
-      if (t + 1 < K) {
-        int32_t* pn = w.pidx + (size_t)((t + 1) % nring) * w.Bp;
-        if (int e = cacto_per_sample(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
-                                     per->uniforms + (size_t)(t + 1) * B, B, pn, w.pisw,
-                                     late_count ? nullptr : per->exp_counter, pst_s))
-          return e;
-        CACTO_CHECK_HIP(hipEventRecord(ms->ev_samp, pst_s));
-      }
-    }
     const bool dw = devwait && t >= 3;
+    const unsigned long long wait_c = dw && inject.exchange(0) ? ~0ull : base + t - 2;
     PerRunArgs pra{};
     PerSampleArgs psa{};
     if (ovl) {
@@ -2738,21 +2644,17 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
                             per->uniforms + (size_t)(t + 1) * B, B, w.pidx + (size_t)((t + 1) % nring) * w.Bp,
                             w.pisw, nullptr, 0, w.runs};
     }
-    if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d, dw ? sig : nullptr, base + t - 2,
+    if (int e = critic_step_tail(sys, nets, cfg, w, st, cur.critic_d, nxt.critic_d, dw ? sig : nullptr, wait_c,
                                  devwait_actor ? sig : nullptr, base + t + 1, ovl ? &pra : nullptr,
                                  ovl && t + 1 < K ? &psa : nullptr, thru))
       return e;
     *cbuf = (t + 1) % 3;
-    if (streamval) CACTO_CHECK_HIP(hipStreamWriteValue64(st, ms->pipe_wsig, base + t + 1, 0));
-    else if (!devwait_actor) CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
-    if (per && !pst && !ovl)
+    if (!devwait_actor) CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+    if (per && !ovl)
       if (int e = per_priority_update(per, idx, y, V, B, late_count, st)) return e;
-    if (streamval)
-      CACTO_CHECK_HIP(hipStreamWaitValue64(side, ms->pipe_wsig, base + t + 1, hipStreamWaitValueGte));
-    else if (!devwait_actor)
-      CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+    if (!devwait_actor) CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side, devwait_actor ? sig + 2 : nullptr,
-                                   base + t + 1, thru, per ? 1 : 0, asplit))
+                                   base + t + 1, per ? 1 : 0))
       return e;
     if (int e = actor_step_tail(sys, nets, cfg, w, side, devwait ? sig : nullptr, base + t + 1)) return e;
     if (devwait) {
@@ -2772,7 +2674,24 @@ extern "C" int cacto_pipeline_status(const cacto_sys* sys, unsigned long long* o
   if (!sys->pipe_sig) return CACTO_OK;
   CACTO_CHECK_HIP(hipDeviceSynchronize());
   CACTO_CHECK_HIP(hipMemcpy(out4_h, sys->pipe_sig, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  out4_h[3] = sys->pipe_probe < 0 ? 0 : (unsigned long long)sys->pipe_probe + 1;
   return CACTO_OK;
+}
+
+extern "C" int cacto_pipeline_check(cacto_sys* sys, void* stream) {
+  CACTO_REQUIRE(sys, "cacto_pipeline_check: bad arguments");
+  if (!sys->pipe_sig || !sys->latch_host) return CACTO_OK;
+  std::lock_guard<std::mutex> lock(sys->pipe_mu);
+  CACTO_CHECK_HIP(hipStreamSynchronize(as_stream(stream)));
+  volatile unsigned long long* lh = reinterpret_cast<volatile unsigned long long*>(sys->latch_host);
+  if (*lh == 0) return CACTO_OK;
+  // collected: clear both copies, so the handle's next calls run again
+  CACTO_CHECK_HIP(hipMemset(sys->pipe_sig + 1, 0, sizeof(unsigned long long)));
+  *lh = 0;
+  set_error("cacto_pipeline_check: a device-side wait of the two-stream update pipeline timed out since the last "
+            "check (kernels serialized?); the updates of that call ran without their cross-stream order and their "
+            "results are not trustworthy — rerun them with CACTO_PIPE_DEVWAIT=0");
+  return CACTO_EINVAL;
 }
 
 extern "C" int cacto_update_n(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,

@@ -102,10 +102,8 @@ __global__ void __launch_bounds__(SPT == 1 ? 256 : PER_THREADS) k_per_sample(con
                                                            const double* __restrict__ uniforms, int B,
                                                            int32_t* __restrict__ idx_out, float* __restrict__ w_out,
                                                            double* __restrict__ exp_counter,
-                                                           const double* __restrict__ shards, int n_shards,
-                                                           int prio) {
+                                                           const double* __restrict__ shards, int n_shards) {
   __shared__ double seg_s, total_s, maxw_s, scale_s;
-  if (prio) __builtin_amdgcn_s_setprio(3);  // (CACTO_PER_PRIO) ahead of the other stream's chain waves
   // the multi-workgroup launch (SPT = 1) stages a deeper top (4,096 nodes: two rounds of global
   // levels instead of three below it) and needs no index copy
   constexpr int TOPN = SPT == 1 ? 4 * TOP_NODES : TOP_NODES;
@@ -404,8 +402,7 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
                                                        const float* __restrict__ y, const float* __restrict__ V,
                                                        double* __restrict__ exp_counter, int count, double fresh,
                                                        double eps, double alpha, double* max_priority,
-                                                       const int32_t* __restrict__ skip, int prio) {
-  if (prio) __builtin_amdgcn_s_setprio(3);
+                                                       const int32_t* __restrict__ skip) {
   // 64 KiB: both subtrees and the index list (binary searches and neighbour tests in LDS); the
   // unused heap slots ts[0] / tm[0] hold the run bounds and the last-workgroup flag
   __shared__ double ts[2 * PER_SUB], tm[2 * PER_SUB];  // local node j (1-based heap of the subtree)
@@ -753,16 +750,6 @@ namespace {
 // leaves, count, subtree rebuild in LDS, the top by the last workgroup). Smaller batches keep the
 // one-workgroup kernels (fewer launches). Every path forms the same values (bit-identical indices, weights, trees).
 // CACTO_PER_MW_MIN overrides the bound (read once; benchmarks).
-// CACTO_PER_PRIO=1: the large-batch sampler and priority update at the highest wave priority
-// (s_setprio 3), so their dependent loads issue ahead of the concurrent chain waves (A/B; read once)
-int per_prio() {
-  static const int v = [] {
-    const char* e = std::getenv("CACTO_PER_PRIO");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
-
 int per_mw_min() {
   static const int v = [] {
     const char* e = std::getenv("CACTO_PER_MW_MIN");
@@ -793,7 +780,7 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
       hipLaunchKernelGGL(k_per_sample_mw, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sa);
     else
       hipLaunchKernelGGL((k_per_sample<1, 1>), dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, sum_tree_d, min_tree_d, capacity,
-                         max_idx, beta, uniforms_d, B, idx_d, is_w_d, nullptr, shards_d, n_shards, per_prio());
+                         max_idx, beta, uniforms_d, B, idx_d, is_w_d, nullptr, shards_d, n_shards);
     CACTO_CHECK_HIP(hipGetLastError());
     if (exp_counter_d) {
       hipLaunchKernelGGL(k_per_count, dim3((B + 255) / 256), dim3(256), 0, st, idx_d, B, exp_counter_d);
@@ -802,7 +789,7 @@ int launch_per_sample(const double* sum_tree_d, const double* min_tree_d, int64_
     return CACTO_OK;
   }
   hipLaunchKernelGGL((k_per_sample<PER_MAX_B / PER_THREADS, 4>), dim3(1), dim3(PER_THREADS), 0, st, sum_tree_d, min_tree_d, capacity, max_idx, beta,
-                     uniforms_d, B, idx_d, is_w_d, exp_counter_d, shards_d, n_shards, 0);
+                     uniforms_d, B, idx_d, is_w_d, exp_counter_d, shards_d, n_shards);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;
 }
@@ -849,7 +836,7 @@ int launch_per_set(double* sum_tree_d, double* min_tree_d, int64_t capacity, con
   if (mw && fused_env && nroot <= PER_FUSED_MAX_ROOTS) {
     hipLaunchKernelGGL(k_per_update_sub, dim3((unsigned)nroot), dim3(256), 0, st, sum_tree_d, min_tree_d, capacity,
                        (int)sub, idx_d, values_d, n, y_d, V_d, exp_counter_d, count, fresh, eps, alpha, max_priority_d,
-                       skip_d, per_prio());
+                       skip_d);
     CACTO_CHECK_HIP(hipGetLastError());
     return CACTO_OK;
   }

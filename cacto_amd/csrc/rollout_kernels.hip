@@ -137,11 +137,10 @@ __device__ __forceinline__ float add_from_above(float v, int off) {
 // h2 (LDS, [slot][feature]) for the 64 features of this wave. k = 64 kb + 16 v + q; lane 4q+i
 // reads {x[i][64kb + 16v + q], v = 0..3}.
 // Summation order (every kernel that can run a system forms the same one, so the schedule never
-// changes a result): SPLIT (the systems k_rollout_ks runs: NJ <= 2) — each half of K (k < 128,
-// k >= 128) as two MFMA chains over its even and odd k in increasing k, the half's sum = even +
-// odd, h2 = lrelu((lo + hi) + b2) (k_rollout_ks forms the two halves on two waves); otherwise (the
-// revolute chains, whose 16-slot kernels have no registers for the split) h2 = lrelu((even + odd)
-// + b2) over all of K.
+// changes a result): SPLIT (NJ <= 3: the systems k_rollout_ks runs, the planar 3R chain among
+// them) — each half of K (k < 128, k >= 128) as two MFMA chains over its even and odd k in
+// increasing k, the half's sum = even + odd, h2 = lrelu((lo + hi) + b2) (k_rollout_ks forms the two
+// halves on two waves); otherwise (the 6-joint chain) h2 = lrelu((even + odd) + b2) over all of K.
 template <int NG, int NS, int REGK, int LDSK, bool PF, bool SPLIT, typename WT>
 __device__ __forceinline__ void ro_layer2(const RoActorRegs<NS, REGK>& R, WT& W, const float* __restrict__ W2g,
                                           const Lane& L) {
@@ -701,8 +700,10 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   const cacto_sys_params& p = sd.p;
   const Lane L;
   const int G = gridDim.x;
-  // chains with configuration-dependent M: RNEA (wave 0) and CRBA (waves 1-3) run concurrently
-  const bool split_dyn = NJ > 0 && !(RoConstDyn<NJ>::ok && p.const_dyn);
+  // chains with configuration-dependent M: RNEA (wave 0) and CRBA (waves 1-3) run concurrently,
+  // except the planar 3R chain, which steps with the closed form (planar3_step, as k_rollout_ks)
+  const bool planar = NJ == 3 && sd.pl[0] != 0.0;
+  const bool split_dyn = NJ > 0 && !(RoConstDyn<NJ>::ok && p.const_dyn) && !planar;
   constexpr int REGK = RoSplit<NJ, NG>::REGK, LDSK = RoSplit<NJ, NG>::LDSK;
   RoActorRegs<ns, REGK> R;
   if (use_actor) ro_load_actor<NG, ns, na, REGK, LDSK>(N, L, R, Sh.W);
@@ -740,7 +741,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (!use_actor) __syncthreads();
       }
     }
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2), (NJ <= 2)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2), (NJ <= 3)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
     RSTAMP(1);
     const bool active = L.lane < SL && (L.wave == 0 ? sr.act : Sh.sact[c] != 0);
     if (split_dyn) {
@@ -777,6 +778,8 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
 #pragma unroll
             for (int i = 0; i < NJ; ++i) h[i] = Sh.hS[i * SL + c];
             chain_step<NJ>(sd, s, ad, M, h, sn);
+          } else if (NJ == 3 && planar) {
+            planar3_step(Planar3(sd.pl), ks.dt, s, ad, sn);
           } else {
             ro_simulate<NJ>(ks, sr.cd, s, ad, sn);
           }
@@ -1093,6 +1096,12 @@ __device__ __forceinline__ V lane_pick(const V* x, int lane) {
   return v;
 }
 
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // ---------------------------------------------------------------- one slot per wave, K split
 // k_rollout_ks: one 8-wave workgroup per CU runs 8 episode slots, wave w owning slot w: after
 // layer 2 the wave forms its slot's action (layer 3 — ro_actor's P = 64 lane chains per slot are
@@ -1107,12 +1116,24 @@ __device__ __forceinline__ V lane_pick(const V* x, int lane) {
 // is read from LDS per step — for all 8 slots (two groups of 4 samples, 256 MFMAs), and parks its
 // half sum; layer 3 adds the two halves (the SPLIT order of ro_layer2, so results are identical to
 // the other rollout kernels). Two hardware barriers per step (one workgroup = one team).
+// Systems: SI, DI, car, car_park and the planar 3R chain (the manipulator), whose dynamics are the
+// closed form planar3_step (M(q), h(q, v) from the link COM vectors, one 3x3 adjugate solve) —
+// short enough for one wave per slot, where the generic chain needs RNEA / CRBA spread over a
+// workgroup (k_rollout<3, NG> steps a planar chain with planar3_step too).
 template <int NJ>
 struct RoKsShared {
   float h1[2 * 4 * RoCfg<1>::H1B];  // layer-1 output of the 8 slots (groups 0, 1), layer-2 operand layout
   float P[2][8 * 256];              // layer-2 half sums [k half][slot][feature]
   int act[8];                       // slot active flags, published by the barrier that ends a step
   int qhead;                        // the workgroup's next queue entry
+  // the planar 3R chain keeps W3^T, b2 and its link constants here instead of in registers (its
+  // wider input and output layers and the float64 dynamics would otherwise not fit beside the 128
+  // layer-2 weight registers); read with layer 3's half sums and during the dynamics' sincos
+  static constexpr bool LW = NJ == 3;
+  float w3s[LW ? 3 * 256 : 1];  // W3^T [a][f]
+  float b2s[LW ? 256 : 1];
+  float4 w1s[LW ? 8 * 64 : 1];  // W1 [q][lane][m] = W1[q][lane + 64 m] (q < ns), then b1 [lane][m] at q = 7
+  double pls[LW ? 20 : 1];
 };
 
 template <int NJ>
@@ -1128,7 +1149,8 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int fq = w & 3, hk = w >> 2;  // layer 2: features 64 fq + lane, rows [128 hk, 128 hk + 128)
   const int sg = w >> 2, si = w & 3;  // this wave's slot w = 4 sg + si (group, sample)
-  float w2[128], b2[4], w1[ns][4], b1[4], w3[na][4], b3[na];
+  constexpr bool LW = RoKsShared<NJ>::LW;
+  float w2[128], b2[LW ? 1 : 4], w1[LW ? 1 : ns][4], b1[LW ? 1 : 4], w3[LW ? 1 : na][4], b3[na];
   if (use_actor) {
     const float* W1 = N.flat + N.t.woff[0];
     const float* W2 = N.flat + N.t.woff[1];
@@ -1137,16 +1159,33 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
     for (int k = 0; k < 128; ++k) w2[k] = W2[(128 * hk + k) * 256 + 64 * fq + lane];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
+      if constexpr (!LW) {
 #pragma unroll
-      for (int q = 0; q < ns; ++q) w1[q][m] = W1[q * 256 + lane + 64 * m];
-      b1[m] = N.bias(0, lane + 64 * m);
-      b2[m] = N.bias(1, lane + 64 * m);
+        for (int q = 0; q < ns; ++q) w1[q][m] = W1[q * 256 + lane + 64 * m];
+        b1[m] = N.bias(0, lane + 64 * m);
+        b2[m] = N.bias(1, lane + 64 * m);
 #pragma unroll
-      for (int a = 0; a < na; ++a) w3[a][m] = W3[(lane + 64 * m) * na + a];
+        for (int a = 0; a < na; ++a) w3[a][m] = W3[(lane + 64 * m) * na + a];
+      }
     }
 #pragma unroll
     for (int a = 0; a < na; ++a) b3[a] = N.bias(2, a);
+    if constexpr (LW) {
+      for (int e = threadIdx.x; e < na * 256; e += 8 * CACTO_WAVE) Sh.w3s[e] = W3[(e & 255) * na + (e >> 8)];
+      for (int e = threadIdx.x; e < 256; e += 8 * CACTO_WAVE) Sh.b2s[e] = N.bias(1, e);
+      for (int e = threadIdx.x; e < 8 * 64; e += 8 * CACTO_WAVE) {
+        const int q = e >> 6, l = e & 63;
+        float4 v;
+        if (q < ns)
+          v = make_float4(W1[q * 256 + l], W1[q * 256 + l + 64], W1[q * 256 + l + 128], W1[q * 256 + l + 192]);
+        else
+          v = make_float4(N.bias(0, l), N.bias(0, l + 64), N.bias(0, l + 128), N.bias(0, l + 192));
+        Sh.w1s[e] = v;
+      }
+    }
   }
+  if constexpr (LW)
+    if (threadIdx.x < 20) Sh.pls[threadIdx.x] = sd.pl[threadIdx.x];
   for (int e = threadIdx.x; e < 2 * 4 * H1B; e += 8 * CACTO_WAVE) Sh.h1[e] = 0.f;
   if (threadIdx.x == 0) Sh.qhead = 0;
   __syncthreads();
@@ -1156,8 +1195,10 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
 #pragma unroll
   for (int q = 0; q < ns; ++q) nl = lane == q ? nrm.n[q] : nl;
   const bool tl = lane == ns - 1;
+  // the prismatic chain's constant Cholesky factor and bias forces; the planar 3R chain's link
+  // constants (planar3_step)
   ConstDyn<NJ> cd;
-  if constexpr (NJ > 0) {
+  if constexpr (NJ > 0 && NJ != 3) {
 #pragma unroll
     for (int k = 0; k < NJ * NJ; ++k) cd.L[k] = sd.cd_L[k];
 #pragma unroll
@@ -1206,12 +1247,25 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
     float x0[ns];
 #pragma unroll
     for (int q = 0; q < ns; ++q) x0[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), q));
+    if constexpr (LW) {
+      float4 wq[ns + 1];  // W1 rows and b1 of this lane's 4 features, from LDS
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float acc = 0.f;
+      for (int q = 0; q <= ns; ++q) wq[q] = Sh.w1s[(q < ns ? q : 7) * 64 + lane];
 #pragma unroll
-      for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], w1[q][m], acc);
-      Sh.h1[(sg * 4 + m) * H1B + (lane & 15) * 20 + 4 * si + (lane >> 4)] = lrelu(fadd(acc, b1[m]));
+      for (int m = 0; m < 4; ++m) {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], get4(wq[q], m), acc);
+        Sh.h1[(sg * 4 + m) * H1B + (lane & 15) * 20 + 4 * si + (lane >> 4)] = lrelu(fadd(acc, get4(wq[ns], m)));
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < ns; ++q) acc = __builtin_fmaf(x0[q], w1[q][m], acc);
+        Sh.h1[(sg * 4 + m) * H1B + (lane & 15) * 20 + 4 * si + (lane >> 4)] = lrelu(fadd(acc, b1[m]));
+      }
     }
   };
 
@@ -1287,9 +1341,9 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int f = lane + 64 * m;
-          const float h = lrelu(fadd(fadd(Sh.P[0][w * 256 + f], Sh.P[1][w * 256 + f]), b2[m]));
+          const float h = lrelu(fadd(fadd(Sh.P[0][w * 256 + f], Sh.P[1][w * 256 + f]), LW ? Sh.b2s[f] : b2[m % (LW ? 1 : 4)]));
 #pragma unroll
-          for (int i = 0; i < na; ++i) pa[i] = fmaf(w3[i][m], h, pa[i]);
+          for (int i = 0; i < na; ++i) pa[i] = fmaf(LW ? Sh.w3s[i * 256 + f] : w3[LW ? 0 : i][m], h, pa[i]);
         }
         if constexpr (na == 2) {
           const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[0]), __float_as_uint(pa[1]), false, false);
@@ -1300,6 +1354,25 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
           for (int off = 8; off >= 1; off >>= 1) v = add_from_above(v, off);
           a[0] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)), b3[0]);
           a[1] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)), b3[1 % na]);
+        } else if constexpr (na == 3) {
+          // actions 0 / 1 as above, action 2 through the same levels on its own (lanes 0-31 hold
+          // the sums after the first swap); the adds are the butterfly's, so the bits are too
+          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[0]), __float_as_uint(pa[1]), false, false);
+          const auto q32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa[2]), __float_as_uint(pa[2]), false, false);
+          float v = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+          float v2 = __uint_as_float(q32[0]) + __uint_as_float(q32[1]);
+          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+          const auto q16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v2), __float_as_uint(v2), false, false);
+          v = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+          v2 = __uint_as_float(q16[0]) + __uint_as_float(q16[1]);
+#pragma unroll
+          for (int off = 8; off >= 1; off >>= 1) {
+            v = add_from_above(v, off);
+            v2 = add_from_above(v2, off);
+          }
+          a[0] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)), b3[0]);
+          a[1] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)), b3[1 % na]);
+          a[2 % na] = fadd(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v2), 0)), b3[2 % na]);
         } else {
 #pragma unroll
           for (int off = 32; off >= 1; off >>= 1)
@@ -1317,7 +1390,15 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
       double ad[na], sn[ns];
 #pragma unroll
       for (int i = 0; i < na; ++i) ad[i] = (double)a[i];
-      ro_simulate<NJ>(ks, cd, s, ad, sn);
+      if constexpr (NJ == 3) {
+        // sin / cos of q1 on even lanes and of q2 on odd lanes at once (joint_sincos is the
+        // function planar3_step calls, so the bits are the same)
+        double sv, cv;
+        joint_sincos((lane & 1) ? s[2] : s[1], &sv, &cv);
+        planar3_step_sc(Planar3(Sh.pls), ks.dt, s, ad, readlane_d(sv, 0), readlane_d(cv, 0), readlane_d(sv, 1),
+                        readlane_d(cv, 1), sn);
+      } else
+        ro_simulate<NJ>(ks, cd, s, ad, sn);
       bool bad = false;
 #pragma unroll
       for (int i = 0; i < ns; ++i) bad |= isnan(sn[i]);
@@ -1353,267 +1434,6 @@ __global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
   }
 #endif
 #undef KMARK
-}
-
-// ---------------------------------------------------------------- actor waves beside dynamics waves
-// k_rollout_sw (revolute chains with 3 joints: the manipulator). The per-step float64 dynamics of a
-// chain whose M depends on q (RNEA, CRBA, Cholesky: ~9 k cycles of dependent f64 work, one lane per
-// slot) left the matrix cores idle for 40 % of k_rollout's step. Here an 8-wave workgroup gives the
-// two kinds of work their own waves — waves 0-3 run the actor (layer-2 rows 64 w + lane of W2 in
-// their registers, the rest in LDS), waves 4-7 the dynamics (RNEA on wave 4, the CRBA columns on
-// waves 5-7, as k_rollout's waves 0-3) — so every SIMD holds one wave of each and issues MFMAs for one
-// while the other waits on f64 latency. The 16 episode slots form two halves of two groups; in
-// half-step k the actor waves run the actor of half X = k & 1 while the dynamics waves step half
-// Y = 1 - X with the actions the actor produced for it in half-step k - 1: each half advances one
-// env step every two half-steps. Each role synchronises with a team barrier (an LDS arrival counter),
-// the two roles meet at one workgroup barrier per half-step. The actor waves also compute the joint
-// placements of the half they just ran, for its dynamics in the next half-step (r05 stamps: on the
-// dynamics waves they were 7.1 k of a 16.3 k-cycle dynamics half-step; the actor waves waited 9.1 k of
-// theirs at the end barrier). Every per-slot value is formed by the
-// functions k_rollout<3, 4> uses, in the same order (ro_actor / ro_layer2 without SPLIT, ro_chain_nle,
-// ro_chain_mass_cols, chain_step, ro_advance, ro_refill), so results are bit-identical to it.
-template <int NJ>
-struct RoSwCfg {
-  static constexpr int NG = 4, SL = 16, NH = 2, SH = 8;  // groups and slots; per half
-  // layer-2 rows: [0, REGK) in the actor waves' registers, [REGK, REGK + LDSK) in LDS, the rest
-  // streamed from L2 at every actor pass (the dynamics, not the actor, bound the half-step)
-#ifdef RO_SW_REGK
-  static constexpr int REGK = RO_SW_REGK;
-#else
-  static constexpr int REGK = 160;  // 176 / 80 and 192 / 64 measured no fewer spills (16 B, the dynamics role)
-#endif
-#ifdef RO_SW_LDSK
-  static constexpr int LDSK = RO_SW_LDSK;
-#else
-  static constexpr int LDSK = 96;
-#endif
-  static_assert(REGK % 16 == 0 && LDSK % 16 == 0 && REGK + LDSK <= 256, "row split");
-};
-
-template <int NJ>
-struct RoSwShared {
-  static constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA, SL = RoSwCfg<NJ>::SL, SH = RoSwCfg<NJ>::SH;
-  using H = RoCfg<RoSwCfg<NJ>::NH>;  // per-half actor layout (8 slots)
-  struct {
-    float4 w2[RoSwCfg<NJ>::LDSK / 4 * 4 * 64];  // W2[REGK + 4kq + j][64w + lane] at (kq*4 + w)*64 + lane
-    float w3[na * 256];
-    float b3[8];
-    float h1[2 * RoSwCfg<NJ>::NH * 4 * H::H1B];  // per half: its groups' layer-1 output
-    float h2[2 * SH * H::H2S];
-    float x0[2 * RoSwCfg<NJ>::NH * 64];  // slot c at (c >> 2) * 64 + 4q + (c & 3): ro_refill's layout
-    float a[2 * SH * na];
-  } W;
-  double sS[SL * ns];
-  double MS[SL * NJ * NJ], hS[SL * NJ];
-  RoChain<NJ, SL> ch;
-  int sb[SL], sn[SL], st[SL], sact[SL];
-  int any[2][2];  // [half-step parity][half]: a slot of the half is active
-  int bar_a, bar_d;
-};
-
-#ifdef CACTO_STAMPS
-__device__ unsigned long long g_swacc[1024 * 2 * 6];  // k_rollout_sw: [workgroup][role][phase 0-4, half-steps]
-#endif
-
-template <int NJ>
-__global__ void __launch_bounds__(8 * CACTO_WAVE, 1)
-    k_rollout_sw(const SysDevice* __restrict__ sdp, NetView N, const double* __restrict__ S0,
-                 const int32_t* __restrict__ nsteps, int T, int use_actor, double* __restrict__ Straj,
-                 float* __restrict__ Atraj, int32_t* __restrict__ status, const int32_t* __restrict__ order, int B) {
-  using Cf = RoSwCfg<NJ>;
-  constexpr int ns = Dims<NJ>::NS, na = Dims<NJ>::NA, SL = Cf::SL, SH = Cf::SH, NH = Cf::NH;
-  constexpr int REGK = Cf::REGK, LDSK = Cf::LDSK;
-  using H = RoCfg<NH>;
-  __shared__ RoSwShared<NJ> Sh;
-  const SysDevice& sd = *sdp;
-  const cacto_sys_params& p = sd.p;
-  const bool dyn = threadIdx.x >= 4 * CACTO_WAVE;  // role, uniform per wave
-  Lane L;  // team-local: tid 0..255, wave 0..3 within the role
-  L.tid = threadIdx.x & 255;
-  L.wave = L.tid >> 6;
-  if (dyn && use_actor) {
-    const float* W2 = N.flat + N.t.woff[1];
-    const float* W3 = N.flat + N.t.woff[2];
-    for (int e = L.tid; e < LDSK * 64; e += CACTO_THREADS) {
-      const int lane = e & 63, w = (e >> 6) & 3, kq = e >> 8;
-      const int k = REGK + 4 * kq, col = 64 * w + lane;
-      Sh.W.w2[e] = make_float4(W2[k * 256 + col], W2[(k + 1) * 256 + col], W2[(k + 2) * 256 + col],
-                               W2[(k + 3) * 256 + col]);
-    }
-    for (int e = L.tid; e < na * 256; e += CACTO_THREADS) Sh.W.w3[e] = W3[(e & 255) * na + (e >> 8)];
-    if (L.tid < 8) Sh.W.b3[L.tid] = L.tid < na ? N.bias(2, L.tid) : 0.f;
-  }
-  for (int e = threadIdx.x; e < 2 * NH * 64; e += 8 * CACTO_WAVE) Sh.W.x0[e] = 0.f;
-  for (int e = threadIdx.x; e < SL * ns; e += 8 * CACTO_WAVE) Sh.sS[e] = 0.0;
-  if (threadIdx.x < SL) Sh.sact[threadIdx.x] = 0;
-  if (threadIdx.x == 0) Sh.bar_a = Sh.bar_d = 0;
-  __syncthreads();
-  const int G = gridDim.x, vb = (int)blockIdx.x;
-  int head = 0;  // queue position (dynamics wave 0, uniform)
-  const RoNorm<ns> nrm(p);
-  const bool d0 = dyn && L.wave == 0;
-  const int c = L.lane % SL;  // dynamics wave 0: lane c <-> slot c
-  RoSlotRegs<NJ, RoSwCfg<NJ>::NG> sr;
-  if (d0) {
-    ro_refill<NJ, RoSwCfg<NJ>::NG>(L.lane < SL, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L, vb);
-    const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
-    if (L.lane == 0) {
-      Sh.any[0][0] = (m & 0xffull) != 0;
-      Sh.any[0][1] = (m & 0xff00ull) != 0;
-    }
-    sr.load(Sh, c, false);
-  }
-  __syncthreads();
-  RoTeamBar abar{&Sh.bar_a, 0, L.lane}, dbar{&Sh.bar_d, 0, L.lane};
-  const float* W2g = N.flat + N.t.woff[1];
-  // per-phase cycles (CACTO_STAMPS): actor role [0] actor + placements, [1] end barrier; dynamics role
-  // [0] loop test, [1] RNEA / CRBA + team barrier, [2] step, stores, refill, next input, [3] end
-  // barrier; [5] half-steps
-#ifdef CACTO_STAMPS
-  unsigned long long wacc[5] = {0, 0, 0, 0, 0}, wprev = __builtin_amdgcn_s_memtime();
-  int wsteps = 0;
-  auto wmark = [&](int ph) {
-    const unsigned long long now = __builtin_amdgcn_s_memtime();
-#pragma unroll
-    for (int k = 0; k < 5; ++k)
-      if (k == ph) wacc[k] += now - wprev;
-    wprev = now;
-  };
-#define SWMARK(k) wmark(k)
-#else
-#define SWMARK(k) \
-  do {            \
-  } while (0)
-#endif
-  // The two roles run separate loops (so the actor's register-resident weights are not live across
-  // the dynamics code); both leave at the same half-step (the flags they read are the same) and meet
-  // at the one workgroup barrier of every half-step.
-  if (!dyn) {
-    RoActorRegs<ns, REGK> R;
-    if (use_actor) {
-      const float* W1 = N.flat + N.t.woff[0];
-      const float* W2 = N.flat + N.t.woff[1];
-      const int f = 64 * L.wave + L.lane;
-#pragma unroll
-      for (int k = 0; k < REGK; ++k) R.w2[k] = W2[k * 256 + f];
-#pragma unroll
-      for (int q = 0; q < ns; ++q) R.w1[q] = W1[q * 256 + f];
-      R.b1 = N.bias(0, f);
-      R.b2 = N.bias(1, f);
-    }
-    for (int it = 0;; ++it) {
-      const int par = it & 1, X = par, Y = 1 - par;
-      const bool anyX = Sh.any[par][X] != 0, anyY = Sh.any[par][Y] != 0;
-      if (!anyX && !anyY) break;
-      if (anyX && use_actor) {
-        RoTeamView<na> V{Sh.W.w2, Sh.W.w3, Sh.W.b3, Sh.W.h1 + X * NH * 4 * H::H1B, Sh.W.h2 + X * SH * H::H2S,
-                         Sh.W.x0 + X * NH * 64, Sh.W.a + X * SH * na};
-        ro_actor<NH, ns, na, REGK, LDSK, false, false>(R, V, W2g, L, it, abar);
-      }
-      // the joint placements X(q_i) of half X's slots for its dynamics in the next half-step (s_t of
-      // the half is final: its last dynamics pass was in half-step it - 1), spread over the 4 waves
-      if (anyX) {
-        const int e = L.lane * 4 + L.wave;  // item (slot X*8 + e % 8, joint e / 8)
-        if (e < SH * NJ) {
-          const int cc = X * SH + e % SH, i = e / SH;
-          if (Sh.sact[cc])
-            se3_st<SL>(Sh.ch.X + i * 12 * SL + cc,
-                       joint_placement(JointView{sd.joints + i * CACTO_JOINT_COLS}, Sh.sS[cc * ns + i]));
-        }
-      }
-      SWMARK(0);
-      __syncthreads();
-      SWMARK(1);
-#ifdef CACTO_STAMPS
-      ++wsteps;
-#endif
-    }
-  } else {
-    for (int it = 0;; ++it) {
-      const int par = it & 1, Y = 1 - par;
-      const bool anyX = Sh.any[par][par] != 0, anyY = Sh.any[par][Y] != 0;
-      if (!anyX && !anyY) break;
-      // the dynamics of half Y, from the actions its actor pass wrote in half-step it - 1
-      // (its joint placements were computed by the actor waves at the end of that actor pass)
-      const bool run = anyY && it > 0;
-      SWMARK(0);
-      const int cy = Y * SH + (L.lane & (SH - 1));  // this lane's slot of half Y
-      const bool act_y = run && L.lane < SH && Sh.sact[cy] != 0;
-      if (run) {
-        if (L.wave == 0) {
-          if (act_y) ro_chain_nle<NJ, SL>(sd, Sh.ch, cy, Sh.sS + cy * ns, Sh.sS + cy * ns + NJ, Sh.hS + cy);
-        } else if (act_y) {
-          ro_chain_mass_cols<NJ, SL>(sd, Sh.ch, cy, Sh.MS + cy, RoMassCols<NJ>::lo(L.wave), RoMassCols<NJ>::hi(L.wave));
-        }
-        dbar();
-      }
-      SWMARK(1);
-      if (d0) {
-        // lane c holds slot c's registers; the lanes of half Y step their slots
-        const bool mine = run && L.lane < SL && (c / SH) == Y;
-        const bool active = mine && sr.act;
-        bool fin = false;
-        float a[na];
-        if (active) {
-          double ad[na], sn[ns], M[NJ * NJ], h[NJ];
-#pragma unroll
-          for (int i = 0; i < na; ++i) {
-            a[i] = use_actor ? Sh.W.a[(Y * SH + (c - Y * SH)) * na + i] : 0.f;
-            ad[i] = (double)a[i];
-          }
-#pragma unroll
-          for (int k = 0; k < NJ * NJ; ++k) M[k] = Sh.MS[k * SL + c];
-#pragma unroll
-          for (int i = 0; i < NJ; ++i) h[i] = Sh.hS[i * SL + c];
-          chain_step<NJ>(sd, sr.s, ad, M, h, sn);
-#pragma unroll
-          for (int i = 0; i < ns; ++i) {
-            Sh.sS[c * ns + i] = sn[i];
-            sr.s[i] = sn[i];
-          }
-        }
-        if (run) {
-          // the next actor input of half Y's slots from s_{t+1} (one (slot, feature) item per lane);
-          // a slot refilled below gets its s_0 row from ro_refill afterwards (later in program order)
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-          if (L.lane < SH * ns) {
-            const int cc = Y * SH + L.lane % SH, f = L.lane / SH;
-            float nf = 1.f;
-#pragma unroll
-            for (int q = 0; q < ns; ++q) nf = f == q ? nrm.n[q] : nf;
-            const float q = fdiv((float)Sh.sS[cc * ns + f], nf);
-            const float v = f == ns - 1 ? fsub(fmul(q, 2.0f), 1.0f) : q;
-            Sh.W.x0[(cc >> 2) * 64 + 4 * f + (cc & 3)] = nrm.on ? v : (float)Sh.sS[cc * ns + f];
-          }
-        }
-        if (active) {
-          fin = ro_advance<NJ, RoSwCfg<NJ>::NG>(c, sr.b, sr.t, sr.s, a, sd, T, Straj, Atraj, status, nrm, sr.n);
-          sr.t += 1;
-        }
-        ro_refill<NJ, RoSwCfg<NJ>::NG>(fin, c, head, Sh, sd, S0, nsteps, order, T, B, G, Straj, status, nrm, L, vb);
-        if (fin) sr.load(Sh, c, false);
-        const uint64_t m = __ballot(L.lane < SL && Sh.sact[c]);
-        if (L.lane == 0) {
-          Sh.any[1 - par][0] = (m & 0xffull) != 0;
-          Sh.any[1 - par][1] = (m & 0xff00ull) != 0;
-        }
-      }
-      SWMARK(2);
-      __syncthreads();
-      SWMARK(3);
-#ifdef CACTO_STAMPS
-      ++wsteps;
-#endif
-    }
-  }
-#ifdef CACTO_STAMPS
-  if (L.lane == 0 && L.wave == 0) {
-    unsigned long long* o = g_swacc + ((size_t)blockIdx.x * 2 + (dyn ? 1 : 0)) * 6;
-    for (int k = 0; k < 5; ++k) o[k] = wacc[k];
-    o[5] = wsteps;
-  }
-#endif
-#undef SWMARK
 }
 
 // Rewards and end-effector positions of every recorded step (Env.step's reward and
@@ -1805,20 +1625,26 @@ struct LaunchRollout {
     // automatic only where it measured faster: the prismatic chain (DI 0.75 -> 0.72 ms at 4096
     // episodes); car_park's step was slower on two teams (0.42 -> 0.50 ms)
     const bool tt_auto = tt_sys && NJ > 0;
-    if ((groups == -1 || groups == -3) && !tt_sys) {
-      set_error("cacto_rollout_sched: groups -1 / -3 need a system without configuration-dependent M");
+    // planar 3-joint chains (the manipulator): k_rollout_ks with the closed-form planar3_step
+    constexpr bool ks_ok = tt_ok || NJ == 3;
+    const bool planar = NJ == 3 && sys->host.pl[0] != 0.0;
+    const bool ks_sys = tt_sys || planar;
+    if ((groups == -1 && !tt_sys) || (groups == -3 && !ks_sys)) {
+      set_error("cacto_rollout_sched: groups -1 needs a system without configuration-dependent M, -3 such a system "
+                "or a planar 3-joint chain");
       return CACTO_EINVAL;
     }
     // one slot per wave with layer 2 split over K (k_rollout_ks) for every system it can run, up
     // to two episodes per slot. Measured at 4096 episodes (ms per rollout, one MI355X): DI
     // k_rollout_tt 0.750 / one slot per wave in two teams (round 4, removed) 0.630 / k_rollout_ks
     // 0.578; SI single-team 0.519 / ks 0.292; car_park single-team 0.432 / ks 0.405; car 1.865 / 1.768.
-    const bool ks_auto = tt_sys && B <= 2 * 8 * cus;
+    // The planar chain takes it at every batch size.
+    const bool ks_auto = (tt_sys && B <= 2 * 8 * cus) || planar;
     if (groups == -3 || (groups == 0 && ks_auto)) {
       // one slot per wave, layer 2 split over K (k_rollout_ks), one 8-wave workgroup per CU
       if (wgs <= 0) wgs = std::min(cus, ceil_div(B, 8));
       wgs = std::max(1, std::min(wgs, ceil_div(B, 8)));
-      if constexpr (tt_ok)
+      if constexpr (ks_ok)
         hipLaunchKernelGGL(k_rollout_ks<NJ>, dim3(wgs), dim3(8 * CACTO_WAVE), 0, st, sys->dev, v, S0, n, T,
                            use_actor, S, A, status, order, B);
       CACTO_CHECK_HIP(hipGetLastError());
@@ -1834,27 +1660,6 @@ struct LaunchRollout {
       CACTO_CHECK_HIP(hipGetLastError());
       if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
       return CACTO_OK;
-    }
-    // 3-joint revolute chains (the manipulator): actor waves beside dynamics waves (k_rollout_sw),
-    // on request (groups == -4) or automatically with CACTO_RO_SW=1 (A/B; bit-identical to k_rollout<3, 4>)
-    static const bool sw_env = [] {
-      const char* e = std::getenv("CACTO_RO_SW");
-      return e && e[0] == '1';
-    }();
-    if constexpr (NJ == 3) {
-      if (groups == -4 || (groups == 0 && sw_env && !sys->host.p.const_dyn)) {
-        if (wgs <= 0) wgs = std::min(cus, ceil_div(B, RoSwCfg<NJ>::SL));
-        wgs = std::max(1, std::min(wgs, ceil_div(B, RoSwCfg<NJ>::SL)));
-        hipLaunchKernelGGL(k_rollout_sw<NJ>, dim3(wgs), dim3(8 * CACTO_WAVE), 0, st, sys->dev, v, S0, n, T, use_actor,
-                           S, A, status, order, B);
-        CACTO_CHECK_HIP(hipGetLastError());
-        if (R || EE) return LaunchRolloutRewards<NJ>::run(sys, S, A, n, T, use_actor, W, R, EE, B, st);
-        return CACTO_OK;
-      }
-    }
-    if (groups == -4) {
-      set_error("cacto_rollout_sched: groups -4 (actor waves beside dynamics waves) needs a 3-joint revolute chain");
-      return CACTO_EINVAL;
     }
     // the float64 6-joint chain dynamics need the registers that more slots would take
     constexpr int gmax = 4;
@@ -1906,12 +1711,6 @@ extern "C" int cacto_debug_rollout_ws_acc(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_wsacc), sizeof(unsigned long long) * 1024 * 8 * 7));
   return CACTO_OK;
 }
-// k_rollout_sw's accumulated phase cycles: 1024 x 2 x 6 values (see the kernel)
-extern "C" int cacto_debug_rollout_sw_acc(unsigned long long* out_h) {
-  CACTO_CHECK_HIP(hipDeviceSynchronize());
-  CACTO_CHECK_HIP(hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_swacc), sizeof(unsigned long long) * 1024 * 2 * 6));
-  return CACTO_OK;
-}
 // k_rollout_tt's accumulated phase cycles: 1024 x 2 x 2 x 10 values (see the kernel)
 extern "C" int cacto_debug_rollout_tt_acc(unsigned long long* out_h) {
   CACTO_CHECK_HIP(hipDeviceSynchronize());
@@ -1926,10 +1725,9 @@ extern "C" int cacto_rollout_sched(const cacto_sys* sys, const float* actor_netb
                                    const int32_t* order_d, int B, int groups, int workgroups, void* stream) {
   CACTO_REQUIRE(sys && S0_d && nsteps_d && T >= 0 && B >= 0, "cacto_rollout: bad arguments");
   CACTO_REQUIRE(!use_actor || actor_netbuf_d, "cacto_rollout: use_actor needs the actor net buffer");
-  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -3 ||
-                    groups == -4,
-                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams), -3 (one slot per wave, layer 2 "
-                "split over K) or -4 (actor waves beside dynamics waves, 3-joint chains)");
+  CACTO_REQUIRE(groups == 0 || groups == 1 || groups == 2 || groups == 4 || groups == -1 || groups == -3,
+                "cacto_rollout_sched: groups must be 0, 1, 2, 4, -1 (two teams) or -3 (one slot per wave, layer 2 "
+                "split over K)");
   CACTO_REQUIRE(workgroups >= 0, "cacto_rollout_sched: workgroups must be >= 0");
   CACTO_REQUIRE(!(R_traj_d || EE_traj_d) || (S_traj_d && (A_traj_d || !use_actor)),
                 "cacto_rollout: R_traj / EE_traj need S_traj (and A_traj when use_actor)");

@@ -476,6 +476,7 @@ class RL_AC:
                 for _ in range(k):
                     update_step_counter = self._after_step(update_step_counter)
                 i += k
+            self.check_pipeline()
             return update_step_counter
         idx_all = buffer.sample_indices(n, rng)                  # [n, B] int32 on device
         # the updates between two checkpoint saves (RL.py:139-141) run as one pipelined call
@@ -486,7 +487,16 @@ class RL_AC:
             for _ in range(k):
                 update_step_counter = self._after_step(update_step_counter)
             i += k
+        self.check_pipeline()
         return update_step_counter
+
+    def check_pipeline(self):
+        """Raise if a device-side wait of the two-stream update pipeline timed out since the last
+        check (cacto_pipeline_check: synchronizes the current stream, clears the latch): the
+        updates of that call ran without their cross-stream order (RL.py:104-109 orders critic(t)
+        before actor(t)), so their weights must not be used. learn_and_update calls it before it
+        returns, RL_save_weights before it writes a checkpoint."""
+        L.lib().call("cacto_pipeline_check", self.sys.handle, stream())
 
     def _learn_and_update_relo(self, update_step_counter, buffer, n, B):
         """RL.py:120-143 with RB_type 'ReLO' (replay_buffer.py:193-196): the priority rule needs
@@ -574,6 +584,7 @@ class RL_AC:
 
     def RL_save_weights(self, update_step_counter='final'):
         """RL.py:191-195: Keras-2.11 .h5 files the reference can load."""
+        self.check_pipeline()
         base = "%s/N_try_%s/" % (self.conf.NNs_path, self.N_try)
         self.actor_model.save_weights(base + "actor_%s.h5" % update_step_counter)
         self.critic_model.save_weights(base + "critic_%s.h5" % update_step_counter)

@@ -241,11 +241,25 @@ int cacto_update(const cacto_sys* sys, const cacto_nets* nets, const cacto_updat
                  float* y_d, float* V_d, float* Vt_d, void* workspace_d, size_t workspace_bytes,
                  void* stream);
 
-/* Diagnostic: the two-stream pipeline's device-side ordering words (CACTO_PIPE_DEVWAIT=1): out4_h[0]
- * actor chains finished, [1] 1 if a device-side wait ever timed out (an ordering bug; the waits are
- * bounded so that it cannot hang the GPU), [2] critic Adam steps finished, [3] 0. Synchronizes the
- * device. All zero before the first pipelined call. */
+/* Diagnostic: the two-stream pipeline's device-side ordering words: out4_h[0] actor chains finished,
+ * [1] 1 if a device-side wait timed out since the last cacto_pipeline_check (the waits are bounded
+ * so that an ordering fault cannot hang the GPU), [2] critic Adam steps finished, [3] the handle's
+ * concurrency probe: 0 not run, 1 the two streams' kernels did not run concurrently (queue markers
+ * order them), 2 they did (device-side waits). Synchronizes the device. All zero before the first
+ * pipelined call. */
 int cacto_pipeline_status(const cacto_sys* sys, unsigned long long* out4_h);
+/* Collects the two-stream pipeline's timeout latch: synchronizes `stream` (the stream the pipelined
+ * calls were issued on), and if a device-side wait of any cacto_update_n[_per] call since the last
+ * check timed out — its updates then ran without their cross-stream order — clears the latch and
+ * returns CACTO_EINVAL (the message says so); otherwise CACTO_OK. A set latch also makes the next
+ * pipelined call refuse to run until it is collected. The Python layer calls it at the end of every
+ * learn_and_update and before every checkpoint save (RL.py:139-143), so no result of a timed-out
+ * call leaves unflagged. Ordering: device-side waits are the default; queue markers are used while
+ * the stream is being captured into a graph, when the environment serializes kernels
+ * (AMD_SERIALIZE_KERNEL, HIP_LAUNCH_BLOCKING) and when a one-time probe per handle finds that the
+ * two streams' kernels do not run concurrently (e.g. under counter collection);
+ * CACTO_PIPE_DEVWAIT=0 / 1 forces markers / device waits. */
+int cacto_pipeline_check(cacto_sys* sys, void* stream);
 /* K consecutive updates on minibatch indices idx_d [K][B] (learn_and_update's loop with its
  * minibatches drawn up front, RL.py:120-143; no IS weights). Bit-identical to K cacto_update calls.
  * The critic step of update t+1 overlaps the actor step of update t (the critic step never reads

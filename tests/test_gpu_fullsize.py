@@ -53,8 +53,9 @@ def test_fullsize_rollout_properties(system, R):
             np.testing.assert_allclose(S[e, k + 1], oe.simulate(S[e, k], A[e, k].astype(np.float64)), rtol=1e-12,
                                        atol=1e-12)
     # schedule invariance at full size: another (groups, workgroups) split gives the same bits (the
-    # manipulator also on the actor-waves-beside-dynamics-waves kernel, groups = -4)
-    for sched in [(1, 512)] + ([(-4, 0)] if system == "manipulator" else []):
+    # manipulator, whose default is the one-slot-per-wave kernel, also on the generic kernel's
+    # 16-slot workgroups, groups = 4)
+    for sched in [(1, 512)] + ([(4, 0)] if system == "manipulator" else []):
         other = rl.rollout_batch(S0, n, T, want=("S", "A"), sched=sched)
         torch.cuda.synchronize()
         oS, oA = other["S"].cpu().numpy(), other["A"].cpu().numpy()

@@ -94,6 +94,46 @@ def test_graph_replay_equals_eager_updates_with_per():
         assert torch.equal(getattr(ebuf, name), getattr(gbuf, name)), name
 
 
+def test_captured_two_stream_pipeline_replays_equal_eager_calls():
+    """cacto_update_n above the paired threshold (B = 1024: the two-stream pipeline) captured into a
+    graph and replayed twice equals two eager calls bit for bit. The device-side waits compare device
+    counters with absolute targets baked into the launches, so a replay would find its targets
+    already reached: while the stream is being captured the pipeline orders its streams
+    with queue markers instead."""
+    conf = load_conf("double_integrator", fresh=True)
+    env = make_env(conf)
+    ns = conf.nb_state
+    rng = np.random.default_rng(21)
+    N, B, K = 6000, 1024, 5
+    S = np.column_stack([rng.uniform(-15, 15, (N, 4)), rng.uniform(0, 9.9, N)])
+    rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.05, rng.normal(size=(N, ns)) * 0.3,
+                           (rng.uniform(size=(N, 1)) < 0.1).astype(float), np.zeros((N, 1))], axis=1)
+    storage = torch.as_tensor(rows, device="cuda")
+    idx = torch.as_tensor(rng.integers(0, N, size=(K, B)).astype(np.int32), device="cuda")
+    graphed = _learner(conf, env)
+    graphed.update_rows_n(storage, idx[:1])        # the handle's side stream, probe and workspace first
+    torch.cuda.synchronize()
+    ref = _learner(conf, env)
+    ref.update_rows_n(storage, idx[:1])
+    ref.update_rows_n(storage, idx)
+    ref.update_rows_n(storage, idx)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            graphed.update_rows_n(storage, idx)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(_state(ref), _state(graphed)):
+        assert torch.equal(a, b)
+    assert int(graphed.steps[0]) == 2 * K + 1
+    graphed.check_pipeline()
+    ref.check_pipeline()
+
+
 @pytest.mark.parametrize("system,B,K,MC", [("double_integrator", 128, 7, 0), ("double_integrator", 1000, 7, 0),
                                          ("manipulator", 64, 7, 0), ("double_integrator", 128, 1, 0),
                                          ("double_integrator", 128, 2, 0), ("double_integrator", 128, 8, 0),

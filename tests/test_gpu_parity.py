@@ -280,17 +280,16 @@ def test_rollout_di_known_answer():
 
 
 @pytest.mark.parametrize("system", ["double_integrator", "manipulator", "car_park", "ur5"])
-@pytest.mark.parametrize("ep,sched", [(1, (0, 0)), (1, (1, 3)), (0, (2, 2)), (1, (-3, 3)), (0, (-3, 2)), (1, (-4, 2)),
-                                     (0, (-4, 3))])
+@pytest.mark.parametrize("ep,sched", [(1, (0, 0)), (1, (1, 3)), (0, (2, 2)), (1, (-3, 3)), (0, (-3, 2)), (1, (4, 2))])
 def test_rollout_rewards_separate_launch(system, ep, sched):
     """cacto_rollout_rewards over a recorded S/A-only rollout gives exactly the R / EE of the
     combined cacto_rollout call (bench.py launches the two kernels apart) — under the automatic
     schedule and a slot-refilling one (1 group, 3 workgroups), with the actor and with zero
     controls (ep == 0), and with an episode of length 0 (EE_0 only)."""
-    if sched[0] == -3 and system in CHAINS:
-        pytest.skip("one slot per wave: systems without configuration-dependent M only")
-    if sched[0] == -4 and system != "manipulator":
-        pytest.skip("actor waves beside dynamics waves: the 3-joint chain only")
+    if sched[0] == -3 and system == "ur5":
+        pytest.skip("one slot per wave: systems without configuration-dependent M and the planar 3R chain")
+    if sched[0] == 4 and system != "manipulator":
+        pytest.skip("4 groups per workgroup: the manipulator's generic-kernel schedule")
     conf, genv, oe, nn, rl = _nets(system, None, seed=2)
     rng = random.Random(5)
     S0 = np.array([oe.reset(rng) for _ in range(37)])
@@ -393,17 +392,17 @@ def test_rollout_per_step_consistency(system):
                                           ("car_park", (-1, 3)), ("double_integrator", (-3, 3)),
                                           ("double_integrator", (-3, 1)), ("double_integrator", (-3, 6)),
                                           ("single_integrator", (-3, 2)), ("car_park", (-3, 2)),
-                                          ("car_park", (-3, 3)), ("car", (-3, 2)), ("manipulator", (-4, 1)),
-                                          ("manipulator", (-4, 2)), ("manipulator", (-4, 4))])
+                                          ("car_park", (-3, 3)), ("car", (-3, 2)), ("manipulator", (-3, 1)),
+                                          ("manipulator", (-3, 2)), ("manipulator", (-3, 4)), ("manipulator", (2, 3))])
 def test_rollout_slot_refill_matches_one_episode_per_slot(system, sched):
     """Few workgroups force every slot to run several episodes back to back (refill at the step
     boundary, zero-length episodes completed on the spot); every episode must come out exactly as
     in a schedule with one episode per slot, and agree with the oracle's step-by-step semantics.
     groups = -1: the two-team kernel (k_rollout_tt, two 4-slot teams per workgroup on team
     barriers); groups = -3: one slot per wave with layer 2 split over K across the waves
-    (k_rollout_ks, queue entries taken through an LDS counter); groups = -4: actor waves beside
-    dynamics waves, the two slot halves half a step apart (k_rollout_sw, the 3-joint chain) — all
-    against the single-team kernel's one-episode-per-slot schedule."""
+    (k_rollout_ks, queue entries taken through an LDS counter; the manipulator's default, its
+    planar closed-form dynamics) — all against the single-team kernel's one-episode-per-slot
+    schedule (k_rollout<NJ, 1>, for the manipulator the same planar3_step)."""
     conf, genv, oe, nn, rl = _nets(system, None, seed=4)
     rng = random.Random(11)
     n_ep = 45

@@ -2,32 +2,27 @@
 the sequential sample -> update_rows -> update_priorities_device loop, bit for bit, under every
 build-time-free schedule knob the pipeline reads once per process — so each combination runs in
 its own child process:
-  * CACTO_PIPE_EVERY2 = 0 / 1: cross-stream markers every iteration / every other iteration (the
-    default with PER), with the three-buffer critic rotation and the pidx[t % 3] ring;
-  * CACTO_PIPE_DEVWAIT = 1: that ordering on the device (the actor's GEMM publishes finished
-    chains, the critic's Adam polls) instead of queue markers, with a four-buffer PER index ring;
-    = 2: also the actor chain's wait on the critic's Adam (the critic's Adam publishes, the chain
-    polls before its critic pass; not with PER); = 3: that wait without fences (the Adam writes the
-    critic through to memory at agent scope, the chain polls relaxed);
-  * CACTO_PIPE_SIGNAL = 1: the side stream's wait on the critic's Adam as a stream write-value /
-    wait-value pair instead of an event;
+  * CACTO_PIPE_DEVWAIT = 0: cross-stream queue markers (every other iteration with PER, every
+    iteration without), the three-buffer critic rotation and the pidx[t % 3] ring; = 1: the
+    ordering on the device (the actor's GEMM publishes finished chains, the critic's Adam polls;
+    the critic's Adam writes the critic through to memory and publishes, the actor chain polls
+    relaxed), with a four-buffer PER index ring; unset: the library's own choice (device waits
+    after the handle's one-time concurrency probe);
   * CACTO_PER_FUSED = 0 / 1: the priority update (with the sampler's deferred exp_counter += 1) as
     the one-launch subtree kernel k_per_update_sub, or the round-3 chain k_per_count ->
     k_per_leaves_mw -> k_per_subtrees -> k_per_top;
-  * CACTO_PER_STREAM = 0 / 1: (with DEVWAIT >= 1) the priority update of update t and the sample of
-    t + 1 on a third stream beside the critic's GEMM and Adam, with a five-buffer index ring, or on
-    the critic stream;
   * CACTO_PER_DEEP_TOP = 0 / 1: the multi-workgroup sampler of round 4 or the 8,192-node one;
-  * CACTO_ACTOR_SPLIT = 1: (with DEVWAIT = 3) an actor chain of more tiles than CUs in launches
-    of at most 256 tiles, each waiting on the device;
-  * CACTO_PER_OVERLAP = 0 / 1: (with DEVWAIT >= 1, the default) the priority update of update t
+  * CACTO_PER_OVERLAP = 0 / 1: (with device waits, the default) the priority update of update t
     inside the critic GEMM's launch (k_wgrad_big_per: 256-leaf subtrees, the runs recorded by the
-    sampler) and the sample of t + 1 inside the critic Adam's (k_adam_sample: 4,096-node top).
+    sampler) and the sample of t + 1 inside the critic Adam's (k_adam_sample: 4,096-node top), or
+    both on the critic stream between its launches.
 The 4,096-node sampler is also checked standalone against the oracle at every descent split
-(CACTO_PER_TOP=4096, its own child).
+(CACTO_PER_TOP=4096, its own child). A device-side wait that times out (forced once per process by
+CACTO_PIPE_FAULT_INJECT=1) makes the learn_and_update call that ran it raise, and the handle runs
+again after that report (its own child).
 K = 6 and 7 (even / odd: the critic ends in the caller's buffer or a workspace copy), and the
-non-PER loop (DI, B = 1024, K = 7, and B = 8192, K = 5: more actor tiles than CUs) against
-sequential updates under the same knobs. Every child
+non-PER loop (DI, B = 1024, K = 7, and B = 8192, K = 5: more actor tiles than CUs, so the side
+stream keeps its queue marker) against sequential updates under the same knobs. Every child
 also writes the trees after a priority update with an unsorted index list holding duplicates
 (B = 1024, the fused kernel's filter path), and all children must agree on every byte.
 replay_buffer.py:139-218, RL.py:120-143."""
@@ -110,8 +105,8 @@ def _child():
         runs.append([t.cpu().numpy() for t in (rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf,
                                                rl.actor_m, rl.critic_v, rl.steps)])
     out["di_equal"] = all(np.array_equal(x, z) for x, z in zip(*runs))
-    # B = 8192: 512 actor tiles, more than the CUs (with CACTO_ACTOR_SPLIT=1 the actor chain is issued
-    # as launches of at most 256 tiles, each under the device-side wait)
+    # B = 8192: 512 actor tiles, more than the CUs (the side stream orders its actor chain with a queue
+    # marker; the critic stream's wait stays on the device)
     didx8 = torch.as_tensor(rng.integers(0, N, size=(5, 8192)).astype(np.int32), device="cuda")
     runs = []
     for pipelined in (False, True):
@@ -126,7 +121,8 @@ def _child():
         runs.append([t.cpu().numpy() for t in (rl8.actor_model.buf, rl8.critic_model.buf, rl8.target_critic.buf,
                                                rl8.actor_m, rl8.critic_v, rl8.steps)])
     out["di8192_equal"] = all(np.array_equal(x, z) for x, z in zip(*runs))
-    # no device-side wait of the pipeline ever timed out (cacto_pipeline_status word 1)
+    # no device-side wait of the pipeline ever timed out (cacto_pipeline_status word 1), and how the
+    # handle ordered the streams (word 3: 2 = device waits after the probe, 1 = queue markers)
     import ctypes
     from cacto_amd import _lib as L
     latch = 0
@@ -134,6 +130,7 @@ def _child():
         st = (ctypes.c_ulonglong * 4)()
         L.lib().call("cacto_pipeline_status", sysobj.handle, st)
         latch |= int(st[1])
+        out["probe"] = int(st[3])
     out["latch"] = latch
     # an unsorted index list with duplicates through the public priority update
     _, buf = setup()
@@ -153,23 +150,21 @@ def test_pipelined_per_b4096_equals_sequential_every_schedule():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = {}
-    for every2, fused, devwait, signal, pstream, deep, overlap, split in (
-            ("0", "1", "0", "0", "1", "1", "1", "0"), ("1", "1", "0", "0", "1", "1", "1", "0"),
-            ("1", "0", "0", "0", "1", "0", "1", "0"), ("0", "1", "1", "0", "1", "1", "1", "0"),
-            ("0", "1", "1", "0", "1", "1", "0", "0"), ("0", "1", "1", "0", "0", "0", "0", "0"),
-            ("0", "0", "1", "0", "1", "1", "0", "0"), ("0", "1", "2", "0", "1", "1", "1", "0"),
-            ("0", "1", "3", "0", "1", "1", "1", "0"), ("0", "1", "3", "0", "1", "1", "1", "1"),
-            ("0", "1", "1", "1", "1", "1", "1", "0")):
-        env = dict(os.environ, CACTO_PIPE_EVERY2=every2, CACTO_PER_FUSED=fused, CACTO_PIPE_DEVWAIT=devwait,
-                   CACTO_PIPE_SIGNAL=signal, CACTO_PER_STREAM=pstream, CACTO_PER_DEEP_TOP=deep,
-                   CACTO_PER_OVERLAP=overlap, CACTO_ACTOR_SPLIT=split)
+    for fused, devwait, deep, overlap in (("1", "0", "1", "1"), ("0", "0", "0", "1"), ("1", "1", "1", "1"),
+                                          ("1", "1", "1", "0"), ("0", "1", "0", "0"), ("1", None, "1", "1")):
+        env = dict(os.environ, CACTO_PER_FUSED=fused, CACTO_PER_DEEP_TOP=deep, CACTO_PER_OVERLAP=overlap)
+        env.pop("CACTO_PIPE_DEVWAIT", None)
+        if devwait is not None:
+            env["CACTO_PIPE_DEVWAIT"] = devwait
         r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
-        res[(every2, fused, devwait, signal, pstream, deep, overlap, split)] = json.loads(line[len("RESULT "):])
+        res[(fused, devwait, deep, overlap)] = json.loads(line[len("RESULT "):])
     for key, r in res.items():
         assert r["K6_equal"] and r["K7_equal"] and r["di_equal"] and r["di8192_equal"] and r["latch"] == 0, key
+    # the library's own choice on a GPU box: the two streams run concurrently, so device-side waits
+    assert res[("1", None, "1", "1")]["probe"] == 2, res[("1", None, "1", "1")]
     for field in ("K6_hash", "K7_hash", "unsorted_hash"):
         assert len({r[field] for r in res.values()}) == 1, field
 
@@ -227,8 +222,62 @@ def test_sampler_4096_top_every_depth():
     assert json.loads(line[len("RESULT "):])["ok"]
 
 
+def _timeout_child():
+    """learn_and_update (RL.py:120-143) on the two-stream pipeline with its first device-side wait
+    given an unreachable target (CACTO_PIPE_FAULT_INJECT=1): the wait gives up after its bound and
+    latches; the same call must raise, the report clears the latch, and the next call runs clean."""
+    import torch
+    sys.path.insert(0, ROOT)
+    from cacto_amd.confs import load_conf
+    from cacto_amd.environment import make_env
+    from cacto_amd.neural_network import NN
+    from cacto_amd.replay_buffer import ReplayBuffer
+    from cacto_amd.rl import RL_AC
+    conf = load_conf("double_integrator", fresh=True)
+    conf.BATCH_SIZE = 1024
+    conf.UPDATE_LOOPS = [6, 6]
+    conf.save_interval = 1000
+    conf.NNs_path = None
+    env = make_env(conf)
+    rng = np.random.default_rng(3)
+    N, ns = 8000, conf.nb_state
+    S = np.column_stack([rng.uniform(-3, 3, (N, ns - 1)), rng.uniform(0, 4.9, N)])
+    rows = np.concatenate([S, rng.normal(size=(N, 1)), S + 0.01, rng.normal(size=(N, ns)) * 0.3,
+                           np.zeros((N, 1)), np.zeros((N, 1))], axis=1)
+    rl = RL_AC(env, NN(env, conf, w_S=1e-2, seed=3), conf)
+    rl.setup_model()
+    buf = ReplayBuffer(conf, env.sys)
+    buf.add_rows(rows)
+    out = {}
+    try:
+        rl.learn_and_update(0, buf, 0, rng=np.random.default_rng(5))
+        out["raised"] = False
+    except RuntimeError as e:
+        out["raised"] = "timed out" in str(e)
+    rl.learn_and_update(6, buf, 1, rng=np.random.default_rng(6))   # the latch was collected: runs clean
+    torch.cuda.synchronize()
+    out["second_ok"] = True
+    print("RESULT " + json.dumps(out), flush=True)
+
+
+@pytest.mark.gpu
+def test_timed_out_device_wait_raises_in_the_same_learn_and_update_call():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, CACTO_PIPE_DEVWAIT="1", CACTO_PIPE_FAULT_INJECT="1")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "timeout"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    res = json.loads(line[len("RESULT "):])
+    assert res == {"raised": True, "second_ok": True}, res
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "sampler":
         _sampler_child()
+    elif len(sys.argv) > 1 and sys.argv[1] == "timeout":
+        _timeout_child()
     else:
         _child()

@@ -2,7 +2,7 @@
 CACTO_STAMPS build. Not part of the product path.
 
     python -c "from cacto_amd.build import build_variant; build_variant('libcacto_hip_stamps', ['CACTO_STAMPS'])"
-    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/rollout_stamps.py [system [R]]
+    CACTO_HIP_LIB=cacto_amd/libcacto_hip_stamps.so python tools/rollout_stamps.py [system [R [groups,workgroups]]]
 """
 import ctypes
 import os
@@ -26,8 +26,9 @@ def main():
     S0, n = bench.initial_states(env, conf, R, seed=0)
     T = int(n.max())
     inputs = rl.rollout_inputs(S0, n)
+    sched = tuple(int(x) for x in sys.argv[3].split(",")) if len(sys.argv) > 3 else None
     for _ in range(3):
-        out = rl.rollout_batch(None, None, T, inputs=inputs)
+        out = rl.rollout_batch(None, None, T, inputs=inputs, sched=sched or (0, 0))
     torch.cuda.synchronize()
     st = (ctypes.c_ulonglong * 20)()
     L.lib().dll.cacto_debug_rollout_stamps(st)
