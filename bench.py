@@ -57,6 +57,8 @@ def parse():
                    help="replay the update loop as one HIP graph (RL_AC.capture_updates) instead of launching "
                         "it eagerly; measured equal on MI355X (the update is bound by its kernels, not launches)")
     p.add_argument("--extra-systems", default="manipulator,car_park,ur5")
+    p.add_argument("--no-dp1", action="store_true",
+                   help="skip the one-rank RCCL data-parallel update leg (N = 1 only)")
     p.add_argument("--no-config0", action="store_true",
                    help="skip BASELINE configs[0] (single integrator, one main.py training iteration, GPU vs CPU)")
     p.add_argument("--no-diagnostics", action="store_true",
@@ -531,12 +533,12 @@ def update_phase(rl, buf, B, K, W, world, seed):
     W = max(W, UPDATE_WARMUP)
     gen = np.random.Generator(np.random.PCG64(seed))
     idx = torch.as_tensor(gen.integers(0, buf.max_idx(), size=(K + W, B)).astype(np.int32), device="cuda")
-    if world == 1 and not USE_GRAPH:
+    if (world == 1 and not USE_GRAPH) or rl._dp:
         rl.update_rows_n(buf.storage, idx[:W])     # warm-up on the timed path (creates its stream)
     else:
         for i in range(W):
             rl.update_rows(buf.storage, idx[i])
-    graph = rl.capture_updates(buf.storage, idx[W:]) if world == 1 and USE_GRAPH else None
+    graph = rl.capture_updates(buf.storage, idx[W:]) if world == 1 and USE_GRAPH and not rl._dp else None
     cuts = [W + j * K // 5 for j in range(6)]
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     barrier(world)
@@ -550,6 +552,7 @@ def update_phase(rl, buf, B, K, W, world, seed):
         for j in range(5):
             rl.update_rows_n(buf.storage, idx[cuts[j]:cuts[j + 1]])
             ev[j + 1].record()
+    HOST["enqueue_s"] = time.perf_counter() - t0
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
@@ -579,12 +582,14 @@ EXTRA = {
 def per_loop(rl, world):
     """The PER update loop learn_and_update runs (RL.py:122-137 between checkpoint saves): one rank
     calls RL_AC.update_rows_n_per (cacto_update_n_per: sample -> update -> priorities, pipelined on
-    two streams); N ranks call RL_AC.update_rows_n_per_dp (rl.py learn_and_update: each rank samples
-    its shard against the union's (sum, min, rows), the paired critic/actor gradients all-reduced in
-    two stages). None with --graph (the sequential loop replayed as one HIP graph)."""
-    if USE_GRAPH and world == 1:
+    two streams); N ranks (or one rank with an explicit RCCL group, the dp1 leg) call
+    RL_AC.update_rows_n_per_dp (rl.py learn_and_update: each rank samples its shard against the
+    union's (sum, min, rows), the paired critic/actor gradients all-reduced in two stages). None with
+    --graph (the sequential loop replayed as one HIP graph)."""
+    dp = world > 1 or rl._dp
+    if USE_GRAPH and not dp:
         return None
-    return rl.update_rows_n_per if world == 1 else rl.update_rows_n_per_dp
+    return rl.update_rows_n_per_dp if dp else rl.update_rows_n_per
 
 
 def per_update_phase(rl, buf, B, K, W, world, seed):
@@ -610,6 +615,7 @@ def per_update_phase(rl, buf, B, K, W, world, seed):
         for j in range(5):
             loop(buf, U[cuts[j]:cuts[j + 1]])       # sample -> update -> priorities, K/5 updates per call
             ev[j + 1].record()
+    HOST["enqueue_s"] = time.perf_counter() - t0
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
@@ -643,12 +649,62 @@ def extra_system(name, args, world, rank):
                                ms_per_update=1e3 * wall / args.update_steps, segments=seg,
                                tflops=flop * args.update_steps / wall / 1e12,
                                mfma_frac=flop * args.update_steps / wall / (FP32_MFMA_PEAK * world))
+    dp1 = None
+    if DP1_GROUP is not None and name in ("car_park", "ur5"):
+        dp1 = dp1_phase(rl, buf, cfg, args, ups["B=%d" % cfg["batches"][-1]])
     return dict(config=cfg["config"], env_steps_per_s=r["total_steps"] / r["wall"], rollouts_per_gpu=cfg["R"],
                 rollout_kernel_ms=r["kernel_ms"], env_steps_per_launch=r["steps_per_call"], segments=r["segments"],
                 long_region=r["long_region"],
                 rollout_mfma_frac=r["steps_per_call"] * fa_flops(ns, na) / (r["seq_kernel_ms"] * 1e-3) /
                 FP32_MFMA_PEAK,
-                w_S=cfg["w_S"], per=cfg["per"], critic_updates=ups, ddp_labels=ddp)
+                w_S=cfg["w_S"], per=cfg["per"], critic_updates=ups, ddp_labels=ddp, dp1_rccl=dp1)
+
+
+# host time of the last timed update region's issue (before its closing synchronize)
+HOST = {"enqueue_s": None}
+# a one-rank RCCL process group (N = 1 runs, unless --no-dp1): the data-parallel update loops of
+# configs[3] / configs[4] timed on one GPU
+DP1_GROUP = None
+
+
+def init_dp1_group():
+    """One-rank 'nccl' (RCCL) group on this GPU, the setup of tests/test_gpu_dp.py's RCCL tests: with an
+    explicit group RL_AC takes its data-parallel path (set_data_parallel) at world size 1."""
+    import torch.distributed as dist
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % free_port(), rank=0, world_size=1,
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    return dist.group.WORLD
+
+
+def dp1_phase(rl, buf, cfg, args, pipelined):
+    """The data-parallel update loop learn_and_update runs at N > 1 (RL_AC._update_rows_n_dp /
+    update_rows_n_per_dp: per update the paired [critic t | actor t-1] gradient stages, two async
+    RCCL all-reduces, the Adam steps; with PER the shard statistics all-gathered per sample) over a
+    one-rank RCCL group, at the configuration's per-GPU batch, beside the single-rank pipelined rate
+    of the same batch: the cost of the exchange path itself (host issue + collectives) without
+    other ranks, and its host issue time per update. (Its HIP-graph form, RL_AC.capture_updates over
+    RCCL, is not timed here: a capture as long as this loop trips the RCCL process group's watchdog,
+    which polls an event recorded inside the capture.)"""
+    B = cfg["batches"][-1]
+    K = args.update_steps
+    rl.set_data_parallel(1, DP1_GROUP)
+    if cfg["per"]:
+        buf.set_data_parallel(1, DP1_GROUP)     # the shard statistics all-gathered per sample
+    try:
+        if cfg["per"]:
+            wall, seg, loop = per_update_phase(rl, buf, B, K, 3, 1, seed=400)
+        else:
+            wall, seg = update_phase(rl, buf, B, K, 3, 1, seed=400)
+            loop = "_update_rows_n_dp"
+        enq = HOST["enqueue_s"]
+    finally:
+        rl.set_data_parallel(1, None)
+        if cfg["per"]:
+            buf.set_data_parallel(1, None)
+    rate = K / wall
+    return dict(batch=B, loop=loop, updates_per_s=rate, ms_per_update=1e3 * wall / K, segments=seg,
+                host_enqueue_us_per_update=1e6 * enq / K, pipelined_single_rank_updates_per_s=pipelined["value"],
+                vs_pipelined=rate / pipelined["value"])
 
 
 def cpu_baseline_rollout(conf, rl, roll, seconds):
@@ -815,6 +871,12 @@ def flat_summary(updates, upd_roof, extra, world):
             b = k.split("=")[1]
             out["%s_updates_per_s_b%s" % (name, b)] = u["value"]
             out["%s_update_mfma_frac_b%s" % (name, b)] = u["mfma_frac"]
+        d = e.get("dp1_rccl")
+        if d:
+            pre = "dp1_rccl_%s_b%d_" % (name, d["batch"])
+            out[pre + "updates_per_s"] = d["updates_per_s"]
+            out[pre + "host_us_per_update"] = d["host_enqueue_us_per_update"]
+            out[pre + "vs_pipelined"] = d["vs_pipelined"]
     return out
 
 
@@ -858,6 +920,9 @@ def main():
                                    ms_per_update=1e3 * wall / K, tflops=flop * K / wall / 1e12,
                                    mfma_frac=flop * K / wall / (FP32_MFMA_PEAK * world), segments=seg)
     extra = {}
+    global DP1_GROUP
+    if world == 1 and not args.no_dp1 and ("car_park" in args.extra_systems or "ur5" in args.extra_systems):
+        DP1_GROUP = init_dp1_group()
     for sysname in [s for s in args.extra_systems.split(",") if s and s != args.system]:
         extra[sysname] = extra_system(sysname, args, world, rank)
     cpu = None
@@ -946,7 +1011,7 @@ def main():
             line["di_update_counter_over_algorithmic_b%d" % Bu] = r["counter_over_algorithmic"]
             line["di_update_counter_bytes_b%d" % Bu] = r["counter_bytes_per_update"]
         print(json.dumps(line))
-    if world > 1:
+    if world > 1 or DP1_GROUP is not None:
         import torch.distributed as dist
         dist.destroy_process_group()
 

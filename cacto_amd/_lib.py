@@ -81,6 +81,14 @@ _SIGS = {
     "cacto_update_n": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, C.c_int, C.c_int, vp, sz, vp]),
     "cacto_update_n_per": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, i64, i64, C.c_double, vp,
                                      vp, C.c_double, C.c_double, C.c_double, vp, C.c_int, C.c_int, vp, sz, vp]),
+    "cacto_dp_unique_ids": (C.c_int, [vp, C.c_int]),
+    "cacto_dp_attach": (C.c_int, [vp, vp, C.c_int, C.c_int]),
+    "cacto_dp_detach": (C.c_int, [vp]),
+    "cacto_update_n_dp": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, C.c_int, C.c_int, vp, sz,
+                                    vp]),
+    "cacto_update_n_per_dp": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, i64, i64, C.c_double,
+                                        vp, vp, C.c_double, C.c_double, C.c_double, vp, C.c_int, C.c_int, vp, sz,
+                                        vp]),
     "cacto_update_pair_grads": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, vp, C.c_int, vp, vp,
                                           vp, vp, sz, vp]),
     "cacto_update_pair_grads_stage": (C.c_int, [vp, C.POINTER(Nets), C.POINTER(UpdateCfg), vp, vp, vp, vp, C.c_int,

@@ -157,6 +157,7 @@ extern "C" int cacto_sys_destroy(cacto_sys* sys) {
   for (int32_t* t : sys->wa_items)
     if (t) (void)hipFree(t);
   if (sys->side) (void)hipStreamSynchronize(sys->side);
+  cacto_dp_release(sys);
   if (sys->ev_critic) (void)hipEventDestroy(sys->ev_critic);
   for (hipEvent_t e : sys->ev_actor)
     if (e) (void)hipEventDestroy(e);

@@ -28,6 +28,13 @@ struct cacto_sys {
   unsigned long long* pipe_sig = nullptr;
   unsigned long long pipe_seq = 0;
   int pipe_probe = -1;
+  // data-parallel updates over RCCL (cacto_dp_attach): one communicator per stream of the pipeline
+  // (critic stream, side stream: each orders its own collectives), the all-reduced gradients (one
+  // flat buffer per network) and the PER shard statistics ([3] this rank's, [world][3] all ranks')
+  void* dp_comm[2] = {nullptr, nullptr};
+  int dp_rank = 0, dp_world = 0;
+  float *dp_gc = nullptr, *dp_ga = nullptr;
+  double* dp_stats = nullptr;
   // k_wgrad_adam work lists, [8 XCD bins][wa_stride] item codes (layer << 16 | net << 15 | item, -1 = none), for
   // the critic alone, the actor alone and both (built at creation, cacto_build_wgrad_adam_items)
   int32_t* wa_items[3] = {nullptr, nullptr, nullptr};
@@ -43,6 +50,7 @@ inline int64_t flat_span(const NetTopo& t) { return ((int64_t)t.params + 63) / 6
 cacto::NetView cacto_make_view(const cacto_sys* sys, int net, const float* netbuf);
 int cacto_const_dyn_init(cacto_sys* sys);  // SysDevice::cd_* of a prismatic-only chain (env_kernels.hip)
 int cacto_build_wgrad_adam_items(cacto_sys* sys);  // learn_kernels.hip
+void cacto_dp_release(cacto_sys* sys);  // learn_kernels.hip: the RCCL communicators and buffers
 // replay_kernels.hip: batches from this size on take the multi-workgroup PER kernels; the update
 // pipelines then issue the sample's exp_counter increment just before the priority update (its only
 // reader), off the sample -> critic chain path
@@ -53,4 +61,5 @@ int cacto_per_update_count(double* sum_tree_d, double* min_tree_d, int64_t capac
                            double alpha, double* max_priority_d, int B, hipStream_t st);
 int cacto_per_sample_runs_launch(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
                                  double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
-                                 int32_t* runs_d, hipStream_t st);
+                                 int32_t* runs_d, hipStream_t st, const double* shards_d = nullptr,
+                                 int n_shards = 0);

@@ -12,6 +12,7 @@
 //   -> k_adam : sum chunks in fixed order (deterministic), Adam, packed copies, soft update.
 #include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -2638,7 +2639,7 @@ int update_pipeline_body(const cacto_sys* sys, const cacto_nets* nets, const cac
     PerSampleArgs psa{};
     if (ovl) {
       pra = PerRunArgs{per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->max_idx,
-                       per->fresh, per->eps, per->alpha, per->max_priority, w.runs};
+                       per->fresh, per->eps, per->alpha, per->max_priority, w.runs, nullptr};
       if (t + 1 < K)
         psa = PerSampleArgs{per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
                             per->uniforms + (size_t)(t + 1) * B, B, w.pidx + (size_t)((t + 1) % nring) * w.Bp,
@@ -2729,4 +2730,297 @@ extern "C" int cacto_update_n_per(const cacto_sys* sys, const cacto_nets* nets, 
   if (fused_adam(w.Bp))
     return update_pipeline_pair(sys, nets, cfg, storage_d, nullptr, &per, K, B, w, as_stream(stream));
   return update_pipeline(sys, nets, cfg, storage_d, nullptr, &per, K, B, w, as_stream(stream));
+}
+
+// ---------------------------------------------------------------- data-parallel pipeline (RCCL)
+// The data-parallel learn_and_update (main.py:219-225 runs the reference's loop on one process; here
+// one process per GPU, the gradients all-reduced over xGMI). The K updates of a call run as the
+// two-stream pipeline of cacto_update_n with each network's exchange inside its own stream:
+//   stream : [PER: shard stats -> all-gather -> stratified sample over the union] critic chain(t) ->
+//            weight-gradient GEMM -> slab reduce -> all-reduce (comm 0) -> Adam(t) (+ soft target
+//            update) [-> PER priority update]
+//   side   : [marker: Adam(t)] actor chain(t) against C_{t+1} -> GEMM -> reduce -> all-reduce (comm 1)
+//            -> Adam
+// Every rank issues the same collectives in the same order on each communicator, one communicator
+// per stream, so neither stream's collectives can interleave with the other's. The streams are
+// ordered with queue markers (no device-side polls beside collectives that wait for other ranks).
+// The gradients are scaled by 1/B_global inside the chain kernels, so the exchange is a plain sum;
+// every rank applies the same Adam to the same sum, so the replicas stay bit-identical. With one
+// rank the all-reduce is the identity and the result equals cacto_update_n / the Python
+// dp_pipeline bit for bit (tests/test_gpu_dp.py). The host issues ~14 HIP / RCCL calls per update
+// (the Python loop of RL_AC issued ~10 ctypes calls and two torch.distributed collectives: ~160 us
+// of host time per update, more than the GPU's).
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+namespace {
+// RCCL entry points of the copy already in the process (torch.distributed's, found by soname), else
+// the ROCm library: no link-time dependency, one RCCL instance per process.
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGetErrorString) err = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+    if (!h) return x;
+    x.get_id = reinterpret_cast<decltype(x.get_id)>(dlsym(h, "ncclGetUniqueId"));
+    x.init = reinterpret_cast<decltype(x.init)>(dlsym(h, "ncclCommInitRank"));
+    x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    x.all_gather = reinterpret_cast<decltype(x.all_gather)>(dlsym(h, "ncclAllGather"));
+    x.err = reinterpret_cast<decltype(x.err)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.get_id && x.init && x.destroy && x.all_reduce && x.all_gather && x.err;
+    return x;
+  }();
+  return r;
+}
+
+int rccl_fail(ncclResult_t r, const char* what) {
+  set_error(std::string(what) + ": " + (rccl().err ? rccl().err(r) : "RCCL error"));
+  return CACTO_EHIP;
+}
+#define CACTO_CHECK_RCCL(call, what)            \
+  do {                                          \
+    const ncclResult_t r_ = (call);             \
+    if (r_ != ncclSuccess) return rccl_fail(r_, what); \
+  } while (0)
+
+int update_pipeline_dp_body(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                            const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
+                            const Workspace& w, hipStream_t st, int* cbuf) {
+  cacto_sys* ms = const_cast<cacto_sys*>(sys);
+  const Rccl& R = rccl();
+  ncclComm_t cc = static_cast<ncclComm_t>(ms->dp_comm[0]), ca = static_cast<ncclComm_t>(ms->dp_comm[1]);
+  hipStream_t side = ms->side;
+  const int Pc = sys->critic.params, Pa = sys->actor.params;
+  const size_t nb_stride = align64((size_t)flat_span(sys->critic) + (size_t)2 * sys->critic.blocks * 256);
+  float* const buf[3] = {nets->critic_d, w.cshadow, w.cshadow + nb_stride};
+  float* const y = w.scal;
+  float* const V = w.scal + w.Bp;
+  const bool sob = cfg->w_S != 0.0;
+  const int soft = cfg->MC ? 0 : 1;
+  // queue markers: every other iteration with PER, every iteration without (update_pipeline_body)
+  const bool every2 = per != nullptr;
+  // PER in the critic's GEMM and Adam launches (per_overlap_ok, as cacto_update_n_per): the priority
+  // update of update t inside the GEMM's launch, then this shard's statistics and their all-gather,
+  // and the sample of t + 1 (IS weights over the union) inside the Adam's launch; the index ring has
+  // five buffers (sample t + 1 overwrites the one actor chain t - 4 read, which the marker before
+  // update t - 1 or t covers). Otherwise the sample and the priority update run between the launches.
+  const bool ovl = per && per_overlap_ok(sys, cfg, per, B, w);
+  const int nring = ovl ? 5 : 3;
+  const int nroot = per ? (int)(per->cap / PER_RUN_SUB) : 0;
+  double* const stats = ms->dp_stats;       // [3] this shard
+  double* const shards = ms->dp_stats + 3;  // [world][3]
+  auto gather_stats = [&]() -> int {
+    if (int e = cacto_per_shard_stats(per->sum_tree, per->min_tree, per->max_idx, stats, st)) return e;
+    CACTO_CHECK_RCCL(R.all_gather(stats, shards, 3, ncclFloat64, cc, st), "ncclAllGather(PER shards)");
+    return CACTO_OK;
+  };
+  for (int t = 0; t < K; ++t) {
+    if (every2) {
+      if (t >= 2 && (t & 1) == 0) CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[((t - 2) >> 1) & 1], 0));
+    } else if (t >= 3) {
+      CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_actor[t % 3], 0));
+    }
+    const int32_t* idx = idx_d + (size_t)t * B;
+    const float* isw = nullptr;
+    if (per) {
+      // replay_buffer.py:139-188 over the union of the ranks' shards: this shard's (sum, min, rows),
+      // all-gathered, then the stratified sample with IS weights against the union
+      int32_t* pi = w.pidx + (size_t)(t % nring) * w.Bp;
+      if (ovl) {
+        if (t == 0) {  // the first sample, recording its runs; later ones run inside the Adam launch
+          CACTO_CHECK_HIP(hipMemsetAsync(w.runs, 0x7f, (size_t)nroot * sizeof(int32_t), st));
+          CACTO_CHECK_HIP(hipMemsetAsync(w.runs + nroot, 0, (size_t)nroot * sizeof(int32_t), st));
+          if (int e = gather_stats()) return e;
+          if (int e = cacto_per_sample_runs_launch(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                                   per->uniforms, B, pi, w.pisw, w.runs, st, shards, ms->dp_world))
+            return e;
+        }
+      } else {
+        if (int e = gather_stats()) return e;
+        if (int e = cacto_per_sample_global(per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                                            per->uniforms + (size_t)t * B, B, shards, ms->dp_world, pi, w.pisw,
+                                            per->exp_counter, st))
+          return e;
+      }
+      idx = pi;
+      isw = w.pisw;
+    }
+    cacto_nets cur = *nets, nxt = *nets;
+    cur.critic_d = buf[t % 3];
+    nxt.critic_d = buf[(t + 1) % 3];
+    if (int e = launch_critic_chain(sys, &cur, cfg, storage_d, idx, isw, B, y, V, nullptr, w, st)) return e;
+    int nch = 0;
+    PerRunArgs pra{};
+    PerSampleArgs psa{};
+    if (ovl) {
+      // the trees after priority update t: the statistics sample t + 1 weighs against, written by the
+      // workgroup of the GEMM's launch that rebuilds the top of the trees (with one subtree, a launch)
+      pra = PerRunArgs{per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->max_idx,
+                       per->fresh, per->eps, per->alpha, per->max_priority, w.runs,
+                       t + 1 < K && nroot > 1 ? stats : nullptr};
+      if (t + 1 < K)
+        psa = PerSampleArgs{per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
+                            per->uniforms + (size_t)(t + 1) * B, B, w.pidx + (size_t)((t + 1) % nring) * w.Bp,
+                            w.pisw, shards, ms->dp_world, w.runs};
+    }
+    if (int e = launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, &nch, nullptr, 0,
+                             ovl ? &pra : nullptr))
+      return e;
+    if (ovl && t + 1 < K) {
+      if (nroot > 1)
+        CACTO_CHECK_RCCL(R.all_gather(stats, shards, 3, ncclFloat64, cc, st), "ncclAllGather(PER shards)");
+      else if (int e = gather_stats())
+        return e;
+    }
+    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pc + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, Pc, ms->dp_gc);
+    CACTO_CHECK_HIP(hipGetLastError());
+    CACTO_CHECK_RCCL(R.all_reduce(ms->dp_gc, ms->dp_gc, (size_t)Pc, ncclFloat32, ncclSum, cc, st),
+                     "ncclAllReduce(critic gradient)");
+    cacto_nets dst = *nets;
+    dst.critic_d = nxt.critic_d;
+    if (int e = launch_adam(sys, &dst, cfg, CACTO_NET_CRITIC, ms->dp_gc, 1, soft, st, cur.critic_d, nullptr, 0, nullptr,
+                            0, ovl && t + 1 < K ? &psa : nullptr))
+      return e;
+    *cbuf = (t + 1) % 3;
+    CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+    if (per && !ovl)
+      if (int e = per_priority_update(per, idx, y, V, B, false, st)) return e;
+    CACTO_CHECK_HIP(hipStreamWaitEvent(side, ms->ev_critic, 0));
+    if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
+    int ncha = 0;
+    if (int e = launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, side, &ncha)) return e;
+    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, side, w.slab_a, ncha, Pa,
+                       ms->dp_ga);
+    CACTO_CHECK_HIP(hipGetLastError());
+    CACTO_CHECK_RCCL(R.all_reduce(ms->dp_ga, ms->dp_ga, (size_t)Pa, ncclFloat32, ncclSum, ca, side),
+                     "ncclAllReduce(actor gradient)");
+    if (int e = launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, ms->dp_ga, 1, 0, side)) return e;
+    if (!every2) {
+      CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[t % 3], side));
+    } else if ((t & 1) == 0) {
+      CACTO_CHECK_HIP(hipEventRecord(ms->ev_actor[(t >> 1) & 1], side));
+    }
+  }
+  return CACTO_OK;
+}
+
+int update_pipeline_dp(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                       const double* storage_d, const int32_t* idx_d, const PerArgs* per, int K, int B,
+                       const Workspace& w, hipStream_t st) {
+  cacto_sys* ms = const_cast<cacto_sys*>(sys);
+  std::lock_guard<std::mutex> lock(ms->pipe_mu);
+  if (!ms->dp_comm[0] || !ms->dp_comm[1]) {
+    set_error("cacto_update_n_dp: no RCCL communicators on this handle (cacto_dp_attach)");
+    return CACTO_EINVAL;
+  }
+  if (int e = ensure_side_stream(ms)) return e;
+  const NetTopo& tc = sys->critic;
+  const size_t nb_bytes = ((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256) * sizeof(float);
+  const size_t nb_stride = align64((size_t)flat_span(tc) + (size_t)2 * tc.blocks * 256);
+  CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
+  CACTO_CHECK_HIP(hipMemcpyAsync(w.cshadow + nb_stride, nets->critic_d, nb_bytes, hipMemcpyDeviceToDevice, st));
+  CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, st));
+  CACTO_CHECK_HIP(hipStreamWaitEvent(ms->side, ms->ev_critic, 0));
+  int cbuf = 0;
+  const int err = update_pipeline_dp_body(sys, nets, cfg, storage_d, idx_d, per, K, B, w, st, &cbuf);
+  CACTO_CHECK_HIP(hipEventRecord(ms->ev_critic, ms->side));
+  CACTO_CHECK_HIP(hipStreamWaitEvent(st, ms->ev_critic, 0));
+  if (cbuf)
+    CACTO_CHECK_HIP(hipMemcpyAsync(nets->critic_d, w.cshadow + (cbuf - 1) * nb_stride, nb_bytes,
+                                   hipMemcpyDeviceToDevice, st));
+  return err;
+}
+}  // namespace
+
+void cacto_dp_release(cacto_sys* sys) {
+  for (void*& c : sys->dp_comm) {
+    if (c && rccl().ok) (void)rccl().destroy(static_cast<ncclComm_t>(c));
+    c = nullptr;
+  }
+  if (sys->dp_gc) (void)hipFree(sys->dp_gc);
+  if (sys->dp_ga) (void)hipFree(sys->dp_ga);
+  if (sys->dp_stats) (void)hipFree(sys->dp_stats);
+  sys->dp_gc = sys->dp_ga = nullptr;
+  sys->dp_stats = nullptr;
+  sys->dp_rank = sys->dp_world = 0;
+}
+
+extern "C" int cacto_dp_unique_ids(void* out_h, int n) {
+  CACTO_REQUIRE(out_h && n >= 1 && n <= 16, "cacto_dp_unique_ids: bad arguments");
+  const Rccl& R = rccl();
+  CACTO_REQUIRE(R.ok, "cacto_dp_unique_ids: RCCL (librccl.so.1) not found");
+  for (int k = 0; k < n; ++k) {
+    ncclUniqueId id;
+    CACTO_CHECK_RCCL(R.get_id(&id), "ncclGetUniqueId");
+    std::memcpy(static_cast<char*>(out_h) + (size_t)k * sizeof(ncclUniqueId), &id, sizeof(ncclUniqueId));
+  }
+  return CACTO_OK;
+}
+
+extern "C" int cacto_dp_attach(cacto_sys* sys, const void* ids_h, int rank, int world) {
+  CACTO_REQUIRE(sys && ids_h && world >= 1 && rank >= 0 && rank < world, "cacto_dp_attach: bad arguments");
+  const Rccl& R = rccl();
+  CACTO_REQUIRE(R.ok, "cacto_dp_attach: RCCL (librccl.so.1) not found");
+  std::lock_guard<std::mutex> lock(sys->pipe_mu);
+  cacto_dp_release(sys);
+  for (int k = 0; k < 2; ++k) {
+    ncclUniqueId id;
+    std::memcpy(&id, static_cast<const char*>(ids_h) + (size_t)k * sizeof(ncclUniqueId), sizeof(ncclUniqueId));
+    ncclComm_t c = nullptr;
+    CACTO_CHECK_RCCL(R.init(&c, world, id, rank), "ncclCommInitRank");
+    sys->dp_comm[k] = c;
+  }
+  CACTO_CHECK_HIP(hipMalloc(&sys->dp_gc, sizeof(float) * sys->critic.params));
+  CACTO_CHECK_HIP(hipMalloc(&sys->dp_ga, sizeof(float) * sys->actor.params));
+  CACTO_CHECK_HIP(hipMalloc(&sys->dp_stats, sizeof(double) * 3 * (world + 1)));
+  sys->dp_rank = rank;
+  sys->dp_world = world;
+  return CACTO_OK;
+}
+
+extern "C" int cacto_dp_detach(cacto_sys* sys) {
+  CACTO_REQUIRE(sys, "cacto_dp_detach: bad arguments");
+  std::lock_guard<std::mutex> lock(sys->pipe_mu);
+  if (sys->side) CACTO_CHECK_HIP(hipStreamSynchronize(sys->side));
+  cacto_dp_release(sys);
+  return CACTO_OK;
+}
+
+extern "C" int cacto_update_n_dp(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                 const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
+                                 size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && idx_d && B > 0 && K >= 0, "cacto_update_n_dp: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  if (K == 0) return CACTO_OK;
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  return update_pipeline_dp(sys, nets, cfg, storage_d, idx_d, nullptr, K, B, w, as_stream(stream));
+}
+
+extern "C" int cacto_update_n_per_dp(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                                     const double* storage_d, double* sum_tree_d, double* min_tree_d, int64_t capacity,
+                                     int64_t max_idx, double beta, const double* uniforms_d, double* exp_counter_d,
+                                     double fresh_factor, double eps, double alpha, double* max_priority_d, int K,
+                                     int B, void* workspace_d, size_t workspace_bytes, void* stream) {
+  CACTO_REQUIRE(sys && cfg && storage_d && sum_tree_d && min_tree_d && uniforms_d && exp_counter_d &&
+                    max_priority_d && B > 0 && K >= 0,
+                "cacto_update_n_per_dp: bad arguments");
+  if (int e = check_nets(nets)) return e;
+  CHECK_WS(workspace_d, workspace_bytes, B);
+  if (K == 0) return CACTO_OK;
+  const Workspace w = plan(sys, B, static_cast<char*>(workspace_d));
+  const PerArgs per{sum_tree_d, min_tree_d, capacity, max_idx, beta, fresh_factor, eps, alpha, uniforms_d,
+                    exp_counter_d, max_priority_d};
+  return update_pipeline_dp(sys, nets, cfg, storage_d, nullptr, &per, K, B, w, as_stream(stream));
 }

@@ -306,6 +306,9 @@ struct PerRunArgs {
   double fresh, eps, alpha;
   double* max_priority;
   int32_t* runs;  // the sampler's per-subtree runs, reset here for the next sample
+  // data parallel (cacto_update_n_per_dp): this shard's (sum, min, rows) after the update, written by
+  // the workgroup that rebuilds the top (k_per_shard_stats' values), for the all-gather; or nullptr
+  double* stats;
 };
 
 struct PerRunLds {
@@ -419,7 +422,14 @@ __device__ __forceinline__ void per_update_run_body(int blk, int nroot, const Pe
     }
     __syncthreads();
   }
-  if (tid == 0) __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // +0.0, node 0
+  if (tid == 0) {
+    __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // +0.0, node 0
+    if (a.stats) {
+      a.stats[0] = L.ts[1];
+      a.stats[1] = L.tm[1];
+      a.stats[2] = (double)a.rows;
+    }
+  }
 }
 
 }  // namespace cacto

@@ -808,10 +808,10 @@ extern "C" int cacto_debug_per_stamps(unsigned long long* out_h) {  // [64][8], 
 // runs (runs_d: 2 cap / PER_RUN_SUB ints, PER_RUN_EMPTY / 0 on entry).
 int cacto_per_sample_runs_launch(const double* sum_tree_d, const double* min_tree_d, int64_t capacity, int64_t max_idx,
                                  double beta, const double* uniforms_d, int B, int32_t* idx_d, float* is_w_d,
-                                 int32_t* runs_d, hipStream_t st) {
+                                 int32_t* runs_d, hipStream_t st, const double* shards_d, int n_shards) {
   using namespace cacto;
   const PerSampleArgs sa{sum_tree_d, min_tree_d, capacity, max_idx, beta, uniforms_d, B, idx_d, is_w_d,
-                         nullptr, 0, runs_d};
+                         shards_d, n_shards, runs_d};
   hipLaunchKernelGGL(k_per_sample_runs, dim3((B + 255) / 256), dim3(256), 0, st, sa);
   CACTO_CHECK_HIP(hipGetLastError());
   return CACTO_OK;

@@ -29,13 +29,22 @@ def layer_shapes(kind, ns, na):
 
 
 # Keras layer names of the reference's three models in one process (the .h5 files it writes,
-# e.g. Results Double Integrator/.../N_try_6/{actor,critic,target_critic}_0.h5)
+# e.g. Results Double Integrator/.../N_try_6/{actor,critic,target_critic}_0.h5): Keras numbers each
+# layer class separately in creation order (actor, critic, target critic, RL.py:52-76), so the
+# sine-elu critic's Dense elu layers continue the actor's dense_* count (NeuralNetwork.py:80-93)
 LAYER_NAMES = {
     "actor": ["dense", "dense_1", "dense_2"],
     "critic": ["sinusodial_representation_dense", "sinusodial_representation_dense_1",
                "sinusodial_representation_dense_2", "sinusodial_representation_dense_3", "dense_3"],
     "target": ["sinusodial_representation_dense_4", "sinusodial_representation_dense_5",
                "sinusodial_representation_dense_6", "sinusodial_representation_dense_7", "dense_4"],
+}
+LAYER_NAMES_SINE_ELU = {
+    "actor": LAYER_NAMES["actor"],
+    "critic": ["sinusodial_representation_dense", "dense_3", "sinusodial_representation_dense_1", "dense_4",
+               "dense_5"],
+    "target": ["sinusodial_representation_dense_2", "dense_6", "sinusodial_representation_dense_3", "dense_7",
+               "dense_8"],
 }
 
 
@@ -50,6 +59,13 @@ class Net:
         self.P = sys.param_count(kind)
         assert self.P == sum(int(np.prod(s)) for s in self.shapes)
         self.buf = torch.zeros(sys.netbuf_floats(kind), dtype=torch.float32, device=DEVICE)
+        # the critic activations belong to the system handle: a critic net fixes them (System.set_critic_type)
+        self.critic_type = getattr(sys, "critic_type", "sine") if kind == CRITIC else None
+        if kind == CRITIC:
+            if getattr(sys, "critic_nets", None) is None:
+                import weakref
+                sys.critic_nets = weakref.WeakSet()
+            sys.critic_nets.add(self)
 
     @property
     def flat(self):
@@ -98,7 +114,7 @@ class Net:
         writer, cacto_amd/h5.py), else an .npz of the Keras-order arrays."""
         ws = self.get_weights()
         if str(path).endswith(".h5"):
-            names = LAYER_NAMES[self.role]
+            names = (LAYER_NAMES_SINE_ELU if self.critic_type == "sine-elu" else LAYER_NAMES)[self.role]
             h5.write_keras_weights(path, [(n, [(n + "/kernel:0", ws[2 * i]), (n + "/bias:0", ws[2 * i + 1])])
                                           for i, n in enumerate(names)])
         else:

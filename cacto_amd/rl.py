@@ -188,16 +188,40 @@ class RL_AC:
 
     dp_world = 1
     dp_group = None
+    _dp_native = False
 
     def set_data_parallel(self, world_size, group=None):
-        """Replicated weights, local minibatch per rank, RCCL all-reduce of the gradients: per
-        update [critic gradient of update t | actor gradient of update t-1] (dp_pipeline), the
-        critic part's all-reduce issued as soon as it is formed, which keeps RL.py:104-109's order
-        (the actor gradient is taken against the critic after its own update). An explicit `group`
-        selects the exchange path even for world_size 1 (a one-rank RCCL group: the path the
-        graph-capture test runs on a one-GPU box)."""
+        """Replicated weights, local minibatch per rank, all-reduce of the gradients. An explicit
+        `group` selects the exchange path even for world_size 1 (a one-rank RCCL group: the path
+        the one-GPU box can run).
+
+        Over RCCL (a process group of backend 'nccl') the K updates of a call run in the library
+        (cacto_update_n_dp / cacto_update_n_per_dp): the two-stream pipeline of cacto_update_n
+        with each network's gradient all-reduced on its own stream's RCCL communicator, created
+        here (cacto_dp_attach; rank 0's unique ids broadcast over the group). Otherwise (gloo: the
+        CPU tests and the one-GPU multi-rank rehearsal), or with CACTO_DP_NATIVE=0, the host loop
+        dp_pipeline: per update [critic gradient of update t | actor gradient of update t-1], the
+        critic part's all-reduce issued as soon as it is formed. Both keep RL.py:104-109's order
+        (the actor gradient is taken against the critic after its own update)."""
         self.dp_world = int(world_size)
         self.dp_group = group
+        self._dp_native = False
+        if not self._dp or os.environ.get("CACTO_DP_NATIVE", "1") == "0":
+            return
+        import torch.distributed as dist
+        if not dist.is_initialized() or dist.get_backend(group) != "nccl":
+            return
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        if world != self.dp_world and group is None:
+            raise ValueError("set_data_parallel(%d): the default process group has %d ranks" % (self.dp_world, world))
+        ids = C.create_string_buffer(2 * 128)
+        if rank == 0:
+            L.lib().call("cacto_dp_unique_ids", ids, 2)
+        obj = [ids.raw]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        ids = C.create_string_buffer(obj[0], 2 * 128)
+        L.lib().call("cacto_dp_attach", self.sys.handle, ids, rank, world)
+        self._dp_native = True
 
     @property
     def _dp(self):
@@ -346,9 +370,11 @@ class RL_AC:
         self._update_rows_n_dp(storage, idx.reshape(1, -1), is_w, y, V)
 
     def _update_rows_n_dp(self, storage, idx_steps, is_w=None, y=None, V=None):
-        """K data-parallel updates through dp_pipeline: per step one C-ABI call for the paired
-        gradients (critic of update t, actor of update t-1) into one buffer, one RCCL all-reduce of
-        it on the current stream, one call for the Adam steps. is_w / y / V only with K = 1 (PER)."""
+        """K data-parallel updates. Over RCCL: one cacto_update_n_dp call (the two-stream pipeline,
+        each network's gradient all-reduced on its stream's communicator). Otherwise dp_pipeline:
+        per step one C-ABI call for the paired gradients (critic of update t, actor of update t-1)
+        into one buffer, the all-reduces through torch.distributed, one call for the Adam steps.
+        is_w / y / V only with K = 1 (PER)."""
         import torch.distributed as dist
         K, B = int(idx_steps.shape[0]), int(idx_steps.shape[1])
         if K != 1 and (is_w is not None or y is not None or V is not None):
@@ -356,6 +382,11 @@ class RL_AC:
                              "K PER updates go through update_rows_n_per_dp")
         ws = self.workspace(B)
         cfg = self._cfg_for(B)
+        if self._dp_native and is_w is None and y is None and V is None:
+            L.lib().call("cacto_update_n_dp", self.sys.handle, C.byref(self.nets), C.byref(cfg),
+                         dptr(storage, torch.float64), dptr(idx_steps.contiguous(), torch.int32), K, B, dptr(ws),
+                         ws.numel() * 4, stream())
+            return
         Pc, Pa = self.critic_model.P, self.actor_model.P
         g = self._dp_grad_buf(Pc + Pa)
         idx_steps = idx_steps.contiguous()
@@ -399,12 +430,22 @@ class RL_AC:
         rank's random.random() draws, in order) go to the device in one copy. Every kernel sees the
         inputs of the sequential loop (sample -> update -> priorities), so the result equals K
         update_rows + update_priorities_device calls (bit for bit when the collective's sums are
-        order-independent, e.g. two ranks)."""
+        order-independent, e.g. two ranks). Over RCCL the whole loop is one cacto_update_n_per_dp
+        call (the shard statistics all-gathered on the device per sample, the two-stream pipeline
+        with in-stream all-reduces)."""
         import torch.distributed as dist
         K, B = int(uniforms.shape[0]), int(uniforms.shape[1])
         u = uniforms.to(device=DEVICE, dtype=torch.float64).contiguous()
         ws = self.workspace(B)
         cfg = self._cfg_for(B)
+        if self._dp_native and buffer.dp_group is self.dp_group:
+            # (y / V: the caller's scratch of the host loop; the library keeps its own)
+            b = buffer
+            L.lib().call("cacto_update_n_per_dp", self.sys.handle, C.byref(self.nets), C.byref(cfg),
+                         dptr(b.storage, torch.float64), dptr(b.sum_tree), dptr(b.min_tree), b.cap, b.max_idx(),
+                         b.beta, dptr(u), dptr(b.exp_counter), b.fresh, b.eps, b.alpha, dptr(b.max_priority), K, B,
+                         dptr(ws), ws.numel() * 4, stream())
+            return
         Pc, Pa = self.critic_model.P, self.actor_model.P
         g = self._dp_grad_buf(Pc + Pa)
         y = torch.empty(B, dtype=torch.float32, device=DEVICE) if y is None else y

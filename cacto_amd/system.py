@@ -141,7 +141,16 @@ class System:
         return int(L.lib().raw("cacto_mlp_param_count")(self.handle, net))
 
     def set_critic_type(self, critic_type):
-        """RL.py:65-76 critic_type of this system's critics: 'sine' or 'sine-elu'."""
+        """RL.py:65-76 critic_type of this system's critics: 'sine' or 'sine-elu'. The activations are
+        a property of the handle, read by every critic kernel: once a critic net exists on it (the
+        learner's critic and target), a different type is refused instead of silently changing
+        those nets' activations."""
+        cur = getattr(self, "critic_type", "sine")
+        live = len(getattr(self, "critic_nets", None) or ())
+        if critic_type != cur and live > 0:
+            raise ValueError("critic_type %r requested on a system whose %d critic net(s) are %r: the activations "
+                             "belong to the system handle (make the other critic type from its own conf / system)"
+                             % (critic_type, live, cur))
         L.lib().call("cacto_sys_set_critic_type", self.handle, {"sine": 0, "sine-elu": 1}[critic_type])
         self.critic_type = critic_type
 

@@ -305,6 +305,34 @@ int cacto_update_pair_grads_stage(const cacto_sys* sys, const cacto_nets* nets, 
 int cacto_update_pair_apply(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
                             const float* grad_d, int critic, int actor, int soft_update, void* stream);
 
+/* Data-parallel learn_and_update over RCCL (main.py:219-225's parallelism as one process per GPU,
+ * SURVEY §8e). cacto_dp_unique_ids writes n RCCL unique ids (128 bytes each) on one rank; every
+ * rank then calls cacto_dp_attach with the same 2 ids (collective: it returns once all `world`
+ * ranks have joined), which gives the handle one communicator per stream of the update pipeline.
+ * The RCCL library is the one already loaded in the process (torch.distributed's), else
+ * librccl.so.1. cacto_dp_detach releases them (cacto_sys_destroy does too). */
+int cacto_dp_unique_ids(void* out_h, int n);
+int cacto_dp_attach(cacto_sys* sys, const void* ids_h, int rank, int world);
+int cacto_dp_detach(cacto_sys* sys);
+/* K data-parallel updates (RL.py:101-118 each) on this rank's minibatch indices idx_d [K][B] (B =
+ * the local batch; cfg->B_global = B * world, the gradients are scaled by 1 / B_global so the
+ * exchange is a plain sum): the two-stream pipeline of cacto_update_n with each network's gradient
+ * all-reduced on its own stream's communicator between its GEMM and its Adam step. Every rank
+ * applies the same Adam to the same sum, so the replicas stay identical; with one rank the result
+ * equals cacto_update_n bit for bit. */
+int cacto_update_n_dp(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                      const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
+                      size_t workspace_bytes, void* stream);
+/* The same with PER (RL.py:122-137 on every rank's replay shard): per update this shard's (sum,
+ * min, rows) all-gathered over the critic stream's communicator, the stratified sample with IS
+ * weights against the union (cacto_per_sample_global), the update, then this shard's priority
+ * update. Arguments as cacto_update_n_per. */
+int cacto_update_n_per_dp(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
+                          const double* storage_d, double* sum_tree_d, double* min_tree_d, int64_t capacity,
+                          int64_t max_idx, double beta, const double* uniforms_d, double* exp_counter_d,
+                          double fresh_factor, double eps, double alpha, double* max_priority_d, int K, int B,
+                          void* workspace_d, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- rollouts --------------- */
 
 /* B episodes from S0_d [B,ns] (float64), each for nsteps_d[b] <= T steps:

@@ -370,9 +370,23 @@ def test_dp_per_loop_pipelined_equals_sequential():
     assert not np.array_equal(res[0][0][1][2], res[1][0][1][2])
 
 
+def _host_loop_learner(group):
+    """A learner whose data-parallel updates run the host loop dp_pipeline (torch.distributed
+    collectives) instead of the library's RCCL pipeline."""
+    rl = _learner(1)
+    os.environ["CACTO_DP_NATIVE"] = "0"
+    try:
+        rl.set_data_parallel(1, group)
+    finally:
+        del os.environ["CACTO_DP_NATIVE"]
+    assert not rl._dp_native
+    return rl
+
+
 def _rccl_worker(rank, port, rows, idx, q):
     """One rank over RCCL (backend 'nccl'): the exchange path of RL_AC (an explicit process group
-    selects it at world size 1) run eagerly and captured into a HIP graph."""
+    selects it at world size 1) — the library's pipeline (cacto_update_n_dp) eager and captured into
+    a HIP graph, and the host loop dp_pipeline."""
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
@@ -383,13 +397,16 @@ def _rccl_worker(rank, port, rows, idx, q):
         single.update_rows_n(storage, ix)                     # the one-rank pipeline (no exchange)
         eager = _learner(1)
         eager.set_data_parallel(1, dist.group.WORLD)
-        eager.update_rows_n(storage, ix)                      # dp_pipeline, RCCL all-reduces
+        assert eager._dp_native
+        eager.update_rows_n(storage, ix)                      # cacto_update_n_dp, RCCL all-reduces
+        host = _host_loop_learner(dist.group.WORLD)
+        host.update_rows_n(storage, ix)                       # dp_pipeline, torch.distributed all-reduces
         graphed = _learner(1)
         graphed.set_data_parallel(1, dist.group.WORLD)
         g = graphed.capture_updates(storage, ix)
         g.replay()
         torch.cuda.synchronize()
-        first = (_state(single), _state(eager), _state(graphed), graphed.steps.cpu().tolist())
+        first = (_state(single), _state(eager), _state(graphed), _state(host), graphed.steps.cpu().tolist())
         eager.update_rows_n(storage, ix)                      # a second replay continues from the new state
         g.replay()
         torch.cuda.synchronize()
@@ -398,17 +415,20 @@ def _rccl_worker(rank, port, rows, idx, q):
         dist.destroy_process_group()
 
 
-def test_dp_loop_over_rccl_is_graph_capturable():
-    """The data-parallel K-step loop (dp_pipeline: staged gradients, the critic part's all-reduce
-    issued before the actor part is formed, Adam steps after each part lands) over RCCL, captured
-    into one HIP graph: replays equal the eager loop bit for bit, and at one rank (the exchange is
-    the identity) both equal the single-rank pipeline. The first RCCL communicator this package
-    runs; the multi-GPU driver runs the same code with world size N."""
+@pytest.mark.parametrize("B", [128, 1024])
+def test_dp_loop_over_rccl_is_graph_capturable(B):
+    """The data-parallel K-step loop over RCCL — the library's pipeline (cacto_update_n_dp: the
+    two-stream pipeline, each network's gradient all-reduced on its stream's communicator between
+    its GEMM and its Adam step) and the host loop dp_pipeline (staged gradients, torch.distributed
+    all-reduces) — captured into one HIP graph: replays equal the eager loop bit for bit, and at
+    one rank (the exchange is the identity) both loops equal the single-rank pipeline. B = 128: the
+    4-sample-tile chains; 1024: the 16-sample ones. The multi-GPU driver runs the same code with
+    world size N."""
     import torch.multiprocessing as mp
     rng = np.random.default_rng(91)
     N = 4096
     rows = _rows(N, 92)
-    idx = rng.integers(0, N, size=(6, 128))
+    idx = rng.integers(0, N, size=(6, B))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(0, _free_port(), rows, idx, q))
@@ -420,17 +440,18 @@ def test_dp_loop_over_rccl_is_graph_capturable():
         if p.is_alive():
             p.kill()
     assert p.exitcode == 0
-    single, eager, graphed, steps = first
+    single, eager, graphed, host, steps = first
     assert steps == [6, 6] and steps2 == [12, 12]
-    for a, b, c in zip(single, eager, graphed):
-        assert np.array_equal(a, b) and np.array_equal(b, c)
+    for a, b, c, d in zip(single, eager, graphed, host):
+        assert np.array_equal(a, b) and np.array_equal(b, c) and np.array_equal(c, d)
     for a, b in zip(eager2, graphed2):
         assert np.array_equal(a, b)
 
 
 def _rccl_per_worker(rank, port, rows, U, q):
     """One rank over RCCL: the data-parallel PER loop (update_rows_n_per_dp: shard-stats
-    all-gather, stratified sample, staged gradients, priority updates) eager and captured."""
+    all-gather, stratified sample, gradients, priority updates) in the library (eager and
+    captured), the host loop, and the single-rank pipelined PER loop."""
     import torch.distributed as dist
     from cacto_amd.confs import load_conf
     from cacto_amd.replay_buffer import PrioritizedReplayBuffer
@@ -441,16 +462,20 @@ def _rccl_per_worker(rank, port, rows, U, q):
         conf.prioritized_replay_alpha = 0.6
         conf.BATCH_SIZE = U.shape[1]
         out = []
-        for graphed in (False, True):
-            rl = _learner(1)
-            rl.set_data_parallel(1, dist.group.WORLD)
+        for mode in ("eager", "graphed", "host", "single"):
+            rl = _host_loop_learner(dist.group.WORLD) if mode == "host" else _learner(1)
+            if mode in ("eager", "graphed"):
+                rl.set_data_parallel(1, dist.group.WORLD)
             buf = PrioritizedReplayBuffer(conf, rl.sys)
-            buf.set_data_parallel(1, dist.group.WORLD)
+            if mode != "single":
+                buf.set_data_parallel(1, dist.group.WORLD)
             buf.add_rows(rows)
             Ud = torch.as_tensor(U, device="cuda")
-            if graphed:
+            if mode == "graphed":
                 g = rl.capture_updates(None, None, per_buffer=buf, uniforms=Ud)
                 g.replay()
+            elif mode == "single":
+                rl.update_rows_n_per(buf, Ud)
             else:
                 rl.update_rows_n_per_dp(buf, Ud)
             torch.cuda.synchronize()
@@ -461,27 +486,31 @@ def _rccl_per_worker(rank, port, rows, U, q):
         dist.destroy_process_group()
 
 
-def test_dp_per_loop_over_rccl_is_graph_capturable():
+@pytest.mark.parametrize("B", [64, 1024])
+def test_dp_per_loop_over_rccl_is_graph_capturable(B):
     """capture_updates(per_buffer=...) of the data-parallel PER loop over RCCL (one rank): the
     replayed graph equals the eager update_rows_n_per_dp bit for bit — weights, moments, counters,
-    both trees, exp_counter, max_priority."""
+    both trees, exp_counter, max_priority — and so do the host loop and, at one rank, the
+    single-rank pipelined PER loop (cacto_update_n_per)."""
     import torch.multiprocessing as mp
-    rows = _rows(1500, 93)
-    U = np.random.default_rng(94).uniform(size=(5, 64))
+    rows = _rows(3000, 93)
+    U = np.random.default_rng(94).uniform(size=(5, B))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_per_worker, args=(0, _free_port(), rows, U, q))
     p.start()
     try:
-        eager, graphed = q.get(timeout=240)
+        runs = q.get(timeout=240)
     finally:
         p.join(timeout=60)
         if p.is_alive():
             p.kill()
     assert p.exitcode == 0
-    assert eager[1] == graphed[1] == [5, 5]
-    for a, b in zip(eager[0], graphed[0]):
-        assert np.array_equal(a, b)
-    for a, b in zip(eager[2:5], graphed[2:5]):
-        assert np.array_equal(a, b)
-    assert eager[5] == graphed[5]
+    eager = runs[0]
+    for other in runs[1:]:
+        assert eager[1] == other[1] == [5, 5]
+        for a, b in zip(eager[0], other[0]):
+            assert np.array_equal(a, b)
+        for a, b in zip(eager[2:5], other[2:5]):
+            assert np.array_equal(a, b)
+        assert eager[5] == other[5]

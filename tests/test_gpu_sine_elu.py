@@ -3,8 +3,10 @@ the sine critic) on the CACTO_CRITIC_ELU build of the library (cacto_amd/libcact
 default build compiles the sine critic only), in a child process that loads that
 library: forward, dV/ds, the Sobolev critic gradient and the actor gradient against the oracle
 (acts=SINE_ELU, pinned by finite differences in test_oracle_math.py) at B = 128 (4-sample tiles) and
-1024 (16-sample tiles), and the pipelined update loop against the sequential one, bit for bit. The
-default library refuses the critic type (CACTO_EINVAL)."""
+1024 (16-sample tiles) for the double integrator and the manipulator (revolute-chain actor path), the
+pipelined update loop against the sequential one, bit for bit, the .h5 checkpoints' Keras layer names
+(the reference's sine-elu models) and that a 'sine' critic is refused on a handle whose sine-elu
+critics exist. The default library refuses the critic type (CACTO_EINVAL)."""
 import json
 import os
 import subprocess
@@ -94,6 +96,46 @@ def _child():
         torch.cuda.synchronize()
         runs.append([t.cpu().numpy() for t in (rl.actor_model.buf, rl.critic_model.buf, rl.target_critic.buf)])
     out["pipelined_equal"] = all(bool(np.array_equal(a, b)) for a, b in zip(*runs))
+    # the revolute-chain actor path (the manipulator: CRBA / RNEA dynamics Jacobian) at both tile sizes
+    for B in (128, 1024):
+        conf, genv, oe, nn, rl = _nets("manipulator", seed=1)
+        ns = conf.nb_state
+        norm = conf.state_norm_arr.astype(np.float64)
+        rng = np.random.default_rng(23)
+        rows = _rows(conf, B, rng)
+        r32 = rows.astype(np.float32).astype(np.float64)
+        cw = rl.critic_model.get_weights()
+        idx = torch.arange(B, dtype=torch.int32, device="cuda")
+        gc, y, Vr, Vt = rl.critic_grad_rows(torch.as_tensor(rows, device="cuda"), idx)
+        ref = onn.compute_critic_grad(cw, rl.target_critic.get_weights(), r32[:, :ns], r32[:, ns + 1:2 * ns + 1],
+                                      r32[:, ns:ns + 1], r32[:, 2 * ns + 1:3 * ns + 1], r32[:, 3 * ns + 1:3 * ns + 2],
+                                      np.ones((B, 1)), 1e-2, norm, acts=onn.SINE_ELU)
+        out["man_critic_grad_rel_%d" % B] = max(float(rel_l2(a.cpu().numpy(), b)) for a, b in zip(gc, ref[0]))
+        ga = rl.actor_grad_rows(torch.as_tensor(rows, device="cuda"), idx)
+        refa = onn.compute_actor_grad(oe, rl.actor_model.get_weights(), cw, rows[:, :ns].astype(np.float32),
+                                      rows[:, 3 * ns + 2:3 * ns + 3], norm, acts=onn.SINE_ELU)
+        out["man_actor_grad_rel_%d" % B] = max(float(rel_l2(a.cpu().numpy(), b)) for a, b in zip(ga, refa))
+    # checkpoints in the reference's layout: the sine-elu models' Keras layer names (NeuralNetwork.py:80-93,
+    # created after the actor, RL.py:52-76), read back bit for bit
+    import tempfile
+    from cacto_amd import h5
+    names = {}
+    with tempfile.TemporaryDirectory() as d:
+        for role, net in (("critic", rl.critic_model), ("target", rl.target_critic)):
+            path = os.path.join(d, role + ".h5")
+            net.save_weights(path)
+            with open(path, "rb") as f:
+                hf = h5.H5File(f.read())
+            names[role] = h5._strings(hf.attributes(hf.object(hf.root))["layer_names"])
+            out["h5_%s_equal" % role] = all(bool(np.array_equal(a, b)) for a, b in
+                                            zip(h5.read_keras_weights(path), net.get_weights()))
+    out["h5_names"] = names
+    # the activations belong to the handle: a 'sine' critic on it is refused while sine-elu nets live
+    try:
+        nn.create_critic_sine()
+        out["sine_refused"] = False
+    except ValueError:
+        out["sine_refused"] = True
     print("RESULT " + json.dumps(out), flush=True)
 
 
@@ -114,6 +156,14 @@ def test_sine_elu_critic_on_its_build():
         assert res["critic_grad_rel_%d" % B] < 2e-4, res
         assert res["actor_grad_rel_%d" % B] < 2e-4, res
     assert res["pipelined_equal"], res
+    for B in (128, 1024):
+        assert res["man_critic_grad_rel_%d" % B] < 2e-4 and res["man_actor_grad_rel_%d" % B] < 2e-4, res
+    assert res["h5_names"] == {
+        "critic": ["sinusodial_representation_dense", "dense_3", "sinusodial_representation_dense_1", "dense_4",
+                   "dense_5"],
+        "target": ["sinusodial_representation_dense_2", "dense_6", "sinusodial_representation_dense_3", "dense_7",
+                   "dense_8"]}, res
+    assert res["h5_critic_equal"] and res["h5_target_equal"] and res["sine_refused"], res
 
 
 @pytest.mark.gpu
