@@ -74,12 +74,13 @@ __device__ __forceinline__ void joint_sincos(double x, double* sp, double* cp) {
   *cp = ((q + 1) & 2) ? -cc : cc;
 }
 
-// Explicit Euler step of the planar 3R chain: qdd = M^-1 (a - h) by the adjugate (one division),
-// q' = q + v dt, v' = v + qdd dt, t' = t + dt, given (s1, c1, s2, c2) = sin / cos of q1, q2
-// (joint_sincos). Every rollout kernel that runs such a chain steps it with this function, so the
-// schedule never changes a result.
-__device__ __forceinline__ void planar3_step_sc(const Planar3& k, double dt, const double* s, const double* a,
-                                                double s1, double c1, double s2, double c2, double* out) {
+// M(q), h(q, v) of the planar 3R chain in closed form, returned as the adjugate of M (A, symmetric)
+// with r = 1 / det M, so M^-1 = r A and qdd = r A (a - h); sin / cos of q1, q2 given (joint_sincos).
+struct Planar3Terms {
+  double A00, A01, A02, A11, A12, A22, r, h0, h1, h2;
+};
+__device__ __forceinline__ Planar3Terms planar3_terms(const Planar3& k, const double* s, double s1, double c1,
+                                                      double s2, double c2) {
   const double c12 = fma(c1, c2, -(s1 * s2)), s12 = fma(s1, c2, c1 * s2);
   // link-fixed vectors in link 0's frame: joint 1 -> joint 2 (P1), joint i -> COM i (Ci)
   const double P1x = fma(k.p2x, c1, -(k.p2y * s1)), P1y = fma(k.p2x, s1, k.p2y * c1);
@@ -103,25 +104,42 @@ __device__ __forceinline__ void planar3_step_sc(const Planar3& k, double dt, con
   const double b0x = q0 * k.P0x, b0y = q0 * k.P0y;
   const double n1x = fma(q1, C1x, b0x), n1y = fma(q1, C1y, b0y);
   const double n2x = fma(q2, C2x, fma(q1, P1x, b0x)), n2y = fma(q2, C2y, fma(q1, P1y, b0y));
-  const double h2 = -(k.m2 * crs2(C2x, C2y, n2x, n2y));
-  const double h1 = -fma(k.m1, crs2(C1x, C1y, n1x, n1y), k.m2 * crs2(r12x, r12y, n2x, n2y));
-  const double h0 = -fma(k.m0, crs2(k.c0x, k.c0y, n0x, n0y),
-                         fma(k.m1, crs2(r01x, r01y, n1x, n1y), k.m2 * crs2(r02x, r02y, n2x, n2y)));
-  // qdd = adj(M) (a - h) / det M
-  const double e0 = a[0] - h0, e1 = a[1] - h1, e2 = a[2] - h2;
-  const double A00 = fma(M11, M22, -(M12 * M12)), A01 = fma(M02, M12, -(M01 * M22)),
-               A02 = fma(M01, M12, -(M02 * M11)), A11 = fma(M00, M22, -(M02 * M02)),
-               A12 = fma(M01, M02, -(M00 * M12)), A22 = fma(M00, M11, -(M01 * M01));
-  const double r = 1.0 / fma(M00, A00, fma(M01, A01, M02 * A02));
-  const double d0 = fma(A00, e0, fma(A01, e1, A02 * e2)) * r;
-  const double d1 = fma(A01, e0, fma(A11, e1, A12 * e2)) * r;
-  const double d2 = fma(A02, e0, fma(A12, e1, A22 * e2)) * r;
-  out[0] = fma(s[3], dt, s[0]);
-  out[1] = fma(s[4], dt, s[1]);
-  out[2] = fma(s[5], dt, s[2]);
-  out[3] = fma(d0, dt, s[3]);
-  out[4] = fma(d1, dt, s[4]);
-  out[5] = fma(d2, dt, s[5]);
+  Planar3Terms T;
+  T.h2 = -(k.m2 * crs2(C2x, C2y, n2x, n2y));
+  T.h1 = -fma(k.m1, crs2(C1x, C1y, n1x, n1y), k.m2 * crs2(r12x, r12y, n2x, n2y));
+  T.h0 = -fma(k.m0, crs2(k.c0x, k.c0y, n0x, n0y), fma(k.m1, crs2(r01x, r01y, n1x, n1y), k.m2 * crs2(r02x, r02y, n2x, n2y)));
+  T.A00 = fma(M11, M22, -(M12 * M12));
+  T.A01 = fma(M02, M12, -(M01 * M22));
+  T.A02 = fma(M01, M12, -(M02 * M11));
+  T.A11 = fma(M00, M22, -(M02 * M02));
+  T.A12 = fma(M01, M02, -(M00 * M12));
+  T.A22 = fma(M00, M11, -(M01 * M01));
+  T.r = 1.0 / fma(M00, T.A00, fma(M01, T.A01, M02 * T.A02));
+  return T;
+}
+// qdd = M^-1 (a - h)
+__device__ __forceinline__ void planar3_qdd(const Planar3Terms& T, const double* a, double* dv) {
+  const double e0 = a[0] - T.h0, e1 = a[1] - T.h1, e2 = a[2] - T.h2;
+  dv[0] = fma(T.A00, e0, fma(T.A01, e1, T.A02 * e2)) * T.r;
+  dv[1] = fma(T.A01, e0, fma(T.A11, e1, T.A12 * e2)) * T.r;
+  dv[2] = fma(T.A02, e0, fma(T.A12, e1, T.A22 * e2)) * T.r;
+}
+
+// Explicit Euler step of the planar 3R chain (float64 state and action): qdd = M^-1 (a - h), then
+// env_simulate's update q' = q + v dt, v' = v + qdd dt, t' = t + dt — the same operations as the
+// chain's generic step (chain_step), so every kernel that steps the manipulator (the rollouts,
+// cacto_env_step) gives the same bits. (s1, c1, s2, c2) = joint_sincos of q1, q2.
+__device__ __forceinline__ void planar3_step_sc(const Planar3& k, double dt, const double* s, const double* a,
+                                                double s1, double c1, double s2, double c2, double* out) {
+  const Planar3Terms T = planar3_terms(k, s, s1, c1, s2, c2);
+  double dv[3];
+  planar3_qdd(T, a, dv);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double v = s[3 + i];
+    out[i] = s[i] + v * dt;
+    out[3 + i] = v + dv[i] * dt;
+  }
   out[6] = s[6] + dt;
 }
 __device__ __forceinline__ void planar3_step(const Planar3& k, double dt, const double* s, const double* a,
@@ -598,12 +616,26 @@ __device__ inline bool env_simulate(const SysDevice& sd, const double* s, const 
     out[5] = s[5] + dt;
     return true;
   } else {
-    double M[NJ * NJ], h[NJ], dv[NJ];
-    chain_terms<NJ>(sd, s, s + NJ, M, h);
+    double dv[NJ];
+    bool ok = true;
+    bool planar = false;
+    if constexpr (NJ == 3) {
+      if (sd.pl[0] != 0.0) {  // the planar 3R chain: closed form (planar3_terms)
+        double s1, c1, s2, c2;
+        joint_sincos(s[1], &s1, &c1);
+        joint_sincos(s[2], &s2, &c2);
+        planar3_qdd(planar3_terms(Planar3(sd.pl), s, s1, c1, s2, c2), a, dv);
+        planar = true;
+      }
+    }
+    if (!planar) {
+      double M[NJ * NJ], h[NJ];
+      chain_terms<NJ>(sd, s, s + NJ, M, h);
 #pragma unroll
-    for (int i = 0; i < NJ; ++i) dv[i] = a[i] - h[i];
-    const bool ok = cholesky<NJ>(M);
-    chol_solve<NJ>(M, dv);
+      for (int i = 0; i < NJ; ++i) dv[i] = a[i] - h[i];
+      ok = cholesky<NJ>(M);
+      chol_solve<NJ>(M, dv);
+    }
 #pragma unroll
     for (int i = 0; i < NJ; ++i) {
       const double v = s[NJ + i];
@@ -694,6 +726,43 @@ __device__ inline bool env_simulate_derivative_const(const SysDevice& sd, const 
 template <int NJ>
 __device__ inline void env_derivative(const SysDevice& sd, const double* s, double* Fu);
 
+// env_simulate_derivative of the planar 3R chain: the step as env_simulate's, Fu = dt M^-1 (rows
+// 3-5) from the same adjugate, row-normalised.
+__device__ inline bool env_simulate_derivative_planar3(const SysDevice& sd, const double* s, const double* a,
+                                                       bool f32in, double* out, double* Fu) {
+  const double dt = sd.p.dt;
+  double s1, c1, s2, c2, dv[3];
+  joint_sincos(s[1], &s1, &c1);
+  joint_sincos(s[2], &s2, &c2);
+  const Planar3Terms T = planar3_terms(Planar3(sd.pl), s, s1, c1, s2, c2);
+  planar3_qdd(T, a, dv);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double v = s[3 + i];
+    if (f32in) {
+      const float vdt = __fmul_rn((float)v, (float)dt);
+      out[i] = s[i] + (double)vdt;
+      out[3 + i] = (double)(float)(v + dv[i] * dt);
+    } else {
+      out[i] = s[i] + v * dt;
+      out[3 + i] = v + dv[i] * dt;
+    }
+  }
+  out[6] = s[6] + dt;
+  const double Mi[9] = {T.A00, T.A01, T.A02, T.A01, T.A11, T.A12, T.A02, T.A12, T.A22};
+#pragma unroll
+  for (int k = 0; k < 7 * 3; ++k) Fu[k] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double v = Mi[3 * i + c] * T.r * dt;
+      if (sd.p.normalize) v *= sd.inv_norm[3 + i];
+      Fu[(3 + i) * 3 + c] = v;
+    }
+  return true;
+}
+
 // env_simulate(s, a, f32in) and env_derivative(s) together. For a chain, M(q) is factored once and
 // serves both the step and the columns of M^-1 (env_derivative would rebuild it with v = 0; M does
 // not depend on v, so the factor is the same bits).
@@ -704,6 +773,8 @@ __device__ inline bool env_simulate_derivative(const SysDevice& sd, const double
     const cacto_sys_params& p = sd.p;
     constexpr int NS = 2 * NJ + 1, NA = NJ;
     const double dt = p.dt;
+    if constexpr (NJ == 3)
+      if (sd.pl[0] != 0.0) return env_simulate_derivative_planar3(sd, s, a, f32in, out, Fu);
     double M[NJ * NJ], h[NJ], dv[NJ];
     chain_terms<NJ>(sd, s, s + NJ, M, h);
 #pragma unroll

@@ -398,6 +398,28 @@ __device__ __forceinline__ void chain_dynamics_spread(const SysDevice& sd, const
   constexpr int NS = Dims<NJ>::NS, NA = Dims<NJ>::NA;
   const cacto_sys_params& p = sd.p;
   const int wave = tid >> 6, lane = tid & 63;
+  if constexpr (NJ == 3) {
+    if (sd.pl[0] != 0.0) {
+      // the planar 3R chain (the manipulator): the closed form is short, one thread per sample
+      // (env_simulate_derivative's planar path, as the 16-sample chain's)
+      if (tid < T) {
+        const int c = tid;
+        double s[NS], a[NA], sn[NS], F[NS * NA];
+#pragma unroll
+        for (int f = 0; f < NS; ++f) s[f] = (double)st[c * 16 + f];
+#pragma unroll
+        for (int i = 0; i < NA; ++i) a[i] = (double)A[c * NA + i];
+        (void)env_simulate_derivative_planar3(sd, s, a, true, sn, F);
+#pragma unroll
+        for (int f = 0; f < 16; ++f) stn[c * 16 + f] = f < NS ? (float)sn[f] : 0.f;
+#pragma unroll
+        for (int k = 0; k < NS * NA; ++k) Fu[c * CACTO_MAX_STATE * CACTO_MAX_ACTION + k] = (float)F[k];
+      }
+      __syncthreads();
+      __syncthreads();
+      return;
+    }
+  }
   if (wave < 2 && lane < T) {
     const int c = lane;
     double q[NJ], v[NJ];
