@@ -17,6 +17,7 @@ rollouts (cacto_ddp_backward, every system; the TO NLP solve itself is host-side
     python bench.py [--gpus N --steps K --warmup W]
 """
 import argparse
+import ctypes
 import json
 import os
 import random
@@ -919,6 +920,15 @@ def main():
         updates["B=%d" % B] = dict(value=K / wall, unit="critic-updates/s", global_batch=B * world,
                                    ms_per_update=1e3 * wall / K, tflops=flop * K / wall / 1e12,
                                    mfma_frac=flop * K / wall / (FP32_MFMA_PEAK * world), segments=seg)
+    # the two-stream update pipeline's ordering on this box (cacto_pipeline_status: the handle's
+    # one-time concurrency probe) and its timeout latch, collected (a latched wait fails the run)
+    from cacto_amd import _lib as L
+    rl.check_pipeline()
+    st = (ctypes.c_ulonglong * 4)()
+    L.lib().call("cacto_pipeline_status", rl.sys.handle, st)
+    pipe = {"ordering": {0: "not run", 1: "queue markers (probe: streams not concurrent)",
+                         2: "device-side waits (probe: streams concurrent)"}[int(st[3])],
+            "forced": os.environ.get("CACTO_PIPE_DEVWAIT")}
     extra = {}
     global DP1_GROUP
     if world == 1 and not args.no_dp1 and ("car_park" in args.extra_systems or "ur5" in args.extra_systems):
@@ -999,6 +1009,7 @@ def main():
                          "update": upd_roof,
                          "update_by_batch": {str(k): v for k, v in upd_roofs.items()}},
             "critic_updates": updates,
+            "update_pipeline": pipe,
             "episode_to_buffer": e2b,
             "ddp_labels": ddp,
             "rollout_diagnostics": diag,

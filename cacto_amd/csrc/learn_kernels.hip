@@ -87,6 +87,7 @@ __device__ __forceinline__ int chain_tile_of(int b, int ntiles, int xcd_tiles) {
 // that chain has finished) carries no data; for the read-after-write order (the actor chain reads
 // what the critic's Adam wrote) the Adam's stores went through to memory before it published (see
 // ChainScalars and DESIGN §3's memory-ordering contract).
+// ("Memory-ordering contract", sites 2 and 3)
 __device__ __forceinline__ void pipe_wait(const unsigned long long* wait_p, unsigned long long wait_v,
                                           unsigned long long* latch) {
   if (!wait_p) return;
@@ -104,6 +105,7 @@ __device__ __forceinline__ void pipe_wait(const unsigned long long* wait_p, unsi
 // (AMD_SERIALIZE_KERNEL, HIP_LAUNCH_BLOCKING, counter collection) the first of the two to run cannot
 // see the other's flag, so a device-side wait would spin until its bound: the pipeline then orders
 // the streams with queue markers.
+// ("Memory-ordering contract", site 4)
 __global__ void k_pipe_probe(unsigned long long* w, int role) {
   if (threadIdx.x != 0) return;
   unsigned long long* mine = w + 4 + role;
@@ -1201,6 +1203,7 @@ __device__ __forceinline__ AdamScalars adam_scalars(const AdamArgs& a, const int
 // done) for the actor chain's wait: every thread's stores have completed (waitcnt) before its
 // workgroup counts itself; no fence, no L2 write-back.
 // nblk: the Adam step's workgroups (the launch's, or the leading part of k_adam_sample's).
+// ("Memory-ordering contract", site 2: why no release / acquire is needed here)
 __device__ __forceinline__ void adam_publish_thru(unsigned long long* sig_p, unsigned long long sig_v, int nblk) {
   if (!sig_p) return;
   __shared__ int last;

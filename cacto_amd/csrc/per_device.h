@@ -398,7 +398,8 @@ __device__ __forceinline__ void per_update_run_body(int blk, int nroot, const Pe
     }
   }
   if (nroot == 1) return;
-  // last workgroup done: the root stores have completed (vmcnt 0) before the count
+  // last workgroup done: the root stores have completed (vmcnt 0) before the count (agent-scope
+  // publication without a fence: DESIGN.md §3, "Memory-ordering contract", site 1)
   unsigned long long* done = reinterpret_cast<unsigned long long*>(a.sum_tree);
   if (tid == 0) {
     __builtin_amdgcn_s_waitcnt(0);

@@ -529,7 +529,8 @@ __global__ void __launch_bounds__(256) k_per_update_sub(double* __restrict__ sum
     __syncthreads();
   }
   if (nroot == 1) return;
-  // last workgroup done: the root stores have completed (vmcnt 0) before the count
+  // last workgroup done: the root stores have completed (vmcnt 0) before the count (agent-scope
+  // publication without a fence: DESIGN.md §3, "Memory-ordering contract", site 1)
   unsigned long long* done = reinterpret_cast<unsigned long long*>(sum_tree);
   if (tid == 0) {
     __builtin_amdgcn_s_waitcnt(0);
