@@ -1344,12 +1344,47 @@ __global__ void __launch_bounds__(256) k_soft(NetTopo t, const float* __restrict
   }
 }
 
+// The data-parallel path's chunk sum (the gradient each rank all-reduces): out[p] = the nch
+// partials of parameter p summed in chunk order, as k_adam sums them. NCH > 0: one parameter per
+// thread with every partial loaded at once (clamped, branch-free), so a thread waits for one memory
+// latency instead of one per chunk (the looped form, NCH = 0, issued one load per add: 16-32
+// dependent round trips, 7-8 us per launch at B = 4096).
+template <int NCH>
 __global__ void __launch_bounds__(256) k_reduce(const float* __restrict__ slab, int nch, int P, float* __restrict__ out) {
+  if constexpr (NCH > 0) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    const int pc = min(p, P - 1);
+    float q[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) q[k] = slab[(size_t)min(k, nch - 1) * P + pc];
+    float g = q[0];
+#pragma unroll
+    for (int k = 1; k < NCH; ++k)
+      if (k < nch) g += q[k];
+    if (p < P) out[p] = g;
+    return;
+  }
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
     float g = slab[p];
     for (int ch = 1; ch < nch; ++ch) g += slab[(size_t)ch * P + p];
     out[p] = g;
   }
+}
+
+int launch_reduce(const float* slab, int nch, int P, float* out, hipStream_t st) {
+  const int full = (P + 255) / 256;
+  if (nch <= 8)
+    hipLaunchKernelGGL(k_reduce<8>, dim3(full), dim3(256), 0, st, slab, nch, P, out);
+  else if (nch <= 16)
+    hipLaunchKernelGGL(k_reduce<16>, dim3(full), dim3(256), 0, st, slab, nch, P, out);
+  else if (nch <= 32)
+    hipLaunchKernelGGL(k_reduce<32>, dim3(full), dim3(256), 0, st, slab, nch, P, out);
+  else if (nch <= 64)
+    hipLaunchKernelGGL(k_reduce<64>, dim3(full), dim3(256), 0, st, slab, nch, P, out);
+  else
+    hipLaunchKernelGGL(k_reduce<0>, dim3(std::min(full, 1024)), dim3(256), 0, st, slab, nch, P, out);
+  CACTO_CHECK_HIP(hipGetLastError());
+  return CACTO_OK;
 }
 
 // ---------------------------------------------------------------- fused weight gradient + Adam (small batches)
@@ -2217,8 +2252,7 @@ extern "C" int cacto_critic_grad(const cacto_sys* sys, const cacto_nets* nets, c
   if (int e = launch_critic_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, is_w_d, B, y_d, V_d, Vt_d, w, st, &nch))
     return e;
   const int P = sys->critic.params;
-  hipLaunchKernelGGL(k_reduce, dim3(std::min((P + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, P, grad_d);
-  CACTO_CHECK_HIP(hipGetLastError());
+  if (int e = launch_reduce(w.slab, nch, P, grad_d, st)) return e;
   return CACTO_OK;
 }
 
@@ -2233,8 +2267,7 @@ extern "C" int cacto_actor_grad(const cacto_sys* sys, const cacto_nets* nets, co
   int nch = 0;
   if (int e = launch_actor_chain_and_wgrad(sys, nets, cfg, storage_d, idx_d, B, w, st, &nch)) return e;
   const int P = sys->actor.params;
-  hipLaunchKernelGGL(k_reduce, dim3(std::min((P + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, nch, P, grad_d);
-  CACTO_CHECK_HIP(hipGetLastError());
+  if (int e = launch_reduce(w.slab_a, nch, P, grad_d, st)) return e;
   return CACTO_OK;
 }
 
@@ -2287,10 +2320,7 @@ int pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_
     if (!idx_a_d) return CACTO_OK;
     int nch = 0;
     if (int e = launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, st, &nch)) return e;
-    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, st, w.slab_a, nch, Pa,
-                       grad_d + Pc);
-    CACTO_CHECK_HIP(hipGetLastError());
-    return CACTO_OK;
+    return launch_reduce(w.slab_a, nch, Pa, grad_d + Pc, st);
   }
   float* yb = y_d ? y_d : w.scal;
   float* Vb = V_d ? V_d : w.scal + w.Bp;
@@ -2310,8 +2340,7 @@ int pair_grads(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_
     const bool sob = cfg->w_S != 0.0;
     int nch = 0;
     if (int e = launch_wgrad(sys->critic, w.crit, sob ? 0 : w.Bp, 2 * w.Bp, w.Bp, w.slab, st, &nch)) return e;
-    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pc + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, Pc, grad_d);
-    CACTO_CHECK_HIP(hipGetLastError());
+    if (int e = launch_reduce(w.slab, nch, Pc, grad_d, st)) return e;
   }
   if (stages & 2) return pair_grads(sys, nets, cfg, storage_d, idx_c_d, is_w_d, idx_a_d, B, grad_d, y_d, V_d,
                                     workspace_d, workspace_bytes, 2, st);
@@ -2908,8 +2937,7 @@ int update_pipeline_dp_body(const cacto_sys* sys, const cacto_nets* nets, const 
       else if (int e = gather_stats())
         return e;
     }
-    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pc + 255) / 256, 1024)), dim3(256), 0, st, w.slab, nch, Pc, ms->dp_gc);
-    CACTO_CHECK_HIP(hipGetLastError());
+    if (int e = launch_reduce(w.slab, nch, Pc, ms->dp_gc, st)) return e;
     CACTO_CHECK_RCCL(R.all_reduce(ms->dp_gc, ms->dp_gc, (size_t)Pc, ncclFloat32, ncclSum, cc, st),
                      "ncclAllReduce(critic gradient)");
     cacto_nets dst = *nets;
@@ -2925,9 +2953,7 @@ int update_pipeline_dp_body(const cacto_sys* sys, const cacto_nets* nets, const 
     if (int e = launch_actor_chain(sys, &nxt, cfg, storage_d, idx, B, w, side)) return e;
     int ncha = 0;
     if (int e = launch_wgrad(sys->actor, w.act, 0, w.Bp, 0, w.slab_a, side, &ncha)) return e;
-    hipLaunchKernelGGL(k_reduce, dim3(std::min((Pa + 255) / 256, 1024)), dim3(256), 0, side, w.slab_a, ncha, Pa,
-                       ms->dp_ga);
-    CACTO_CHECK_HIP(hipGetLastError());
+    if (int e = launch_reduce(w.slab_a, ncha, Pa, ms->dp_ga, side)) return e;
     CACTO_CHECK_RCCL(R.all_reduce(ms->dp_ga, ms->dp_ga, (size_t)Pa, ncclFloat32, ncclSum, ca, side),
                      "ncclAllReduce(actor gradient)");
     if (int e = launch_adam(sys, nets, cfg, CACTO_NET_ACTOR, ms->dp_ga, 1, 0, side)) return e;

@@ -49,6 +49,18 @@ def _warm(i):
     return i
 
 
+def _stop_resource_tracker():
+    """The spawn context starts multiprocessing's resource-tracker process; stop it once the pool is
+    gone so the caller (bench.py) leaves no child behind."""
+    import gc
+    from multiprocessing import resource_tracker
+    gc.collect()                                 # the pool's semaphores are unregistered first
+    try:
+        resource_tracker._resource_tracker._stop()
+    except Exception:
+        pass
+
+
 def training_iteration(conf_name, weights, seed=0, nb_cpus=2, ep=0, update_sample=None, w_S=0.0):
     """Returns a dict of timings: episodes (pool), buffer add, updates (measured count) and the
     projection of the iteration's UPDATE_LOOPS[ep] updates."""
@@ -64,6 +76,10 @@ def training_iteration(conf_name, weights, seed=0, nb_cpus=2, ep=0, update_sampl
         t0 = time.perf_counter()
         tmp = pool.map(_sample, [(conf_name, weights["actor"], s, ep) for s in ics])
         t1 = time.perf_counter()
+        pool.close()
+        pool.join()                              # reap the workers (the with block only terminates them)
+    del pool
+    _stop_resource_tracker()
     t_pool = t0 - t_s
     tmp = [x for x in tmp if x is not None]
     buf = obuf.ReplayBuffer(conf.REPLAY_SIZE, conf.nb_state)
