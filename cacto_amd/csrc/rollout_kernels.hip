@@ -396,6 +396,85 @@ __device__ __forceinline__ void ro_chain_nle(const SysDevice& sd, RoChain<NJ, SL
   }
 }
 
+// A double of the lane below (SHR: row_shr:1) or above (SHL: row_shl:1) in the 16-lane DPP row, two
+// 32-bit moves; a row's first / last lane gets zeros (its callers select over those lanes).
+constexpr int DPP_SHR1 = 0x111, DPP_SHL1 = 0x101;
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ SV dpp_sv(const SV& v) {
+  return SV{v3(dpp_d<CTRL>(v.l.x), dpp_d<CTRL>(v.l.y), dpp_d<CTRL>(v.l.z)),
+            v3(dpp_d<CTRL>(v.a.x), dpp_d<CTRL>(v.a.y), dpp_d<CTRL>(v.a.z))};
+}
+__device__ __forceinline__ SV sv_sel(bool p, const SV& a, const SV& b) {
+  return SV{v3(p ? a.l.x : b.l.x, p ? a.l.y : b.l.y, p ? a.l.z : b.l.z),
+            v3(p ? a.a.x : b.a.x, p ? a.a.y : b.a.y, p ? a.a.z : b.a.z)};
+}
+
+// ro_chain_nle spread over wave 0 by (slot, joint): lane 8 c + j runs joint j of slot c with its
+// placement X_j in registers (one LDS read per step instead of one per joint and pass). The
+// velocity / acceleration recursion advances one joint per round — each round every lane applies
+// its X_j to its parent's (v, a), handed up from the lane below by a DPP row shift, so after round j
+// lane j holds v_j, a_j — then the per-joint force terms run on all joints at once, and the force
+// recursion hands act_force(X_j, f_j) down one lane per round. Each value is formed by the same
+// operations in the same order as chain_nle, so h is bit-identical; only the serial chain of LDS
+// round trips is gone. Slots whose lanes hold no episode compute on stale placements; their h is
+// not read.
+template <int NJ, int SL>
+__device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, RoChain<NJ, SL>& C, const double* sS,
+                                                   double* hS, int lane) {
+  static_assert(NJ <= 8 && SL * 8 <= 64, "8 lanes per slot, one wave");
+  constexpr int ns = Dims<NJ>::NS;
+  const int cr = lane >> 3, jr = lane & 7;
+  const int c = min(cr, SL - 1), j = min(jr, NJ - 1);
+  const bool base = jr == 0, top = jr >= NJ - 1;
+  const JointView jv{sd.joints + j * CACTO_JOINT_COLS};
+  const SE3 X = se3_ld<SL>(C.X + j * 12 * SL + c);
+  const double qd = sS[c * ns + NJ + j];
+  const SV S = joint_S(jv);
+  const Inertia I = jv.inertia();
+  const SV Sq{qd * S.l, qd * S.a};
+  const SV zero{v3(0, 0, 0), v3(0, 0, 0)};
+  const SV gacc{v3(-sd.p.gravity[0], -sd.p.gravity[1], -sd.p.gravity[2]), v3(0, 0, 0)};
+  SV vp = zero, ap = gacc, vi, ai;
+#pragma unroll
+  for (int r = 0; r < NJ; ++r) {
+    vi = act_motion_inv(X, vp);
+    vi.l = vi.l + Sq.l;
+    vi.a = vi.a + Sq.a;
+    ai = act_motion_inv(X, ap);
+    const SV cm = cross_motion(vi, Sq);
+    ai.l = ai.l + cm.l;
+    ai.a = ai.a + cm.a;
+    if (r < NJ - 1) {
+      vp = sv_sel(base, zero, dpp_sv<DPP_SHR1>(vi));
+      ap = sv_sel(base, gacc, dpp_sv<DPP_SHR1>(ai));
+    }
+  }
+  const SV Iv = inertia_mul(I, vi);
+  const SV Ia = inertia_mul(I, ai);
+  const SV vf = cross_force(vi, Iv);
+  SV f;
+  f.l = Ia.l + vf.l;
+  f.a = Ia.a + vf.a;
+  SV fc = f;
+#pragma unroll
+  for (int r = 0; r < NJ - 1; ++r) {
+    const SV fp = dpp_sv<DPP_SHL1>(act_force(X, fc));
+    SV g;
+    g.l = f.l + fp.l;
+    g.a = f.a + fp.a;
+    fc = sv_sel(top, fc, g);
+  }
+  const double h = sdot(S, fc);
+  if (cr < SL && jr < NJ) hS[j * SL + c] = h;
+}
+
 // chain_mass (env.h) from the workspace placements, split by columns over waves 1-3: column i of
 // M needs the composite inertia Ic_i = I_i + X_{i+1}^* Ic_{i+1} (tip to base) and then i force
 // transports toward the base. Wave 3 takes columns {0, 1} (the whole composite chain), wave 2 the
@@ -746,8 +825,11 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
     const bool active = L.lane < SL && (L.wave == 0 ? sr.act : Sh.sact[c] != 0);
     if (split_dyn) {
       if constexpr (NJ > 0) {
-        if (L.wave == 0 && active) {
-          ro_chain_nle<NJ, SL>(sd, Sh.ch, c, Sh.sS + c * ns, Sh.sS + c * ns + NJ, Sh.hS + c);
+        if (L.wave == 0) {
+          if constexpr (SL * 8 <= 64)
+            ro_chain_nle_lanes<NJ, SL>(sd, Sh.ch, Sh.sS, Sh.hS, L.lane);
+          else if (active)
+            ro_chain_nle<NJ, SL>(sd, Sh.ch, c, Sh.sS + c * ns, Sh.sS + c * ns + NJ, Sh.hS + c);
           RSTAMP(9);
         } else if (active) {
           ro_chain_mass_cols<NJ, SL>(sd, Sh.ch, c, Sh.MS + c, RoMassCols<NJ>::lo(L.wave), RoMassCols<NJ>::hi(L.wave));
