@@ -60,9 +60,21 @@ __device__ __forceinline__ floatx4 mfma_bc(float x, float w, floatx4 c) {
 // dynamics of the manipulator / UR5 need many registers, so those systems keep fewer rows in
 // registers (and the UR5 streams some); the LDS share is what fits beside the step buffers.
 template <int NJ, int NG>
+#ifndef RO_STREAM_PF
+#define RO_STREAM_PF 2  // ro_layer2's L2-streamed weight rows loaded two 16-row blocks ahead (one at NG > 1)
+#endif
+#ifndef RO_CHAIN6_LDSK1
+#define RO_CHAIN6_LDSK1 128
+#endif
 struct RoSplit {
-  static constexpr int REGK = NJ <= 2 ? 192 : NJ == 3 ? (NG == 4 ? 160 : 128) : NG == 4 ? 48 : 64;
-  static constexpr int LDSK = NJ <= 2 ? 64 : NJ == 3 ? (NG == 4 ? 96 : 128) : NG == 4 ? 80 : 112;
+#ifndef RO_CHAIN6_REGK1
+#define RO_CHAIN6_REGK1 128  // the 6-joint chain at one slot group: W2 wholly resident (128 + 128 rows)
+#endif
+#ifndef RO_CHAIN6_PF
+#define RO_CHAIN6_PF 0
+#endif
+  static constexpr int REGK = NJ <= 2 ? 192 : NJ == 3 ? (NG == 4 ? 160 : 128) : NG == 4 ? 48 : NG == 1 ? RO_CHAIN6_REGK1 : 64;
+  static constexpr int LDSK = NJ <= 2 ? 64 : NJ == 3 ? (NG == 4 ? 96 : 128) : NG == 4 ? 80 : NG == 1 ? RO_CHAIN6_LDSK1 : 112;
   static_assert(REGK % 16 == 0 && LDSK % 16 == 0 && REGK + LDSK <= 256, "row split");
 };
 
@@ -159,6 +171,22 @@ __device__ __forceinline__ void ro_layer2(const RoActorRegs<NS, REGK>& R, WT& W,
     for (int qq = 0; qq < 4; ++qq) wl[qq] = W.w2[(((k0 - REGK) / 4 + qq) * 4 + L.wave) * 64 + L.lane];
   };
   auto in_lds = [](int k0) { return k0 >= REGK && k0 < REGK + LDSK; };
+  // rows streamed from L2 (the 6-joint chain): each 16-row block's loads issued one block ahead,
+  // the first at the layer's start, so their latency overlaps the register / LDS blocks' MFMAs
+  constexpr bool SPF = REGK + LDSK < 256 && RO_STREAM_PF > 0;
+  constexpr int SD = RO_STREAM_PF > 1 && NG == 1 ? 2 : 1;  // blocks in flight (two need 16 more registers)
+  constexpr int S0 = REGK + LDSK;               // the first streamed row
+  float wgn[SPF ? SD : 1][16];
+  auto g_w = [&](int k0, float* wg) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) wg[q] = W2g[(k0 + q) * 256 + 64 * L.wave + L.lane];
+  };
+  if constexpr (SPF) {
+#pragma unroll
+    for (int d = 0; d < SD; ++d)
+      if (S0 + 16 * d < 256) g_w(S0 + 16 * d, wgn[d]);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads here (the scheduler would sink them to their use)
+  }
   float4 xn[NG], wn[4];
   if constexpr (PF) {
 #pragma unroll
@@ -192,8 +220,17 @@ __device__ __forceinline__ void ro_layer2(const RoActorRegs<NS, REGK>& R, WT& W,
           lds_w(k0, wl);
         }
       } else if (k0 >= REGK + LDSK) {
+        if constexpr (SPF) {
+          const int d = ((k0 - S0) / 16) % SD;  // a constant once the loops unroll
 #pragma unroll
-        for (int q = 0; q < 16; ++q) wg[q] = W2g[(k0 + q) * 256 + 64 * L.wave + L.lane];
+          for (int q = 0; q < 16; ++q) wg[q] = wgn[d][q];
+          if (k0 + 16 * SD < 256) {
+            g_w(k0 + 16 * SD, wgn[d]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {
+          g_w(k0, wg);
+        }
       }
       if constexpr (PF)
         if (!in_lds(k0) && in_lds(k0 + 16)) lds_w(k0 + 16, wn);
@@ -406,6 +443,19 @@ __device__ __forceinline__ double dpp_d(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+// the same with the lanes whose source lies outside the row keeping `old` (bound_ctrl off)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d_old(double old, double v) {
+  const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ SV dpp_sv_old(const SV& old, const SV& v) {
+  return SV{v3(dpp_d_old<CTRL>(old.l.x, v.l.x), dpp_d_old<CTRL>(old.l.y, v.l.y), dpp_d_old<CTRL>(old.l.z, v.l.z)),
+            v3(dpp_d_old<CTRL>(old.a.x, v.a.x), dpp_d_old<CTRL>(old.a.y, v.a.y), dpp_d_old<CTRL>(old.a.z, v.a.z))};
+}
 template <int CTRL>
 __device__ __forceinline__ SV dpp_sv(const SV& v) {
   return SV{v3(dpp_d<CTRL>(v.l.x), dpp_d<CTRL>(v.l.y), dpp_d<CTRL>(v.l.z)),
@@ -426,14 +476,28 @@ __device__ __forceinline__ SV sv_sel(bool p, const SV& a, const SV& b) {
 // round trips is gone. Slots whose lanes hold no episode compute on stale placements; their h is
 // not read.
 template <int NJ, int SL>
-__device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, RoChain<NJ, SL>& C, const double* sS,
-                                                   double* hS, int lane) {
-  static_assert(NJ <= 8 && SL * 8 <= 64, "8 lanes per slot, one wave");
+__device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, const double* jt, RoChain<NJ, SL>& C,
+                                                   const double* sS, double* hS, int lane, bool stamp = false) {
+#ifdef CACTO_STAMPS
+#define NSTAMP(k)                                                                   \
+  do {                                                                              \
+    __builtin_amdgcn_s_waitcnt(0);                                                  \
+    if (stamp) g_rstamps[k] = __builtin_amdgcn_s_memtime();                         \
+  } while (0)
+#else
+#define NSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+  // lanes per slot: a whole 16-lane DPP row per slot when the slots fit (SL = 4), so the base
+  // joint's lane takes (0, a_g) as the shift's out-of-row value instead of a select per round
+  constexpr int LPS = SL * 16 <= 64 ? 16 : 8;
+  static_assert(NJ <= LPS && SL * LPS <= 64, "one wave");
   constexpr int ns = Dims<NJ>::NS;
-  const int cr = lane >> 3, jr = lane & 7;
+  const int cr = lane / LPS, jr = lane % LPS;
   const int c = min(cr, SL - 1), j = min(jr, NJ - 1);
   const bool base = jr == 0, top = jr >= NJ - 1;
-  const JointView jv{sd.joints + j * CACTO_JOINT_COLS};
+  const JointView jv{jt + j * CACTO_JOINT_COLS};  // the LDS copy of the joint table
   const SE3 X = se3_ld<SL>(C.X + j * 12 * SL + c);
   const double qd = sS[c * ns + NJ + j];
   const SV S = joint_S(jv);
@@ -442,6 +506,7 @@ __device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, RoChain<
   const SV zero{v3(0, 0, 0), v3(0, 0, 0)};
   const SV gacc{v3(-sd.p.gravity[0], -sd.p.gravity[1], -sd.p.gravity[2]), v3(0, 0, 0)};
   SV vp = zero, ap = gacc, vi, ai;
+  NSTAMP(17);
 #pragma unroll
   for (int r = 0; r < NJ; ++r) {
     vi = act_motion_inv(X, vp);
@@ -452,10 +517,16 @@ __device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, RoChain<
     ai.l = ai.l + cm.l;
     ai.a = ai.a + cm.a;
     if (r < NJ - 1) {
-      vp = sv_sel(base, zero, dpp_sv<DPP_SHR1>(vi));
-      ap = sv_sel(base, gacc, dpp_sv<DPP_SHR1>(ai));
+      if constexpr (LPS == 16) {
+        vp = dpp_sv_old<DPP_SHR1>(zero, vi);
+        ap = dpp_sv_old<DPP_SHR1>(gacc, ai);
+      } else {
+        vp = sv_sel(base, zero, dpp_sv<DPP_SHR1>(vi));
+        ap = sv_sel(base, gacc, dpp_sv<DPP_SHR1>(ai));
+      }
     }
   }
+  NSTAMP(18);
   const SV Iv = inertia_mul(I, vi);
   const SV Ia = inertia_mul(I, ai);
   const SV vf = cross_force(vi, Iv);
@@ -463,6 +534,7 @@ __device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, RoChain<
   f.l = Ia.l + vf.l;
   f.a = Ia.a + vf.a;
   SV fc = f;
+  NSTAMP(19);
 #pragma unroll
   for (int r = 0; r < NJ - 1; ++r) {
     const SV fp = dpp_sv<DPP_SHL1>(act_force(X, fc));
@@ -473,6 +545,85 @@ __device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, RoChain<
   }
   const double h = sdot(S, fc);
   if (cr < SL && jr < NJ) hS[j * SL + c] = h;
+#undef NSTAMP
+}
+
+template <int CTRL>
+__device__ __forceinline__ Inertia dpp_inertia(const Inertia& I) {
+  Inertia o;
+  o.m = dpp_d<CTRL>(I.m);
+  o.h = v3(dpp_d<CTRL>(I.h.x), dpp_d<CTRL>(I.h.y), dpp_d<CTRL>(I.h.z));
+  o.Io.xx = dpp_d<CTRL>(I.Io.xx);
+  o.Io.xy = dpp_d<CTRL>(I.Io.xy);
+  o.Io.xz = dpp_d<CTRL>(I.Io.xz);
+  o.Io.yy = dpp_d<CTRL>(I.Io.yy);
+  o.Io.yz = dpp_d<CTRL>(I.Io.yz);
+  o.Io.zz = dpp_d<CTRL>(I.Io.zz);
+  return o;
+}
+
+// dpp_inertia with -0.0 in every field of the lanes whose source lies outside the row
+template <int CTRL>
+__device__ __forceinline__ Inertia dpp_inertia_nz(const Inertia& I) {
+  constexpr double nz = -0.0;
+  Inertia o;
+  o.m = dpp_d_old<CTRL>(nz, I.m);
+  o.h = v3(dpp_d_old<CTRL>(nz, I.h.x), dpp_d_old<CTRL>(nz, I.h.y), dpp_d_old<CTRL>(nz, I.h.z));
+  o.Io.xx = dpp_d_old<CTRL>(nz, I.Io.xx);
+  o.Io.xy = dpp_d_old<CTRL>(nz, I.Io.xy);
+  o.Io.xz = dpp_d_old<CTRL>(nz, I.Io.xz);
+  o.Io.yy = dpp_d_old<CTRL>(nz, I.Io.yy);
+  o.Io.yz = dpp_d_old<CTRL>(nz, I.Io.yz);
+  o.Io.zz = dpp_d_old<CTRL>(nz, I.Io.zz);
+  return o;
+}
+
+// chain_mass spread over one wave by (slot, joint), lane 8 c + j as in ro_chain_nle_lanes: the
+// composite inertias Ic_{j-1} = I_{j-1} + X_j^* Ic_j advance one joint per round (each lane
+// transports its Ic, the lane below adds its own I), then every column of M at once in a systolic
+// sweep — in round t lane k holds column k + t's force in joint k's frame, transports it to its
+// parent (act_force with its X_k) and hands it down a lane, where sdot with that joint's S gives
+// M[k + t][k - 1]. The same operations in the same order as chain_mass, so M is bit-identical.
+template <int NJ, int SL>
+__device__ __forceinline__ void ro_chain_mass_lanes(const double* jt, RoChain<NJ, SL>& C, double* MS, int lane) {
+  // a 16-lane row per slot when the slots fit (SL = 4), joints at the row's top lanes: the tip
+  // joint's lane then takes -0.0 (x + -0.0 == x for every x) as the shift's out-of-row value
+  // instead of a select per round
+  constexpr int LPS = SL * 16 <= 64 ? 16 : 8, J0 = LPS == 16 ? 16 - NJ : 0;
+  static_assert(NJ <= LPS && SL * LPS <= 64, "one wave");
+  const int cr = lane / LPS, jr = lane % LPS - J0;
+  const int c = min(cr, SL - 1), j = min(max(jr, 0), NJ - 1);
+  const bool top = jr >= NJ - 1, live = cr < SL && jr >= 0 && jr < NJ;
+  const JointView jv{jt + j * CACTO_JOINT_COLS};  // the LDS copy of the joint table
+  const SE3 X = se3_ld<SL>(C.X + j * 12 * SL + c);
+  const SV S = joint_S(jv);
+  const Inertia I = jv.inertia();
+  Inertia Ic = I;
+#pragma unroll
+  for (int r = 0; r < NJ - 1; ++r) {
+    if constexpr (LPS == 16) {
+      const Inertia t = dpp_inertia_nz<DPP_SHL1>(act_inertia(X, Ic));
+      Inertia a = I;
+      add_inertia(a, t);
+      Ic = a;
+    } else {
+      const Inertia t = dpp_inertia<DPP_SHL1>(act_inertia(X, Ic));
+      Inertia a = I;
+      add_inertia(a, t);
+      if (!top) Ic = a;
+    }
+  }
+  SV F = inertia_mul(Ic, S);
+  if (live) MS[(j * NJ + j) * SL + c] = sdot(S, F);
+#pragma unroll
+  for (int t = 1; t < NJ; ++t) {
+    F = dpp_sv<DPP_SHL1>(act_force(X, F));  // column j + t, in this joint's frame
+    const double mij = sdot(S, F);
+    if (live && j + t < NJ) {
+      MS[((j + t) * NJ + j) * SL + c] = mij;
+      MS[(j * NJ + (j + t)) * SL + c] = mij;
+    }
+  }
 }
 
 // chain_mass (env.h) from the workspace placements, split by columns over waves 1-3: column i of
@@ -533,6 +684,7 @@ struct RoShared {
   double sS[SL * ns];                                                 // s_t of every slot
   double MS[NJ > 0 ? SL * NJ * NJ : 1], hS[NJ > 0 ? SL * NJ : 1];    // chain M(q) (or its Cholesky factor), nle: [k][slot]
   RoChain<NJ, SL> ch;
+  double jt[NJ > 0 ? NJ * CACTO_JOINT_COLS : 1];  // the joint table (the per-lane recursions' constants)
   int sb[SL], sn[SL], st[SL], sact[SL];
   int anyact;
 };
@@ -791,6 +943,8 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
   // slot states too: a slot that is never filled still feeds its (unused) actor input row, which
   // then reads zeros rather than stale LDS
   for (int e = L.tid; e < SL * ns; e += CACTO_THREADS) Sh.sS[e] = 0.0;
+  if constexpr (NJ > 0)
+    for (int e = L.tid; e < NJ * CACTO_JOINT_COLS; e += CACTO_THREADS) Sh.jt[e] = sd.joints[e];
   if (L.tid < SL) Sh.sact[L.tid] = 0;
   __syncthreads();
   int head = 0;  // queue position (wave 0, uniform)
@@ -820,17 +974,28 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (!use_actor) __syncthreads();
       }
     }
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2), (NJ <= 3)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
+    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2 || (NJ > 3 && NG == 1 && RO_CHAIN6_PF)), (NJ <= 3)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
     RSTAMP(1);
     const bool active = L.lane < SL && (L.wave == 0 ? sr.act : Sh.sact[c] != 0);
     if (split_dyn) {
       if constexpr (NJ > 0) {
         if (L.wave == 0) {
           if constexpr (SL * 8 <= 64)
-            ro_chain_nle_lanes<NJ, SL>(sd, Sh.ch, Sh.sS, Sh.hS, L.lane);
+            ro_chain_nle_lanes<NJ, SL>(sd, Sh.jt, Sh.ch, Sh.sS, Sh.hS, L.lane
+#ifdef CACTO_STAMPS
+                                       , blockIdx.x == 0 && L.lane == 0 && it == 20
+#endif
+            );
           else if (active)
             ro_chain_nle<NJ, SL>(sd, Sh.ch, c, Sh.sS + c * ns, Sh.sS + c * ns + NJ, Sh.hS + c);
           RSTAMP(9);
+        } else if constexpr (SL * 8 <= 64) {
+          if (L.wave == 1) {
+            ro_chain_mass_lanes<NJ, SL>(Sh.jt, Sh.ch, Sh.MS, L.lane);
+#ifdef CACTO_STAMPS
+            if (blockIdx.x == 0 && L.lane == 0 && it == 20) g_rstamps[10] = __builtin_amdgcn_s_memtime();
+#endif
+          }
         } else if (active) {
           ro_chain_mass_cols<NJ, SL>(sd, Sh.ch, c, Sh.MS + c, RoMassCols<NJ>::lo(L.wave), RoMassCols<NJ>::hi(L.wave));
 #ifdef CACTO_STAMPS

@@ -41,6 +41,10 @@ def main():
         print("   chain dynamics after the actor: RNEA (wave 0) %.0f, CRBA columns (waves 1-3) %s"
               % (float(st[9]) - t[1], ", ".join("%.0f" % (float(st[9 + w]) - t[1]) if st[9 + w] > st[1] else "-"
                                                    for w in (1, 2, 3))))
+    if st[17] > st[1] and st[18] > st[17]:
+        print("   RNEA by lanes: loads %.0f, v / a rounds %.0f, force terms %.0f, force rounds %.0f"
+              % (float(st[17]) - t[1], float(st[18]) - float(st[17]), float(st[19]) - float(st[18]),
+                 float(st[9]) - float(st[19])))
     if st[13] > st[2] or st[14] > st[2]:
         print("   reward waves after the actor / dynamics phase: r_t (wave 1) %s, EE(s_t) (wave 2) %s, EE(s_n) (wave 3) %s"
               % tuple("%.0f" % (float(st[k]) - t[2]) if st[k] > st[2] else "-" for k in (13, 14, 15)))
