@@ -60,6 +60,12 @@ __device__ __forceinline__ floatx4 mfma_bc(float x, float w, floatx4 c) {
 // dynamics of the manipulator / UR5 need many registers, so those systems keep fewer rows in
 // registers (and the UR5 streams some); the LDS share is what fits beside the step buffers.
 template <int NJ, int NG>
+#ifndef RO_DYN_IN_ACTOR
+// 1: the lane RNEA / CRBA inside the actor's layer-2 block (the scheduler keeps them after the MFMA
+// stream, and the layer-2 barrier then waits for them): 124.5 M against 132.1 M env-steps/s (UR5,
+// 2048 episodes) for the dynamics after the actor, so off
+#define RO_DYN_IN_ACTOR 0
+#endif
 #ifndef RO_STREAM_PF
 #define RO_STREAM_PF 2  // ro_layer2's L2-streamed weight rows loaded two 16-row blocks ahead (one at NG > 1)
 #endif
@@ -265,9 +271,15 @@ __device__ __forceinline__ void ro_layer2(const RoActorRegs<NS, REGK>& R, WT& W,
 
 // Actor forward of the workgroup's SL slots: x0 -> h1 -> h2 -> a. Contains 3 barriers (the last
 // one publishes W.a).
-template <int NG, int NS, int NA, int REGK, int LDSK, bool PF, bool SPLIT, typename WT, typename Bar>
+struct RoNoDyn {
+  __device__ __forceinline__ void operator()() const {}
+};
+// dyn: work of this wave that needs nothing layer 2 produces, placed after layer 2's code in the
+// same basic block so the scheduler can interleave it with the layer's MFMAs and LDS waits
+template <int NG, int NS, int NA, int REGK, int LDSK, bool PF, bool SPLIT, typename WT, typename Bar,
+          typename Dyn = RoNoDyn>
 __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, WT& W, const float* __restrict__ W2g,
-                                         const Lane& L, int it, Bar&& bar) {
+                                         const Lane& L, int it, Bar&& bar, Dyn dyn = Dyn{}) {
   using C = RoCfg<NG>;
   // ---- layer 1 (K = NS): one activation VGPR per group covers every k
   {
@@ -294,6 +306,7 @@ __device__ __forceinline__ void ro_actor(const RoActorRegs<NS, REGK>& R, WT& W, 
   RSTAMP(4);
   // ---- layer 2 (K = 256)
   ro_layer2<NG, NS, REGK, LDSK, PF, SPLIT>(R, W, W2g, L);
+  dyn();
   bar();
   RSTAMP(5);
   // ---- layer 3 (256 -> NA): one summation order for every NG (so the schedule never changes a
@@ -477,7 +490,8 @@ __device__ __forceinline__ SV sv_sel(bool p, const SV& a, const SV& b) {
 // not read.
 template <int NJ, int SL>
 __device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, const double* jt, RoChain<NJ, SL>& C,
-                                                   const double* sS, double* hS, int lane, bool stamp = false) {
+                                                   const double* sS, double* hS, double* dump, int lane,
+                                                   bool stamp = false) {
 #ifdef CACTO_STAMPS
 #define NSTAMP(k)                                                                   \
   do {                                                                              \
@@ -544,7 +558,9 @@ __device__ __forceinline__ void ro_chain_nle_lanes(const SysDevice& sd, const do
     fc = sv_sel(top, fc, g);
   }
   const double h = sdot(S, fc);
-  if (cr < SL && jr < NJ) hS[j * SL + c] = h;
+  // every lane stores (no exec-mask branch in the block): lanes without a value write their dump slot
+  const bool own = cr < SL && jr < NJ;
+  *(own ? hS + j * SL + c : dump + lane) = h;
 #undef NSTAMP
 }
 
@@ -585,7 +601,8 @@ __device__ __forceinline__ Inertia dpp_inertia_nz(const Inertia& I) {
 // parent (act_force with its X_k) and hands it down a lane, where sdot with that joint's S gives
 // M[k + t][k - 1]. The same operations in the same order as chain_mass, so M is bit-identical.
 template <int NJ, int SL>
-__device__ __forceinline__ void ro_chain_mass_lanes(const double* jt, RoChain<NJ, SL>& C, double* MS, int lane) {
+__device__ __forceinline__ void ro_chain_mass_lanes(const double* jt, RoChain<NJ, SL>& C, double* MS, double* dump,
+                                                    int lane) {
   // a 16-lane row per slot when the slots fit (SL = 4), joints at the row's top lanes: the tip
   // joint's lane then takes -0.0 (x + -0.0 == x for every x) as the shift's out-of-row value
   // instead of a select per round
@@ -614,15 +631,15 @@ __device__ __forceinline__ void ro_chain_mass_lanes(const double* jt, RoChain<NJ
     }
   }
   SV F = inertia_mul(Ic, S);
-  if (live) MS[(j * NJ + j) * SL + c] = sdot(S, F);
+  // every lane stores (no exec-mask branch in the block): lanes without a value write their dump slot
+  *(live ? MS + (j * NJ + j) * SL + c : dump + lane) = sdot(S, F);
 #pragma unroll
   for (int t = 1; t < NJ; ++t) {
     F = dpp_sv<DPP_SHL1>(act_force(X, F));  // column j + t, in this joint's frame
     const double mij = sdot(S, F);
-    if (live && j + t < NJ) {
-      MS[((j + t) * NJ + j) * SL + c] = mij;
-      MS[(j * NJ + (j + t)) * SL + c] = mij;
-    }
+    const bool w = live && j + t < NJ;
+    *(w ? MS + ((j + t) * NJ + j) * SL + c : dump + lane) = mij;
+    *(w ? MS + (j * NJ + (j + t)) * SL + c : dump + 64 + lane) = mij;
   }
 }
 
@@ -685,6 +702,7 @@ struct RoShared {
   double MS[NJ > 0 ? SL * NJ * NJ : 1], hS[NJ > 0 ? SL * NJ : 1];    // chain M(q) (or its Cholesky factor), nle: [k][slot]
   RoChain<NJ, SL> ch;
   double jt[NJ > 0 ? NJ * CACTO_JOINT_COLS : 1];  // the joint table (the per-lane recursions' constants)
+  double dump[NJ > 0 && NG <= 2 ? 128 : 1];        // the lane recursions' stores of lanes without a value
   int sb[SL], sn[SL], st[SL], sact[SL];
   int anyact;
 };
@@ -974,14 +992,40 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
         if (!use_actor) __syncthreads();
       }
     }
-    if (use_actor) ro_actor<NG, ns, na, REGK, LDSK, (NJ <= 2 || (NJ > 3 && NG == 1 && RO_CHAIN6_PF)), (NJ <= 3)>(R, Sh.W, W2g, L, it, [] { __syncthreads(); });
+    // revolute chains on (slot, joint) lanes: M(q) and h(q, v) depend on s_t only, so wave 0's RNEA
+    // and wave 1's CRBA run inside the actor, interleaved with their layer-2 MFMAs
+    constexpr bool LANE_DYN = NJ > 0 && SL * 8 <= 64;
+    constexpr bool APF = NJ <= 2 || (NJ > 3 && NG == 1 && RO_CHAIN6_PF);
+    // (one slot group: at two the 8-lane layout's registers beside layer 2 would spill)
+    const bool dyn_in_actor = LANE_DYN && SL * 16 <= 64 && split_dyn && use_actor && RO_DYN_IN_ACTOR;
+    auto abar = [] { __syncthreads(); };
+    if (use_actor) {
+      if constexpr (LANE_DYN && SL * 16 <= 64) {
+        if (dyn_in_actor) {
+          if (L.wave == 0)
+            ro_actor<NG, ns, na, REGK, LDSK, APF, (NJ <= 3)>(R, Sh.W, W2g, L, it, abar, [&] {
+              ro_chain_nle_lanes<NJ, SL>(sd, Sh.jt, Sh.ch, Sh.sS, Sh.hS, Sh.dump, L.lane);
+            });
+          else if (L.wave == 1)
+            ro_actor<NG, ns, na, REGK, LDSK, APF, (NJ <= 3)>(R, Sh.W, W2g, L, it, abar, [&] {
+              ro_chain_mass_lanes<NJ, SL>(Sh.jt, Sh.ch, Sh.MS, Sh.dump, L.lane);
+            });
+          else
+            ro_actor<NG, ns, na, REGK, LDSK, APF, (NJ <= 3)>(R, Sh.W, W2g, L, it, abar);
+        } else {
+          ro_actor<NG, ns, na, REGK, LDSK, APF, (NJ <= 3)>(R, Sh.W, W2g, L, it, abar);
+        }
+      } else {
+        ro_actor<NG, ns, na, REGK, LDSK, APF, (NJ <= 3)>(R, Sh.W, W2g, L, it, abar);
+      }
+    }
     RSTAMP(1);
     const bool active = L.lane < SL && (L.wave == 0 ? sr.act : Sh.sact[c] != 0);
-    if (split_dyn) {
+    if (split_dyn && !dyn_in_actor) {
       if constexpr (NJ > 0) {
         if (L.wave == 0) {
           if constexpr (SL * 8 <= 64)
-            ro_chain_nle_lanes<NJ, SL>(sd, Sh.jt, Sh.ch, Sh.sS, Sh.hS, L.lane
+            ro_chain_nle_lanes<NJ, SL>(sd, Sh.jt, Sh.ch, Sh.sS, Sh.hS, Sh.dump, L.lane
 #ifdef CACTO_STAMPS
                                        , blockIdx.x == 0 && L.lane == 0 && it == 20
 #endif
@@ -991,7 +1035,7 @@ __global__ void __launch_bounds__(CACTO_THREADS, 1)
           RSTAMP(9);
         } else if constexpr (SL * 8 <= 64) {
           if (L.wave == 1) {
-            ro_chain_mass_lanes<NJ, SL>(Sh.jt, Sh.ch, Sh.MS, L.lane);
+            ro_chain_mass_lanes<NJ, SL>(Sh.jt, Sh.ch, Sh.MS, Sh.dump, L.lane);
 #ifdef CACTO_STAMPS
             if (blockIdx.x == 0 && L.lane == 0 && it == 20) g_rstamps[10] = __builtin_amdgcn_s_memtime();
 #endif
