@@ -2922,7 +2922,7 @@ int update_pipeline_dp_body(const cacto_sys* sys, const cacto_nets* nets, const 
       // workgroup of the GEMM's launch that rebuilds the top of the trees (with one subtree, a launch)
       pra = PerRunArgs{per->sum_tree, per->min_tree, per->cap, idx, y, V, per->exp_counter, per->max_idx,
                        per->fresh, per->eps, per->alpha, per->max_priority, w.runs,
-                       t + 1 < K && nroot > 1 ? stats : nullptr};
+                       t + 1 < K && nroot > 1 ? shards : nullptr, 3 * ms->dp_rank, 3 * ms->dp_world};
       if (t + 1 < K)
         psa = PerSampleArgs{per->sum_tree, per->min_tree, per->cap, per->max_idx, per->beta,
                             per->uniforms + (size_t)(t + 1) * B, B, w.pidx + (size_t)((t + 1) % nring) * w.Bp,
@@ -2932,8 +2932,9 @@ int update_pipeline_dp_body(const cacto_sys* sys, const cacto_nets* nets, const 
                              ovl ? &pra : nullptr))
       return e;
     if (ovl && t + 1 < K) {
-      if (nroot > 1)
-        CACTO_CHECK_RCCL(R.all_gather(stats, shards, 3, ncclFloat64, cc, st), "ncclAllGather(PER shards)");
+      if (nroot > 1)  // the table with this rank's words filled and the others zero: summed = gathered
+        CACTO_CHECK_RCCL(R.all_reduce(shards, shards, (size_t)3 * ms->dp_world, ncclFloat64, ncclSum, cc, st),
+                         "ncclAllReduce(PER shards)");
       else if (int e = gather_stats())
         return e;
     }

@@ -306,9 +306,12 @@ struct PerRunArgs {
   double fresh, eps, alpha;
   double* max_priority;
   int32_t* runs;  // the sampler's per-subtree runs, reset here for the next sample
-  // data parallel (cacto_update_n_per_dp): this shard's (sum, min, rows) after the update, written by
-  // the workgroup that rebuilds the top (k_per_shard_stats' values), for the all-gather; or nullptr
+  // data parallel (cacto_update_n_per_dp): the ranks' (sum, min, rows) table [world][3], or nullptr.
+  // The workgroup that rebuilds the top writes this shard's values (k_per_shard_stats') at
+  // stats_off and zeros in the other ranks' words, so a sum all-reduce of the table is the
+  // all-gather (x + 0.0 == x for the non-negative statistics)
   double* stats;
+  int stats_off = 0, stats_words = 3;
 };
 
 struct PerRunLds {
@@ -426,9 +429,10 @@ __device__ __forceinline__ void per_update_run_body(int blk, int nroot, const Pe
   if (tid == 0) {
     __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // +0.0, node 0
     if (a.stats) {
-      a.stats[0] = L.ts[1];
-      a.stats[1] = L.tm[1];
-      a.stats[2] = (double)a.rows;
+      for (int k = 0; k < a.stats_words; ++k) a.stats[k] = 0.0;
+      a.stats[a.stats_off + 0] = L.ts[1];
+      a.stats[a.stats_off + 1] = L.tm[1];
+      a.stats[a.stats_off + 2] = (double)a.rows;
     }
   }
 }
