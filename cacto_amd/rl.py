@@ -431,7 +431,7 @@ class RL_AC:
         inputs of the sequential loop (sample -> update -> priorities), so the result equals K
         update_rows + update_priorities_device calls (bit for bit when the collective's sums are
         order-independent, e.g. two ranks). Over RCCL the whole loop is one cacto_update_n_per_dp
-        call (the shard statistics all-gathered on the device per sample, the two-stream pipeline
+        call (the shard statistics exchanged on the device per sample, the two-stream pipeline
         with in-stream all-reduces)."""
         import torch.distributed as dist
         K, B = int(uniforms.shape[0]), int(uniforms.shape[1])

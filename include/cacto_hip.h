@@ -324,7 +324,8 @@ int cacto_update_n_dp(const cacto_sys* sys, const cacto_nets* nets, const cacto_
                       const double* storage_d, const int32_t* idx_d, int K, int B, void* workspace_d,
                       size_t workspace_bytes, void* stream);
 /* The same with PER (RL.py:122-137 on every rank's replay shard): per update this shard's (sum,
- * min, rows) all-gathered over the critic stream's communicator, the stratified sample with IS
+ * min, rows) exchanged over the critic stream's communicator (its row of a [world][3] table, the
+ * other rows zero, sum all-reduced — the all-gather of the statistics), the stratified sample with IS
  * weights against the union (cacto_per_sample_global), the update, then this shard's priority
  * update. Arguments as cacto_update_n_per. */
 int cacto_update_n_per_dp(const cacto_sys* sys, const cacto_nets* nets, const cacto_update_cfg* cfg,
